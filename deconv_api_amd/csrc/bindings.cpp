@@ -1,0 +1,233 @@
+// torch bindings for the gfx950 kernels. Host-only translation unit: validates shapes and
+// storage extents (an out-of-bounds kernel access can take down the whole GPU node), then
+// calls the raw launchers on the current HIP stream (so torch.cuda graphs capture them).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+
+// bytes from t.data_ptr() to the end of its storage
+int64_t avail_bytes(const Tensor& t) {
+  const int64_t total = (int64_t)t.storage().nbytes();
+  return total - t.storage_offset() * (int64_t)t.element_size();
+}
+
+void need(const Tensor& t, int64_t bytes, const char* name) {
+  TORCH_CHECK(bytes <= avail_bytes(t), name, ": kernel would read/write ", bytes, " bytes but only ",
+              avail_bytes(t), " are available");
+}
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " launch failed with code ", rc);
+}
+
+// geom: N,H,W,C, OH,OW,OC,OCpad, KH,KW,stride,pad_h,pad_w, K,Kpad, M, relu,relu_in,accumulate,
+//       code_div, x_ld, mask_ld, out_ld
+void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
+          c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
+          int64_t epi) {
+  TORCH_CHECK(g.size() == 23, "conv: geometry vector must have 23 entries");
+  check_cuda(x, "x");
+  check_cuda(w, "w");
+  check_cuda(out, "out");
+  c10::hip::HIPGuard guard(x.device());
+  dv::ConvArgs a{};
+  a.N = (int)g[0]; a.H = (int)g[1]; a.W = (int)g[2]; a.C = (int)g[3];
+  a.OH = (int)g[4]; a.OW = (int)g[5]; a.OC = (int)g[6]; a.OCpad = (int)g[7];
+  a.KH = (int)g[8]; a.KW = (int)g[9]; a.stride = (int)g[10]; a.pad_h = (int)g[11]; a.pad_w = (int)g[12];
+  a.K = (int)g[13]; a.Kpad = (int)g[14]; a.M = (int)g[15];
+  a.relu = (int)g[16]; a.relu_in = (int)g[17]; a.accumulate = (int)g[18];
+  a.code_div = (int)g[19]; a.x_ld = g[20]; a.mask_ld = g[21]; a.out_ld = g[22];
+
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv: x, w must be bf16");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == (int64_t)a.OCpad * a.Kpad, "conv: w must be [OCpad, Kpad]");
+  TORCH_CHECK(a.K == a.KH * a.KW * a.C && a.Kpad >= a.K && a.Kpad % 64 == 0, "conv: bad K/Kpad");
+  TORCH_CHECK(a.C % 8 == 0 && a.x_ld % 8 == 0 && a.x_ld >= a.C, "conv: C and x_ld must be multiples of 8");
+  TORCH_CHECK(a.M == a.N * a.OH * a.OW && a.M > 0, "conv: M must be N*OH*OW");
+  TORCH_CHECK(a.OC <= a.OCpad && a.stride >= 1 && a.code_div >= 1, "conv: bad OC/stride/code_div");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "conv: x and w must be 16-byte aligned");
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.w = reinterpret_cast<const uint16_t*>(w.data_ptr());
+
+  // input extent
+  int64_t in_pix = (int64_t)a.N * a.H * a.W;
+  if (amode == dv::CONV_A_UNPOOL) {
+    TORCH_CHECK(a.H % 2 == 0 && a.W % 2 == 0, "conv unpool: H, W must be even");
+    in_pix = (int64_t)a.N * (a.H / 2) * (a.W / 2);
+    TORCH_CHECK(code.has_value(), "conv unpool: code required");
+    check_cuda(*code, "code");
+    TORCH_CHECK(code->scalar_type() == at::kByte, "code must be uint8");
+    TORCH_CHECK(a.N % a.code_div == 0, "conv unpool: N % code_div");
+    need(*code, (int64_t)(a.N / a.code_div) * (a.H / 2) * (a.W / 2) * a.C, "code");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(code->data_ptr()) % 8 == 0, "code must be 8-byte aligned");
+    a.code = reinterpret_cast<const uint8_t*>(code->data_ptr());
+  }
+  need(x, ((in_pix - 1) * a.x_ld + a.C) * 2, "x");
+  if (mask.has_value()) {
+    check_cuda(*mask, "mask");
+    TORCH_CHECK(mask->scalar_type() == at::kBFloat16 && a.mask_ld % 8 == 0, "mask must be bf16, ld%8");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(mask->data_ptr()) % 16 == 0, "mask must be 16-byte aligned");
+    need(*mask, ((in_pix - 1) * a.mask_ld + a.C) * 2, "mask");
+    a.mask = reinterpret_cast<const uint16_t*>(mask->data_ptr());
+  }
+  if (bias.has_value()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= a.OCpad, "bias must be fp32 [OCpad]");
+    a.bias = bias->data_ptr<float>();
+  }
+  // output extent
+  int64_t out_rows = a.M;
+  if (epi == dv::CONV_E_POOL) {
+    TORCH_CHECK(a.OH % 2 == 0 && a.OW % 2 == 0, "conv pool: OH, OW must be even");
+    out_rows = a.M / 4;
+    TORCH_CHECK(out_code.has_value(), "conv pool: out_code required");
+    check_cuda(*out_code, "out_code");
+    TORCH_CHECK(out_code->scalar_type() == at::kByte, "out_code must be uint8");
+    need(*out_code, out_rows * a.OC, "out_code");
+    a.out_code = reinterpret_cast<uint8_t*>(out_code->data_ptr());
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16, "pool out must be bf16");
+  } else if (epi == dv::CONV_E_F32) {
+    TORCH_CHECK(out.scalar_type() == at::kFloat, "f32 epilogue needs fp32 out");
+  } else {
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16, "bf16 epilogue needs bf16 out");
+  }
+  need(out, ((out_rows - 1) * a.out_ld + a.OC) * (int64_t)out.element_size(), "out");
+  a.out = out.data_ptr();
+  check_rc(dv::conv_igemm_launch(a, (int)amode, (int)epi, cur_stream()), "conv_igemm");
+}
+
+void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
+  check_cuda(x, "x");
+  c10::hip::HIPGuard guard(x.device());
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "channel_sum: x bf16 contiguous");
+  TORCH_CHECK(sums.scalar_type() == at::kFloat && sums.is_contiguous(), "channel_sum: sums fp32");
+  need(x, N * HW * C * 2, "x");
+  need(sums, N * C * 4, "sums");
+  check_rc(dv::channel_sum_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()), sums.data_ptr<float>(), (int)N,
+                                  (int)HW, (int)C, cur_stream()),
+           "channel_sum");
+}
+
+void topk_pos(Tensor v, Tensor idx, Tensor val, int64_t k) {
+  check_cuda(v, "v");
+  c10::hip::HIPGuard guard(v.device());
+  TORCH_CHECK(v.dim() == 2 && v.scalar_type() == at::kFloat && v.is_contiguous(), "topk: v [N, C] fp32");
+  const int64_t N = v.size(0), C = v.size(1);
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.numel() == N * k, "topk: idx [N, k] int32");
+  TORCH_CHECK(val.scalar_type() == at::kFloat && val.is_contiguous() && val.numel() == N * k, "topk: val [N, k] fp32");
+  check_rc(dv::topk_pos_launch(v.data_ptr<float>(), idx.data_ptr<int>(), val.data_ptr<float>(), (int)N, (int)C, (int)k,
+                               cur_stream()),
+           "topk_pos");
+}
+
+void seed_deconv3x3(Tensor S, Tensor f, Tensor wt, Tensor out) {
+  check_cuda(S, "S");
+  c10::hip::HIPGuard guard(S.device());
+  TORCH_CHECK(S.dim() == 3 && S.scalar_type() == at::kFloat && S.is_contiguous(), "seed: S [B,H,W] fp32");
+  const int64_t B = S.size(0), H = S.size(1), W = S.size(2);
+  TORCH_CHECK(f.scalar_type() == at::kInt && f.numel() == B && f.is_contiguous(), "seed: f [B] int32");
+  TORCH_CHECK(wt.dim() == 4 && wt.size(1) == 3 && wt.size(2) == 3 && wt.scalar_type() == at::kBFloat16 &&
+                  wt.is_contiguous(),
+              "seed: wt [F,3,3,Cin] bf16");
+  const int64_t Cin = wt.size(3);
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == B * H * W * Cin,
+              "seed: out [B,H,W,Cin] bf16");
+  // f values are validated on the host side (ops layer clamps to [-1, F))
+  check_rc(dv::seed_deconv3x3_launch(S.data_ptr<float>(), f.data_ptr<int>(),
+                                     reinterpret_cast<const uint16_t*>(wt.data_ptr()),
+                                     reinterpret_cast<uint16_t*>(out.data_ptr()), (int)B, (int)H, (int)W, (int)Cin,
+                                     cur_stream()),
+           "seed_deconv3x3");
+}
+
+void deprocess_mosaic(Tensor recon, Tensor out, int64_t tiles, bool reverse) {
+  check_cuda(recon, "recon");
+  c10::hip::HIPGuard guard(recon.device());
+  TORCH_CHECK(recon.dim() == 4 && recon.size(3) == 3 && recon.scalar_type() == at::kFloat && recon.is_contiguous(),
+              "deprocess: recon [B*tiles, H, W, 3] fp32");
+  const int64_t BT = recon.size(0), H = recon.size(1), W = recon.size(2);
+  TORCH_CHECK(tiles >= 1 && tiles <= 4 && BT % tiles == 0, "deprocess: tiles");
+  const int64_t B = BT / tiles;
+  const int64_t rows = (tiles + 1) / 2;
+  TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.numel() == B * rows * H * 2 * W * 3,
+              "deprocess: out [B, rows*H, 2*W, 3] u8");
+  check_rc(dv::deprocess_mosaic_launch(recon.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)B, (int)H, (int)W,
+                                       (int)tiles, reverse ? 1 : 0, cur_stream()),
+           "deprocess_mosaic");
+}
+
+void resize_preprocess(Tensor img, Tensor out, int64_t mode) {
+  check_cuda(img, "img");
+  c10::hip::HIPGuard guard(img.device());
+  TORCH_CHECK(img.dim() == 4 && img.size(3) == 3 && img.scalar_type() == at::kByte && img.is_contiguous(),
+              "resize_preprocess: img [B, H, W, 3] u8");
+  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.size(0) == img.size(0),
+              "resize_preprocess: out [B, OH, OW, Cpad] bf16");
+  const int64_t B = img.size(0), Hs = img.size(1), Ws = img.size(2), OH = out.size(1), OW = out.size(2),
+                Cp = out.size(3);
+  if (mode == 1) TORCH_CHECK(Hs == 2 * OH && Ws == 2 * OW, "area mode needs exact 2x");
+  if (mode == 2) TORCH_CHECK(Hs == OH && Ws == OW, "copy mode needs equal size");
+  TORCH_CHECK(Cp >= 3 && (Cp != 8 || reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0), "resize_preprocess: Cpad");
+  check_rc(dv::resize_preprocess_launch(img.data_ptr<uint8_t>(), (int)B, (int)Hs, (int)Ws,
+                                        reinterpret_cast<uint16_t*>(out.data_ptr()), (int)OH, (int)OW, (int)Cp,
+                                        (int)mode, cur_stream()),
+           "resize_preprocess");
+}
+
+void maxpool2x2(Tensor x, Tensor out, Tensor code) {
+  check_cuda(x, "x");
+  c10::hip::HIPGuard guard(x.device());
+  TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "maxpool: x NHWC bf16");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == N * (H / 2) * (W / 2) * C,
+              "maxpool: out");
+  TORCH_CHECK(code.scalar_type() == at::kByte && code.is_contiguous() && code.numel() == out.numel(), "maxpool: code");
+  check_rc(dv::maxpool2x2_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                 reinterpret_cast<uint16_t*>(out.data_ptr()), code.data_ptr<uint8_t>(), (int)N, (int)H,
+                                 (int)W, (int)C, cur_stream()),
+           "maxpool2x2");
+}
+
+void unpool2x2(Tensor p, Tensor code, Tensor out, int64_t code_div, bool relu) {
+  check_cuda(p, "p");
+  c10::hip::HIPGuard guard(p.device());
+  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16 && out.is_contiguous(), "unpool: out NHWC bf16");
+  const int64_t N = out.size(0), H = out.size(1), W = out.size(2), C = out.size(3);
+  TORCH_CHECK(p.scalar_type() == at::kBFloat16 && p.is_contiguous() && p.numel() == N * (H / 2) * (W / 2) * C,
+              "unpool: p");
+  TORCH_CHECK(code_div >= 1 && N % code_div == 0, "unpool: code_div");
+  TORCH_CHECK(code.scalar_type() == at::kByte && code.is_contiguous() && code.numel() == p.numel() / code_div,
+              "unpool: code");
+  check_rc(dv::unpool2x2_launch(reinterpret_cast<const uint16_t*>(p.data_ptr()), code.data_ptr<uint8_t>(),
+                                reinterpret_cast<uint16_t*>(out.data_ptr()), (int)N, (int)H, (int)W, (int)C,
+                                (int)code_div, relu ? 1 : 0, cur_stream()),
+           "unpool2x2");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "deconv_api_amd gfx950 (MI355X) HIP kernels";
+  m.def("conv", &conv, "MFMA implicit-GEMM conv (fwd / unpool-gather / transposed; bf16/pool/f32 epilogues)");
+  m.def("channel_sum", &channel_sum);
+  m.def("topk_pos", &topk_pos);
+  m.def("seed_deconv3x3", &seed_deconv3x3);
+  m.def("deprocess_mosaic", &deprocess_mosaic);
+  m.def("resize_preprocess", &resize_preprocess);
+  m.def("maxpool2x2", &maxpool2x2);
+  m.def("unpool2x2", &unpool2x2);
+  m.attr("ARCH") = "gfx950";
+}

@@ -1,0 +1,67 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of deconv_api_amd.
+//
+// Conventions used by every kernel in this directory:
+//   * activations are NHWC, bf16 stored as raw uint16_t bits, fp32 accumulation;
+//   * a wavefront is 64 lanes (hard-coded, never warpSize);
+//   * launchers are plain C++ functions taking raw pointers + a hipStream_t so the
+//     torch binding layer (bindings.cpp) stays out of the device compile.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dv {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // plain cast: hipcc emits v_cvt_pk_bf16_f32 (RNE, NaN preserving) on gfx950
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// bf16 lane predicates on a packed pair (bits of two bf16 values in one u32)
+__device__ __forceinline__ uint32_t relu_bf2(uint32_t v) {
+  uint32_t lo = (v & 0x8000u) ? 0u : (v & 0xFFFFu);
+  uint32_t hi = (v & 0x80000000u) ? 0u : (v & 0xFFFF0000u);
+  return lo | hi;
+}
+// keep elements of v where the matching element of m is > 0
+__device__ __forceinline__ uint32_t mask_pos_bf2(uint32_t v, uint32_t m) {
+  uint32_t mlo = m & 0xFFFFu, mhi = m >> 16;
+  uint32_t lo = (mlo != 0u && !(mlo & 0x8000u)) ? (v & 0xFFFFu) : 0u;
+  uint32_t hi = (mhi != 0u && !(mhi & 0x8000u)) ? (v & 0xFFFF0000u) : 0u;
+  return lo | hi;
+}
+
+// Bijective XCD-aware workgroup remap (MI355X: 8 XCDs, consecutive dispatch ids go to
+// different XCDs). After the remap logically-adjacent tiles share an XCD (and its L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace dv
+
+#define DV_HIP_CHECK(expr)                                                     \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) return (int)_e;                                      \
+  } while (0)

@@ -1,0 +1,64 @@
+// Host-visible launcher declarations for the gfx950 kernels.
+// Included by the HIP translation units and by bindings.cpp (host-only).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace dv {
+
+// A-operand (implicit-GEMM gather) modes of the conv kernel.
+enum ConvAMode : int {
+  CONV_A_FWD = 0,        // x[n][oh*s-p+kh][ow*s-p+kw][c]
+  CONV_A_UNPOOL = 1,     // max-unpool gather: x is pooled (H/2 x W/2), switch codes select
+  CONV_A_TRANSPOSE = 2,  // transposed conv (dgrad of a strided conv): ih=(oh+p-kh)/s when divisible
+};
+// Epilogues.
+enum ConvEpi : int {
+  CONV_E_BF16 = 0,  // (+bias)(ReLU)(+=out) -> bf16
+  CONV_E_POOL = 1,  // (+bias)(ReLU) -> fused 2x2/s2 max-pool, bf16 pooled + uint8 switch code
+  CONV_E_F32 = 2,   // (+bias)(ReLU)(+=out) -> fp32
+};
+
+struct ConvArgs {
+  const uint16_t* x;      // NHWC bf16 input (pooled map in UNPOOL mode, dy in TRANSPOSE mode)
+  long long x_ld;         // elements between consecutive pixels of x (>= C; concat slices)
+  const uint16_t* mask;   // optional: zero A elements where mask <= 0 (backward through ReLU)
+  long long mask_ld;
+  const uint8_t* code;    // UNPOOL: switch codes [N/code_div][H/2][W/2][C]
+  int code_div;
+  const uint16_t* w;      // packed weights [OCpad][Kpad] bf16, K index = (kh*KW+kw)*C + c
+  const float* bias;      // [OCpad] fp32 or nullptr
+  void* out;              // bf16 or fp32 output, row stride out_ld elements
+  long long out_ld;
+  uint8_t* out_code;      // POOL: switch codes [M/4][OC]
+  int N, H, W, C;         // conv input geometry (UNPOOL: the unpooled H, W)
+  int OH, OW, OC, OCpad;
+  int KH, KW, stride, pad_h, pad_w;
+  int K, Kpad;
+  int M;                  // GEMM rows = N*OH*OW
+  int relu, relu_in, accumulate;
+};
+
+int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
+
+// ---- misc kernels (misc.hip) ----
+// per-(image, channel) sums of a NHWC bf16 tensor: sums[n][c] = sum_{hw} x[n][hw][c]
+int channel_sum_launch(const uint16_t* x, float* sums, int N, int HW, int C, hipStream_t s);
+// per-row stable top-k of positive values: idx[n][k] (-1 when fewer than k positives)
+int topk_pos_launch(const float* v, int* idx, float* val, int N, int C, int k, hipStream_t s);
+// one-channel seeded deconv: out[b][h][w][ci] = relu(sum_taps S[b][h+kh-1][w+kw-1] * wt[f_b][kh][kw][ci])
+int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint16_t* out,
+                          int B, int H, int W, int Cin, hipStream_t s);
+// fp32 recon [B*4][224][224][3] -> u8 mosaic [B][448][448][3] (channel-reversed), Keras deprocess
+int deprocess_mosaic_launch(const float* recon, uint8_t* out, int B, int H, int W, int tiles,
+                            int reverse_channels, hipStream_t s);
+// uint8 [B][Hs][Ws][3] RGB -> bf16 NHWC [B][OH][OW][Cpad]: cv2 INTER_LINEAR resize + caffe mean subtract
+int resize_preprocess_launch(const uint8_t* img, int B, int Hs, int Ws, uint16_t* out, int OH, int OW,
+                             int Cpad, int mode, hipStream_t s);
+// standalone 2x2/s2 max pool with switch codes, and its inverse (unpool scatter to full res)
+int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C,
+                      hipStream_t s);
+int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int N, int H, int W,
+                     int C, int code_div, int relu, hipStream_t s);
+
+}  // namespace dv

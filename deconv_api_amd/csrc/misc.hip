@@ -1,0 +1,394 @@
+// Small gfx950 kernels around the conv core: filter selection, seeded first deconv step,
+// mosaic deprocess, fused resize+preprocess, standalone pool/unpool.
+#include "common.h"
+#include "kernels.h"
+
+namespace dv {
+
+// ---------------------------------------------------------------------------------------
+// channel sums: sums[n][c] = sum_hw x[n][hw][c]   (reference: app/deepdream.py:369-380 sums
+// each filter's activation map; here per image, fp32 accumulate of the stored bf16 map).
+// One block per image; each thread owns 8 channels (one 16-B chunk) of a pixel group.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) channel_sum_kernel(const uint16_t* __restrict__ x,
+                                                          float* __restrict__ sums, int HW, int C) {
+  __shared__ float red[256 * 8];
+  const int n = blockIdx.x;
+  const int cpp = C >> 3;                // chunks per pixel
+  const int groups = 256 / cpp;          // pixel groups per block (C <= 2048)
+  const int tid = threadIdx.x;
+  const int chunk = tid % cpp, grp = tid / cpp;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (grp < groups) {
+    const uint16_t* base = x + (long long)n * HW * C + chunk * 8;
+    for (int p = grp; p < HW; p += groups) {
+      const uint4 v = *reinterpret_cast<const uint4*>(base + (long long)p * C);
+      acc[0] += bf2f(v.x & 0xFFFF); acc[1] += bf2f(v.x >> 16);
+      acc[2] += bf2f(v.y & 0xFFFF); acc[3] += bf2f(v.y >> 16);
+      acc[4] += bf2f(v.z & 0xFFFF); acc[5] += bf2f(v.z >> 16);
+      acc[6] += bf2f(v.w & 0xFFFF); acc[7] += bf2f(v.w >> 16);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[tid * 8 + e] = acc[e];
+  __syncthreads();
+  // deterministic ordered reduction over groups: thread t < C sums channel t
+  for (int c = tid; c < C; c += 256) {
+    const int ch = c >> 3, e = c & 7;
+    float s = 0.f;
+    for (int g = 0; g < groups; ++g) s += red[(g * cpp + ch) * 8 + e];
+    sums[(long long)n * C + c] = s;
+  }
+}
+
+int channel_sum_launch(const uint16_t* x, float* sums, int N, int HW, int C, hipStream_t s) {
+  if (C % 8 != 0 || C > 2048 || N <= 0) return -1;
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(N), dim3(256), 0, s, x, sums, HW, C);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Stable top-k of strictly positive values per row (reference: app/deepdream.py:369-380:
+// keep sums > 0, sort descending with ties in ascending index order, take `top`).
+// One wave per row; k rounds of (value desc, index asc) arg-max over the not-yet-taken set.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) topk_pos_kernel(const float* __restrict__ v, int* __restrict__ idx,
+                                                      float* __restrict__ val, int C, int k) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const float* r = v + (long long)row * C;
+  float last_v = INFINITY;
+  int last_i = -1;
+  for (int t = 0; t < k; ++t) {
+    float bv = 0.f;  // must be > 0 to count
+    int bi = -1;
+    for (int c = lane; c < C; c += 64) {
+      const float x = r[c];
+      const bool after = (x < last_v) || (x == last_v && c > last_i);
+      if (after && x > 0.f && (bi < 0 || x > bv || (x == bv && c < bi))) {
+        bv = x;
+        bi = c;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      const bool take = (oi >= 0) && (bi < 0 || ov > bv || (ov == bv && oi < bi));
+      if (take) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      idx[(long long)row * k + t] = bi;
+      val[(long long)row * k + t] = bi >= 0 ? bv : 0.f;
+    }
+    if (bi < 0) {
+      for (int u = t + 1 + lane; u < k; u += 64) {
+        idx[(long long)row * k + u] = -1;
+        val[(long long)row * k + u] = 0.f;
+      }
+      break;
+    }
+    last_v = bv;
+    last_i = bi;
+  }
+}
+
+int topk_pos_launch(const float* v, int* idx, float* val, int N, int C, int k, hipStream_t s) {
+  if (N <= 0 || k <= 0) return -1;
+  hipLaunchKernelGGL(topk_pos_kernel, dim3(N), dim3(64), 0, s, v, idx, val, C, k);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Seeded first deconv step from a one-channel signal (the selected filter's map):
+//   out[b][h][w][ci] = relu( sum_{kh,kw} S[b][h+kh-1][w+kw-1] * wt[f_b][kh][kw][ci] )
+// with wt[f][kh][kw][ci] = W[2-kh][2-kw][ci][f] (flipped, in/out swapped Keras kernel,
+// reference: app/deepdream.py:80-89). 1/C_out of the work of a dense conv-transpose.
+// f_b < 0 (fewer positive filters than requested) produces a zero map.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) seed_deconv3x3_kernel(const float* __restrict__ S,
+                                                             const int* __restrict__ f,
+                                                             const uint16_t* __restrict__ wt,
+                                                             uint16_t* __restrict__ out, int B, int H,
+                                                             int W, int Cin) {
+  const int cpp = Cin >> 3;
+  const long long total = (long long)B * H * W * cpp;
+  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total; g += (long long)gridDim.x * 256) {
+    const int chunk = (int)(g % cpp);
+    long long pix = g / cpp;
+    const int w = (int)(pix % W);
+    const int h = (int)((pix / W) % H);
+    const int b = (int)(pix / ((long long)W * H));
+    const int fb = f[b];
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (fb >= 0) {
+      const float* Sb = S + (long long)b * H * W;
+      const uint16_t* wf = wt + (long long)fb * 9 * Cin + chunk * 8;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int ih = h + kh - 1;
+        if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int iw = w + kw - 1;
+          if ((unsigned)iw >= (unsigned)W) continue;
+          const float sv = Sb[ih * W + iw];
+          if (sv == 0.f) continue;
+          const uint4 wv = *reinterpret_cast<const uint4*>(wf + (kh * 3 + kw) * Cin);
+          acc[0] += sv * bf2f(wv.x & 0xFFFF); acc[1] += sv * bf2f(wv.x >> 16);
+          acc[2] += sv * bf2f(wv.y & 0xFFFF); acc[3] += sv * bf2f(wv.y >> 16);
+          acc[4] += sv * bf2f(wv.z & 0xFFFF); acc[5] += sv * bf2f(wv.z >> 16);
+          acc[6] += sv * bf2f(wv.w & 0xFFFF); acc[7] += sv * bf2f(wv.w >> 16);
+        }
+      }
+    }
+    uint4 o;
+    o.x = pack_bf2(fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f));
+    o.y = pack_bf2(fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
+    o.z = pack_bf2(fmaxf(acc[4], 0.f), fmaxf(acc[5], 0.f));
+    o.w = pack_bf2(fmaxf(acc[6], 0.f), fmaxf(acc[7], 0.f));
+    *reinterpret_cast<uint4*>(out + pix * Cin + chunk * 8) = o;
+  }
+}
+
+int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint16_t* out, int B, int H,
+                          int W, int Cin, hipStream_t s) {
+  if (Cin % 8 != 0 || B <= 0) return -1;
+  const long long total = (long long)B * H * W * (Cin / 8);
+  const long long blocks = std::min<long long>((total + 255) / 256, 256LL * 16);
+  hipLaunchKernelGGL(seed_deconv3x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, S, f, wt, out, B, H,
+                     W, Cin);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Mosaic + deprocess (reference: app/main.py:67-72 + app/deepdream.py:483-498):
+// the `tiles` reconstructions of one image form a 2x2 mosaic that is normalized as a whole:
+//   x = (x - mean) / (std + 1e-7) * 0.1 + 0.5 ; clip[0,1] ; *255 ; clip ; truncate to u8.
+// Mean/std are population statistics over the whole mosaic (two passes, fp64 block sums).
+// reverse_channels writes channel c at slot 2-c (OpenCV BGR encoder semantics for an RGB
+// encoder). One 1024-thread block per image.
+// ---------------------------------------------------------------------------------------
+__device__ double block_sum_d(double v, double* sh) {
+  v = wave_sum_d(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x < 64) {
+    r = threadIdx.x < (blockDim.x >> 6) ? sh[threadIdx.x] : 0.0;
+    r = wave_sum_d(r);
+    if (threadIdx.x == 0) sh[0] = r;
+  }
+  __syncthreads();
+  r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(1024) deprocess_mosaic_kernel(const float* __restrict__ recon,
+                                                                uint8_t* __restrict__ out, int H, int W,
+                                                                int tiles, int reverse) {
+  __shared__ double sh[16];
+  const int b = blockIdx.x;
+  const long long per_tile = (long long)H * W * 3;
+  const long long total = per_tile * tiles;
+  const float* src = recon + (long long)b * total;
+  const float4* src4 = reinterpret_cast<const float4*>(src);
+  const long long n4 = total >> 2;  // total is a multiple of 4 (H*W*3*4)
+  double s = 0.0;
+  for (long long i = threadIdx.x; i < n4; i += 1024) {
+    const float4 v = src4[i];
+    s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+  }
+  const double mean_d = block_sum_d(s, sh) / (double)total;
+  const float mean = (float)mean_d;
+  double q = 0.0;
+  for (long long i = threadIdx.x; i < n4; i += 1024) {
+    const float4 v = src4[i];
+    const double a0 = v.x - mean, a1 = v.y - mean, a2 = v.z - mean, a3 = v.w - mean;
+    q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+  }
+  const float stdv = (float)sqrt(block_sum_d(q, sh) / (double)total);
+  const float denom = stdv + 1e-7f;
+  const int cols = 2;  // 2x2 mosaic, tile t at (t/2, t%2)
+  const int OW = W * cols;
+  uint8_t* o = out + (long long)b * (long long)H * ((tiles + cols - 1) / cols) * OW * 3;
+  for (long long i = threadIdx.x; i < total; i += 1024) {
+    const int t = (int)(i / per_tile);
+    const long long r = i - t * per_tile;
+    const int c = (int)(r % 3);
+    const long long p = r / 3;
+    const int x = (int)(p % W), y = (int)(p / W);
+    float v = src[i];
+    v = v - mean;
+    v = v / denom;
+    v = v * 0.1f;
+    v = v + 0.5f;
+    v = fminf(fmaxf(v, 0.f), 1.f);
+    v = v * 255.f;
+    v = fminf(fmaxf(v, 0.f), 255.f);
+    const int oy = (t / cols) * H + y, ox = (t % cols) * W + x;
+    const int oc = reverse ? 2 - c : c;
+    o[((long long)oy * OW + ox) * 3 + oc] = (uint8_t)v;  // truncation, like ndarray.astype
+  }
+}
+
+int deprocess_mosaic_launch(const float* recon, uint8_t* out, int B, int H, int W, int tiles, int reverse,
+                            hipStream_t s) {
+  if (B <= 0 || tiles <= 0 || tiles > 4) return -1;
+  hipLaunchKernelGGL(deprocess_mosaic_kernel, dim3(B), dim3(1024), 0, s, recon, out, H, W, tiles, reverse);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused resize + preprocess for one decoded RGB uint8 image (reference: app/main.py:53
+// cv2.resize(img,(224,224)) INTER_LINEAR, then :60-61 img_to_array + preprocess_input).
+// mode 0: OpenCV INTER_LINEAR fixed point (11-bit coefficients, half-pixel centres, edge
+//         clamp; vertical pass as OpenCV's SIMD path: ((S0>>4)*b0>>16 + (S1>>4)*b1>>16 + 2)>>2)
+// mode 1: OpenCV's exact-2x fast area path (INTER_LINEAR with integer scale 2 -> INTER_AREA)
+// mode 2: same size copy
+// Output slot c (c<3) = rgb[c] - mean[c], mean = (103.939, 116.779, 123.68): the RGB image
+// is fed in the slot order the reference's BGR->reverse produced.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void lin_coef(int d, double scale, int ssize, int& s0, int& s1, int& a0, int& a1) {
+  float fx = (float)((d + 0.5) * scale - 0.5);
+  int sx = (int)floorf(fx);
+  fx -= sx;
+  if (sx < 0) {
+    fx = 0.f;
+    sx = 0;
+  }
+  if (sx >= ssize - 1) {
+    fx = 0.f;
+    sx = ssize - 1;
+  }
+  s0 = sx;
+  s1 = sx + 1 < ssize ? sx + 1 : sx;
+  a0 = __float2int_rn((1.f - fx) * 2048.f);
+  a1 = __float2int_rn(fx * 2048.f);
+}
+
+__global__ void __launch_bounds__(256) resize_preprocess_kernel(const uint8_t* __restrict__ img_b, int Hs, int Ws,
+                                                                uint16_t* __restrict__ out_b, int OH, int OW,
+                                                                int Cpad, int mode) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= OH * OW) return;
+  const uint8_t* img = img_b + (long long)blockIdx.y * Hs * Ws * 3;
+  uint16_t* out = out_b + (long long)blockIdx.y * OH * OW * Cpad;
+  const int ox = p % OW, oy = p / OW;
+  int px[3];
+  if (mode == 2) {
+    for (int c = 0; c < 3; ++c) px[c] = img[((long long)oy * Ws + ox) * 3 + c];
+  } else if (mode == 1) {
+    const int sy = oy * 2, sx = ox * 2;
+    for (int c = 0; c < 3; ++c) {
+      const int s = img[((long long)sy * Ws + sx) * 3 + c] + img[((long long)sy * Ws + sx + 1) * 3 + c] +
+                    img[((long long)(sy + 1) * Ws + sx) * 3 + c] + img[((long long)(sy + 1) * Ws + sx + 1) * 3 + c];
+      px[c] = (s + 2) >> 2;
+    }
+  } else {
+    int x0, x1, a0, a1, y0, y1, b0, b1;
+    lin_coef(ox, (double)Ws / OW, Ws, x0, x1, a0, a1);
+    lin_coef(oy, (double)Hs / OH, Hs, y0, y1, b0, b1);
+    for (int c = 0; c < 3; ++c) {
+      const int r0 = img[((long long)y0 * Ws + x0) * 3 + c] * a0 + img[((long long)y0 * Ws + x1) * 3 + c] * a1;
+      const int r1 = img[((long long)y1 * Ws + x0) * 3 + c] * a0 + img[((long long)y1 * Ws + x1) * 3 + c] * a1;
+      const int t0 = ((r0 >> 4) * b0) >> 16;
+      const int t1 = ((r1 >> 4) * b1) >> 16;
+      int v = (t0 + t1 + 2) >> 2;
+      px[c] = v < 0 ? 0 : (v > 255 ? 255 : v);
+    }
+  }
+  const float mean[3] = {103.939f, 116.779f, 123.68f};
+  uint16_t* o = out + (long long)p * Cpad;
+  if (Cpad == 8) {  // one 16-B store per pixel
+    uint4 v;
+    v.x = pack_bf2((float)px[0] - mean[0], (float)px[1] - mean[1]);
+    v.y = (uint32_t)f2bf((float)px[2] - mean[2]);
+    v.z = 0u;
+    v.w = 0u;
+    *reinterpret_cast<uint4*>(o) = v;
+  } else {
+    for (int c = 0; c < Cpad; ++c) o[c] = c < 3 ? f2bf((float)px[c] - mean[c]) : (uint16_t)0;
+  }
+}
+
+int resize_preprocess_launch(const uint8_t* img, int B, int Hs, int Ws, uint16_t* out, int OH, int OW, int Cpad,
+                             int mode, hipStream_t s) {
+  if (Cpad < 3 || mode < 0 || mode > 2 || B <= 0) return -1;
+  hipLaunchKernelGGL(resize_preprocess_kernel, dim3((OH * OW + 255) / 256, B), dim3(256), 0, s, img, Hs, Ws, out,
+                     OH, OW, Cpad, mode);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Standalone 2x2/s2 max pool with first-max switch codes (reference: app/deepdream.py:152-188)
+// and max-unpool to full resolution (reference: app/deepdream.py:191-209). The hot paths fuse
+// both into the conv kernel; these serve pool-layer targets and tests.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) maxpool2x2_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out,
+                                                         uint8_t* __restrict__ code, int N, int H, int W, int C) {
+  const int PH = H >> 1, PW = W >> 1;
+  const long long total = (long long)N * PH * PW * C;
+  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total; g += (long long)gridDim.x * 256) {
+    const int c = (int)(g % C);
+    long long pix = g / C;
+    const int pw = (int)(pix % PW);
+    const int ph = (int)((pix / PW) % PH);
+    const long long n = pix / ((long long)PW * PH);
+    float best = -INFINITY;
+    int bc = 0;
+    for (int r = 0; r < 4; ++r) {
+      const int ih = 2 * ph + (r >> 1), iw = 2 * pw + (r & 1);
+      const float v = bf2f(x[((n * H + ih) * W + iw) * C + c]);
+      if (v > best) {
+        best = v;
+        bc = r;
+      }
+    }
+    out[g] = f2bf(best);
+    code[g] = (uint8_t)bc;
+  }
+}
+
+int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C, hipStream_t s) {
+  if ((H | W) & 1) return -1;
+  const long long total = (long long)N * (H / 2) * (W / 2) * C;
+  const long long blocks = std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(maxpool2x2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
+  return (int)hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) unpool2x2_kernel(const uint16_t* __restrict__ p, const uint8_t* __restrict__ code,
+                                                        uint16_t* __restrict__ out, int N, int H, int W, int C,
+                                                        int code_div, int relu) {
+  const int PH = H >> 1, PW = W >> 1;
+  const long long total = (long long)N * H * W * C;
+  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total; g += (long long)gridDim.x * 256) {
+    const int c = (int)(g % C);
+    long long pix = g / C;
+    const int w = (int)(pix % W);
+    const int h = (int)((pix / W) % H);
+    const long long n = pix / ((long long)W * H);
+    const long long q = ((n * PH + (h >> 1)) * PW + (w >> 1)) * C + c;
+    const long long qc = (((n / code_div) * PH + (h >> 1)) * PW + (w >> 1)) * C + c;
+    uint16_t v = code[qc] == (((h & 1) << 1) | (w & 1)) ? p[q] : (uint16_t)0;
+    if (relu && (v & 0x8000u)) v = 0;
+    out[g] = v;
+  }
+}
+
+int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int N, int H, int W, int C, int code_div,
+                     int relu, hipStream_t s) {
+  if (((H | W) & 1) || code_div <= 0) return -1;
+  const long long total = (long long)N * H * W * C;
+  const long long blocks = std::min<long long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(unpool2x2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, code, out, N, H, W, C, code_div,
+                     relu);
+  return (int)hipGetLastError();
+}
+
+}  // namespace dv

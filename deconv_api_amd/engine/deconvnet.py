@@ -1,0 +1,265 @@
+"""Batched Zeiler-Fergus deconvnet engine on VGG16 (reference: app/deepdream.py:383-476).
+
+What the reference does per request: stack D-layers up to the target (:401-423), run every
+``up`` (:425-428), then for every named layer <= target and each of its top-8 filters run a full
+``down`` chain to the input (:430-474). The HTTP handler then keeps only the first four
+reconstructions of the target layer (app/main.py:67-69).
+
+What this engine does (same outputs, MI355X-shaped):
+  * forward in bf16 NHWC through the MFMA implicit-GEMM conv; every 2x2 max-pool that precedes
+    the target is fused into its conv's epilogue and leaves only a uint8 switch code per pooled
+    element (the backward pass needs switches + weights, never the forward activations);
+  * per-image top-k filter selection on device (channel sums -> stable positive top-k);
+  * the B images x K filters backward chains are folded into one batch of B*K signals that
+    share their image's switch codes (code_div = K); the first step from the one-channel seed
+    is a 9-tap stencil, every later conv-down is the same MFMA kernel with the unpool gather
+    fused into its A-operand load and ReLU on both sides;
+  * the final conv-down writes fp32 reconstructions that the mosaic/deprocess kernel turns into
+    the 2x2 uint8 mosaic of app/main.py:67-72.
+``visualize_all_layers`` keeps the reference's library API (all layers, top-8, across-batch
+filter sums) on top of the same machinery.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import ops
+from ..models.vgg16 import VGG16Runtime, LayerSpec
+
+VALID_MODES = ("all", "max")
+
+
+class UnknownLayerError(KeyError):
+    pass
+
+
+@dataclass
+class ForwardState:
+    target: str
+    out: torch.Tensor  # target output: [B, H, W, C] or [B, units]
+    codes: Dict[str, torch.Tensor] = field(default_factory=dict)  # pool name -> switch codes
+    outputs: Dict[str, torch.Tensor] = field(default_factory=dict)  # kept named outputs (all-layers mode)
+
+
+@dataclass
+class DeconvResult:
+    recon: torch.Tensor  # fp32 [B, K, 224, 224, 3]
+    filters: torch.Tensor  # int32 [B, K] (-1 = no positive filter: zero reconstruction)
+    sums: torch.Tensor  # fp32 [B, K] selection scores
+    mosaic: Optional[torch.Tensor] = None  # u8 [B, 448, 448, 3] (K == 4)
+
+
+class DeconvNet:
+    def __init__(self, rt: VGG16Runtime):
+        self.rt = rt
+        self.specs: List[LayerSpec] = rt.specs
+        self.names = [s.name for s in self.specs]
+
+    # ------------------------------------------------------------------ helpers
+    def _check_layer(self, name: str) -> int:
+        if name not in self.names:
+            raise UnknownLayerError(f"unknown layer {name!r}; valid: {self.names[1:]}")
+        if name == "input_1":
+            raise UnknownLayerError("input_1 has no filters to visualize")
+        i = self.names.index(name)
+        if self.specs[i].kind == "dense" and name not in self.rt.dense:
+            raise UnknownLayerError(f"{name!r} needs the classifier head (include_top=True)")
+        return i
+
+    def _dense_up(self, x: torch.Tensor, name: str) -> torch.Tensor:
+        d = self.rt.dense[name]
+        y = torch.matmul(x.to(d.w.dtype), d.w).float() + d.b
+        if d.spec.activation == "relu":
+            y = y.clamp_min(0)
+        else:
+            y = torch.softmax(y, dim=-1)
+        return y.to(self.rt.dtype if x.is_cuda else torch.float32)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, target: str, fuse_pools: bool = True,
+                keep_all: bool = False) -> ForwardState:
+        """x: preprocessed [B, 224, 224, 8] (bf16 on device). Runs ``up`` through ``target``."""
+        ti = self._check_layer(target)
+        seq = self.specs[1: ti + 1]
+        st = ForwardState(target, x)
+        i = 0
+        while i < len(seq):
+            s = seq[i]
+            if s.kind == "conv":
+                cl = self.rt.convs[s.name]
+                nxt = seq[i + 1] if i + 1 < len(seq) else None
+                if fuse_pools and not keep_all and nxt is not None and nxt.kind == "pool":
+                    x, code = ops.conv2d(x, cl.fwd, relu=True, epilogue="pool")
+                    st.codes[nxt.name] = code
+                    i += 2
+                    continue
+                x = ops.conv2d(x, cl.fwd, relu=True)
+            elif s.kind == "pool":
+                x, code = ops.maxpool2x2(x)
+                st.codes[s.name] = code
+            elif s.kind == "flatten":
+                x = x.reshape(x.shape[0], -1)
+            elif s.kind == "dense":
+                x = self._dense_up(x, s.name)
+            if keep_all:
+                st.outputs[s.name] = x
+            i += 1
+        st.out = x
+        return st
+
+    # ------------------------------------------------------------------ selection
+    @staticmethod
+    def select_filters(out: torch.Tensor, k: int, batch_topk: str = "per_image"):
+        """Top-k positive filters (app/deepdream.py:369-380). Returns idx [B, k], val [B, k]."""
+        B = out.shape[0]
+        sums = ops.channel_sum(out) if out.dim() == 4 else out.float()
+        if batch_topk == "global":
+            g = sums.sum(dim=0, keepdim=True)
+            idx, val = ops.topk_positive(g, k)
+            return idx.expand(B, k).contiguous(), val.expand(B, k).contiguous()
+        return ops.topk_positive(sums, k)
+
+    # ------------------------------------------------------------------ backward
+    def _seed_map(self, out4: torch.Tensor, idx: torch.Tensor, mode: str, batch_topk: str) -> torch.Tensor:
+        """One-channel seed maps S [B*K, H, W] fp32 from the target output (app/deepdream.py:450-465)."""
+        B, H, W, C = out4.shape
+        K = idx.shape[1]
+        fi = idx.long().clamp_min(0)  # [B, K]
+        o = out4.float().permute(0, 3, 1, 2)  # [B, C, H, W]
+        S = torch.gather(o, 1, fi.view(B, K, 1, 1).expand(B, K, H, W))  # [B, K, H, W]
+        if mode == "max":
+            if batch_topk == "global":
+                m = S.amax(dim=(0, 2, 3), keepdim=True)
+            else:
+                m = S.amax(dim=(2, 3), keepdim=True)
+            S = S * (S == m)
+        S = S * (idx >= 0).view(B, K, 1, 1)
+        return S.reshape(B * K, H, W).contiguous()
+
+    def backward(self, st: ForwardState, idx: torch.Tensor, mode: str = "all",
+                 batch_topk: str = "per_image", layer: Optional[str] = None) -> torch.Tensor:
+        """B*K deconv chains from ``layer`` (default: the forward target) to the input.
+        Returns fp32 reconstructions [B, K, 224, 224, 3]."""
+        if mode not in VALID_MODES:
+            raise ValueError(f"Illegal visualize mode {mode!r}; use 'all' or 'max'")
+        layer = layer or st.target
+        li = self.names.index(layer)
+        spec = self.specs[li]
+        B, K = idx.shape
+        dev = idx.device
+        out = st.outputs.get(layer, st.out) if layer != st.target else st.out
+        f = idx.reshape(B * K).to(torch.int32)
+        d: Optional[torch.Tensor] = None
+        pending_code: Optional[torch.Tensor] = None
+        j = li  # index of the layer whose down is applied next
+        if spec.kind == "conv":
+            S = self._seed_map(out, idx, mode, batch_topk)
+            d = ops.seed_deconv3x3(S, f, self.rt.convs[layer].seed_wt)
+            j = li - 1
+        elif spec.kind == "pool":
+            # seed at pooled resolution, unpooled with this pool's switches, then the conv below
+            S = self._seed_map(out, idx, mode, batch_topk)  # [BK, PH, PW]
+            code = st.codes[layer]  # [B, PH, PW, C]
+            fi = idx.long().clamp_min(0)
+            cf = torch.gather(code.permute(0, 3, 1, 2), 1,
+                              fi.view(B, K, 1, 1).expand(B, K, *code.shape[1:3]))  # [B, K, PH, PW]
+            cf = cf.reshape(B * K, *code.shape[1:3])
+            Su = ops.unpool_ref(S.unsqueeze(-1), cf.unsqueeze(-1)).squeeze(-1).clamp_min(0).contiguous()
+            conv_name = self.specs[li - 1].name
+            d = ops.seed_deconv3x3(Su, f, self.rt.convs[conv_name].seed_wt)
+            j = li - 2
+        else:
+            # dense / flatten target: one-hot (unit f) seeds, then linear downs
+            units = out.shape[1]
+            v = torch.gather(out.float(), 1, idx.long().clamp_min(0))  # [B, K]
+            if mode == "max" and batch_topk == "global":
+                # the reference's max runs over the batch axis of output[:, f] (:454-457)
+                v = v * (v == v.amax(dim=0, keepdim=True))
+            v = v * (idx >= 0)
+            seed = torch.zeros(B * K, units, device=dev, dtype=torch.float32)
+            seed.scatter_(1, idx.reshape(B * K, 1).long().clamp_min(0), v.reshape(B * K, 1))
+            d = seed
+            j = li
+            while self.specs[j].kind == "dense":
+                dl = self.rt.dense[self.specs[j].name]
+                d = torch.matmul(d.to(dl.wt.dtype), dl.wt).float()
+                j -= 1
+                if self.specs[j].kind == "dense":
+                    d = d.clamp_min(0)  # the lower dense layer's activation.down (ReLU)
+            assert self.specs[j].kind == "flatten"
+            fs = self.specs[j]
+            d = d.reshape(B * K, fs.out_hw, fs.out_hw, fs.cin).to(self.rt.dtype if dev.type == "cuda" else torch.float32)
+            pending_code = st.codes["block5_pool"]
+            j -= 2  # skip flatten and block5_pool (its unpool is fused into block5_conv3's down)
+        # ---- conv / pool downs to the input ----
+        recon = None
+        while j >= 1:
+            s = self.specs[j]
+            if s.kind == "pool":
+                pending_code = st.codes[s.name]
+                j -= 1
+                continue
+            assert s.kind == "conv", s
+            cl = self.rt.convs[s.name]
+            last = j == 1
+            kw = dict(relu=True, relu_in=True, epilogue="f32" if last else "bf16", use_bias=False)
+            if pending_code is not None:
+                d = ops.conv2d(d, cl.dec, in_mode="unpool", code=pending_code, code_div=K, **kw)
+                pending_code = None
+            else:
+                d = ops.conv2d(d, cl.dec, **kw)
+            if last:
+                recon = d
+            j -= 1
+        if recon is None:  # target was block1_conv1: the seed step already produced the image
+            recon = d[..., :3].float()
+        return recon.reshape(B, K, *recon.shape[1:])
+
+    # ------------------------------------------------------------------ one call
+    def run(self, x: torch.Tensor, layer: str, k: int = 4, mode: str = "all",
+            batch_topk: str = "per_image", mosaic: bool = True) -> DeconvResult:
+        if mode not in VALID_MODES:
+            raise ValueError(f"Illegal visualize mode {mode!r}; use 'all' or 'max'")
+        st = self.forward(x, layer)
+        idx, val = self.select_filters(st.out, k, batch_topk)
+        recon = self.backward(st, idx, mode, batch_topk)
+        res = DeconvResult(recon, idx, val)
+        if mosaic and k == 4:
+            B = recon.shape[0]
+            res.mosaic = ops.deprocess_mosaic(recon.reshape(B * 4, *recon.shape[2:]).contiguous(), 4, True)
+        return res
+
+
+def visualize_all_layers(engine: DeconvNet, data: torch.Tensor, layer_name: str = "predictions",
+                         visualize_mode: str = "all", *, all_layers: bool = True, top: int = 8,
+                         batch_topk: str = "global") -> Dict[str, List]:
+    """Library-parity API of app/deepdream.py:383-476.
+
+    Returns ``{layer: [recon, ...]}`` with one squeezed reconstruction per selected filter (at most
+    ``top``; filters with non-positive sums are dropped as in find_top_filters). With
+    ``all_layers=True`` every conv/pool/flatten/dense layer <= ``layer_name`` is visualized, as
+    the reference does; ``False`` visualizes only the target. Illegal modes raise ValueError
+    (the reference calls sys.exit, :458-460)."""
+    if visualize_mode not in VALID_MODES:
+        raise ValueError(f"Illegal visualize mode {visualize_mode!r}")
+    st = engine.forward(data, layer_name, fuse_pools=not all_layers, keep_all=all_layers)
+    ti = engine.names.index(layer_name)
+    layers = [s.name for s in engine.specs[1: ti + 1] if s.kind in ("conv", "pool", "flatten", "dense")]
+    if not all_layers:
+        layers = [layer_name]
+    result: Dict[str, List] = {}
+    for name in reversed(layers):
+        out = st.outputs.get(name, st.out) if all_layers else st.out
+        sub = ForwardState(name, out, st.codes, st.outputs)
+        idx, val = engine.select_filters(out, top, batch_topk)
+        nsel = int((idx[0] >= 0).sum().item()) if batch_topk == "global" else top
+        recon = engine.backward(sub, idx, visualize_mode, batch_topk, layer=name)
+        lst = []
+        for kk in range(nsel):
+            r = recon[:, kk]
+            lst.append(r.squeeze(0).cpu().numpy() if r.shape[0] == 1 else r.cpu().numpy())
+        result[name] = lst
+    return result

@@ -1,0 +1,271 @@
+"""Convolution op surface: packed weights + NHWC conv with fused prologues/epilogues.
+
+Device tensors run the MFMA implicit-GEMM kernel in ``csrc/conv_igemm.hip``; CPU tensors run a
+PyTorch reference of exactly the same math (fp32 compute, output rounded to the input dtype),
+which is both the CPU execution path and the oracle the GPU tests compare against.
+
+Reference semantics being implemented (rashanarshad/deconv_api):
+  * conv up   = conv3x3 'same' + bias + ReLU           (app/deepdream.py:71-76, 99)
+  * conv down = ReLU(conv(ReLU(y), flip(W)^T)), no bias (app/deepdream.py:78-89, 110, 260)
+  * pool up   = 2x2 max with first-max switch          (app/deepdream.py:152-188)
+  * pool down = switch-masked nearest upsampling       (app/deepdream.py:191-209)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+AMODE = {"plain": 0, "unpool": 1, "transpose": 2}
+EPI = {"bf16": 0, "pool": 1, "f32": 2}
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def oc_pad(oc: int) -> int:
+    """Output-channel padding that selects the kernel's N tile (128 / 64 / 16)."""
+    if oc > 64 and (oc % 128 == 0 or oc > 256):
+        return _round_up(oc, 128)
+    if oc > 16:
+        return _round_up(oc, 64)
+    return 16
+
+
+@dataclass
+class ConvWeights:
+    """A conv in torch OIHW form plus its gfx950 GEMM packing.
+
+    ``w_oihw``: fp32 [OC, C, KH, KW] cross-correlation weights (C already padded to 8).
+    ``kind``: 'fwd' (x -> conv2d(x, w)) or 'transpose' (dy -> conv_transpose2d(dy, w), i.e. the
+    input-gradient of a strided conv whose forward weights are ``w``).
+    Packed device matrix: ``w_gemm[OCpad, Kpad]`` bf16 with K index ``(kh*KW + kw)*Cin + c``.
+    """
+
+    w_oihw: torch.Tensor
+    bias: Optional[torch.Tensor]
+    kind: str = "fwd"
+    w_gemm: Optional[torch.Tensor] = None
+    bias_pad: Optional[torch.Tensor] = None
+
+    @property
+    def KH(self) -> int:
+        return self.w_oihw.shape[2]
+
+    @property
+    def KW(self) -> int:
+        return self.w_oihw.shape[3]
+
+    @property
+    def cin(self) -> int:
+        """channels of the kernel's input tensor"""
+        return self.w_oihw.shape[1] if self.kind == "fwd" else self.w_oihw.shape[0]
+
+    @property
+    def cout(self) -> int:
+        return self.w_oihw.shape[0] if self.kind == "fwd" else self.w_oihw.shape[1]
+
+    @property
+    def K(self) -> int:
+        return self.KH * self.KW * self.cin
+
+    @property
+    def Kpad(self) -> int:
+        return _round_up(self.K, 64)
+
+    @property
+    def OCpad(self) -> int:
+        return oc_pad(self.cout)
+
+    def gemm_matrix(self) -> torch.Tensor:
+        """[OCpad, Kpad] fp32 GEMM B^T matrix (rows = output channels, K contiguous)."""
+        if self.kind == "fwd":
+            m = self.w_oihw.permute(0, 2, 3, 1)  # [OC, KH, KW, C]
+        else:
+            # transposed gather: out ci, K index (kh, kw, co) -> w[co, ci, kh, kw]
+            m = self.w_oihw.permute(1, 2, 3, 0)  # [C_fwd, KH, KW, OC_fwd]
+        m = m.reshape(self.cout, self.K).float()
+        out = torch.zeros(self.OCpad, self.Kpad, dtype=torch.float32)
+        out[: self.cout, : self.K] = m
+        return out
+
+    def to_device(self, device) -> "ConvWeights":
+        device = torch.device(device)
+        w_oihw = self.w_oihw.to(device)
+        bias = None if self.bias is None else self.bias.to(device)
+        cw = ConvWeights(w_oihw, bias, self.kind)
+        if device.type == "cuda":
+            cw.w_gemm = self.gemm_matrix().to(device=device, dtype=torch.bfloat16).contiguous()
+            if bias is not None:
+                bp = torch.zeros(self.OCpad, dtype=torch.float32)
+                bp[: self.cout] = self.bias.float().cpu()
+                cw.bias_pad = bp.to(device)
+        return cw
+
+
+def pad_channels_oihw(w: torch.Tensor, mult: int = 8) -> torch.Tensor:
+    """Zero-pad the input-channel dim (dim 1) of an OIHW weight to a multiple of ``mult``."""
+    c = w.shape[1]
+    cp = _round_up(c, mult)
+    if cp == c:
+        return w
+    out = torch.zeros(w.shape[0], cp, *w.shape[2:], dtype=w.dtype, device=w.device)
+    out[:, :c] = w
+    return out
+
+
+def deconv_weights(fwd: ConvWeights) -> ConvWeights:
+    """Deconvnet 'down' conv of a stride-1 'same' conv (reference app/deepdream.py:78-89):
+    kernel transposed in/out and flipped spatially, zero bias."""
+    assert fwd.kind == "fwd"
+    w = fwd.w_oihw.flip(2, 3).transpose(0, 1).contiguous()
+    return ConvWeights(pad_channels_oihw(w), None, "fwd")
+
+
+# ----------------------------------------------------------------------------------------
+# CPU / oracle helpers
+# ----------------------------------------------------------------------------------------
+
+def unpool_ref(p: torch.Tensor, code: torch.Tensor, code_div: int = 1) -> torch.Tensor:
+    """NHWC max-unpool: out[n, 2ph+dy, 2pw+dx, c] = p[n, ph, pw, c] if code == 2dy+dx."""
+    N, PH, PW, C = p.shape
+    if code_div > 1:
+        code = code.repeat_interleave(code_div, dim=0)
+    pos = torch.arange(4, device=p.device).view(1, 1, 1, 4, 1)
+    sel = code.long().unsqueeze(3) == pos  # [N, PH, PW, 4, C]
+    vals = p.unsqueeze(3) * sel.to(p.dtype)
+    vals = vals.view(N, PH, PW, 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, PH * 2, PW * 2, C)
+    return vals
+
+
+def maxpool_switch_ref(x: torch.Tensor):
+    """NHWC 2x2/s2 max-pool with first-max (row-major) switch code 0..3."""
+    N, H, W, C = x.shape
+    win = x.view(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4, C)
+    val, idx = win.max(dim=3)  # torch returns the first maximal index
+    # torch.max(dim) on CPU returns the first occurrence for ties; make it explicit anyway
+    first = (win == val.unsqueeze(3)).to(torch.int8).argmax(dim=3)
+    return val, first.to(torch.uint8)
+
+
+def _act_out(y: torch.Tensor, relu: bool, dtype) -> torch.Tensor:
+    if relu:
+        y = y.clamp_min(0)
+    return y
+
+
+def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu: bool = True,
+           relu_in: bool = False, in_mode: str = "plain", code: Optional[torch.Tensor] = None,
+           code_div: int = 1, mask: Optional[torch.Tensor] = None, epilogue: str = "bf16",
+           out: Optional[torch.Tensor] = None, accumulate: bool = False, out_hw=None,
+           use_bias: bool = True):
+    """NHWC convolution.
+
+    x: [N, H, W, C] (channel-slice views allowed: stride(3) == 1). For ``in_mode='unpool'`` x is
+    the pooled map [N, H/2, W/2, C] and ``code`` its switch codes ([N/code_div, H/2, W/2, C]).
+    epilogue 'pool' returns ``(pooled, code)``; otherwise the output tensor.
+    """
+    if pad is None:
+        pad = (cw.KH // 2, cw.KW // 2)
+    elif isinstance(pad, int):
+        pad = (pad, pad)
+    N = x.shape[0]
+    if in_mode == "unpool":
+        H, W = x.shape[1] * 2, x.shape[2] * 2
+    else:
+        H, W = x.shape[1], x.shape[2]
+    C = x.shape[3]
+    assert C == cw.cin, f"conv2d: input has {C} channels, weights expect {cw.cin}"
+    if in_mode == "transpose":
+        if out_hw is None:
+            out_hw = ((H - 1) * stride - 2 * pad[0] + cw.KH, (W - 1) * stride - 2 * pad[1] + cw.KW)
+        OH, OW = out_hw
+    else:
+        OH = (H + 2 * pad[0] - cw.KH) // stride + 1
+        OW = (W + 2 * pad[1] - cw.KW) // stride + 1
+    OC = cw.cout
+    if x.is_cuda:
+        return _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
+                           mask, epilogue, out, accumulate, use_bias)
+    return _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
+                       mask, epilogue, out, accumulate, use_bias)
+
+
+def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
+                epilogue, out, accumulate, use_bias):
+    dtype = x.dtype
+    xf = x.float()
+    if in_mode == "unpool":
+        xf = unpool_ref(xf, code, code_div)
+    if mask is not None:
+        xf = xf * (mask.float() > 0)
+    if relu_in:
+        xf = xf.clamp_min(0)
+    X = xf.permute(0, 3, 1, 2)
+    bias = cw.bias.float() if (use_bias and cw.bias is not None) else None
+    if in_mode == "transpose":
+        base_h = (H - 1) * stride - 2 * pad[0] + cw.KH
+        base_w = (W - 1) * stride - 2 * pad[1] + cw.KW
+        Y = F.conv_transpose2d(X, cw.w_oihw.float(), bias, stride=stride, padding=pad,
+                               output_padding=(OH - base_h, OW - base_w))
+    else:
+        Y = F.conv2d(X, cw.w_oihw.float(), bias, stride=stride, padding=pad)
+    y = Y.permute(0, 2, 3, 1)
+    if relu:
+        y = y.clamp_min(0)
+    if epilogue == "pool":
+        y = y.to(dtype).float()  # pool on stored-precision values, like the fused GPU epilogue
+        pv, pc = maxpool_switch_ref(y)
+        pv = pv.to(dtype).contiguous()
+        if out is not None:
+            out.copy_(pv)
+            pv = out
+        return pv, pc.contiguous()
+    odt = torch.float32 if epilogue == "f32" else dtype
+    if out is not None:
+        if accumulate:
+            y = y + out.float()
+        out.copy_(y.to(out.dtype))
+        return out
+    return y.to(odt).contiguous()
+
+
+def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
+                epilogue, out, accumulate, use_bias):
+    lib = native.lib()
+    assert x.dtype == torch.bfloat16 and x.stride(3) == 1, "conv2d(hip): x must be bf16 NHWC (channel stride 1)"
+    assert cw.w_gemm is not None, "conv2d(hip): weights not packed for the device (ConvWeights.to_device)"
+    x_ld = x.stride(2)
+    if in_mode != "unpool":
+        assert x.stride(1) == W * x_ld and x.stride(0) == H * W * x_ld, "conv2d(hip): x pixels must be dense"
+    M = N * OH * OW
+    if epilogue == "pool":
+        assert OH % 2 == 0 and OW % 2 == 0
+        if out is None:
+            out = torch.empty(N, OH // 2, OW // 2, OC, dtype=torch.bfloat16, device=x.device)
+        out_code = torch.empty(N, OH // 2, OW // 2, OC, dtype=torch.uint8, device=x.device)
+    else:
+        out_code = None
+        if out is None:
+            odt = torch.float32 if epilogue == "f32" else torch.bfloat16
+            out = torch.empty(N, OH, OW, OC, dtype=odt, device=x.device)
+    assert out.stride(-1) == 1
+    out_ld = out.stride(-2) if out.dim() == 4 else OC
+    mask_ld = 0
+    if mask is not None:
+        assert mask.dtype == torch.bfloat16 and mask.stride(3) == 1
+        mask_ld = mask.stride(2)
+    if code is not None:
+        code = code.contiguous()
+    geom = [N, H, W, C, OH, OW, OC, cw.OCpad, cw.KH, cw.KW, stride, pad[0], pad[1], cw.K, cw.Kpad, M,
+            int(relu), int(relu_in), int(accumulate), int(code_div), x_ld, mask_ld, out_ld]
+    bias = cw.bias_pad if use_bias else None
+    lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue])
+    if epilogue == "pool":
+        return out, out_code
+    return out

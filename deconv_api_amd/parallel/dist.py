@@ -1,0 +1,141 @@
+"""One process per GPU over torch.distributed (backend "nccl" == RCCL on ROCm, xGMI links).
+
+Data-parallel deconvnet serving/benchmarking (BASELINE config 4):
+  * weights are created (or loaded) on rank 0 and broadcast once over RCCL, bucketed into a
+    few large flat messages (xGMI is point-to-point: fewer, larger collectives);
+  * each rank processes its own shard of the request batch (shards are bucket-padded to one
+    fixed per-rank size so every collective and graph has a static shape);
+  * the uint8 output mosaics are all-gathered with ``all_gather_into_tensor`` (one collective,
+    602 KB per image) so any rank can encode/serve the whole batch;
+  * a Gloo side group carries control-plane traffic (metadata, heartbeats) off the RCCL rings.
+The reference is single-process (Dockerfile:15, app/main.py:46); this layer is new.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+    ctrl_group: Optional[object] = None
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def env_world() -> int:
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init(backend: Optional[str] = None, device_type: Optional[str] = None, timeout_s: int = 600) -> DistInfo:
+    """Initialise from torchrun env vars (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*). Single process
+    without those vars returns a world of 1 and creates no process group."""
+    world = env_world()
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world == 1:
+        return DistInfo(0, 1, 0, device, "none")
+    backend = backend or ("nccl" if device_type == "cuda" else "gloo")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+    if backend == "nccl":
+        kw["device_id"] = device
+    dist.init_process_group(**kw)
+    ctrl = dist.new_group(backend="gloo") if backend == "nccl" else None
+    return DistInfo(rank, world, local, device, backend, ctrl)
+
+
+def shutdown() -> None:
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def barrier(info: DistInfo) -> None:
+    if info.world > 1:
+        if info.backend == "nccl":
+            dist.barrier(device_ids=[info.local_rank])
+        else:
+            dist.barrier()
+
+
+def broadcast_state(sd: Dict[str, torch.Tensor], info: DistInfo, src: int = 0,
+                    bucket_bytes: int = 256 << 20) -> Dict[str, torch.Tensor]:
+    """Broadcast a state dict from ``src`` as flat fp32 buckets (shapes are known on every rank
+    because every rank builds the same architecture). Returns tensors on CPU."""
+    if info.world == 1:
+        return sd
+    names = sorted(sd.keys())
+    out: Dict[str, torch.Tensor] = {}
+    dev = info.device
+    i = 0
+    while i < len(names):
+        group: List[str] = []
+        size = 0
+        while i < len(names) and (not group or size + sd[names[i]].numel() * 4 <= bucket_bytes):
+            group.append(names[i])
+            size += sd[names[i]].numel() * 4
+            i += 1
+        if info.rank == src:
+            flat = torch.cat([sd[n].reshape(-1).float() for n in group]).to(dev)
+        else:
+            flat = torch.empty(size // 4, dtype=torch.float32, device=dev)
+        dist.broadcast(flat, src)
+        off = 0
+        flat = flat.cpu()
+        for n in group:
+            k = sd[n].numel()
+            out[n] = flat[off:off + k].view_as(sd[n]).clone()
+            off += k
+    return out
+
+
+def all_gather_rows(x: torch.Tensor, info: DistInfo, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[b, ...] per rank -> [world*b, ...] on every rank (rank-major order)."""
+    if info.world == 1:
+        return x
+    if out is None:
+        out = torch.empty((info.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous())
+    return out
+
+
+def all_reduce_max(v: float, info: DistInfo) -> float:
+    if info.world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shard_sizes(total: int, world: int, bucket: int = 1) -> List[int]:
+    """Per-rank shard sizes of a ragged batch, each padded up to the same bucket-multiple size
+    (static shapes for collectives/graphs). Returns [per_rank_padded] * world and the real
+    counts via ``shard_counts``."""
+    per = -(-total // world)
+    per = -(-per // bucket) * bucket
+    return [per] * world
+
+
+def shard_counts(total: int, world: int) -> List[int]:
+    per = -(-total // world)
+    return [max(0, min(per, total - r * per)) for r in range(world)]

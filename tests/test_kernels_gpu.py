@@ -1,0 +1,206 @@
+"""GPU: every HIP kernel vs the PyTorch fp32 reference of the same op (ops/*.py CPU path).
+
+bf16 inputs/weights are rounded identically on both sides, so the only differences are fp32
+accumulation order and the final bf16 rounding of the GPU output."""
+import numpy as np
+import pytest
+import torch
+
+from deconv_api_amd import ops
+from deconv_api_amd.ops.conv import ConvWeights, pad_channels_oihw
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _cw(oc, c, kh=3, kw=3, kind="fwd", bias=True, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    shape = (oc, c, kh, kw)
+    w = _bf(torch.randn(*shape, generator=g) / np.sqrt(c * kh * kw))
+    b = _bf(torch.randn(oc if kind == "fwd" else c, generator=g) * 0.1) if bias else None
+    return ConvWeights(w, b, kind)
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-6))
+
+
+def _cmp_conv(x, cw, **kw):
+    x = x.to(torch.bfloat16)
+    ref = ops.conv2d(x.float(), cw, **kw)
+    got = ops.conv2d(x.to(DEV), cw.to_device(DEV), **kw)
+    return ref, got
+
+
+@pytest.mark.parametrize("N,H,W,C,OC", [(2, 16, 16, 8, 64), (1, 14, 14, 64, 64), (2, 9, 7, 128, 256),
+                                        (1, 12, 10, 16, 48), (3, 8, 8, 64, 3), (1, 5, 6, 512, 512),
+                                        (2, 17, 13, 24, 200)])
+def test_conv_fwd_bf16(native_lib, N, H, W, C, OC):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(N, H, W, C, generator=g)
+    cw = _cw(OC, C)
+    for relu in (True, False):
+        ref, got = _cmp_conv(x, cw, relu=relu)
+        assert got.shape == ref.shape and got.dtype == torch.bfloat16
+        assert _rel(got, ref) < 1e-2
+
+
+def test_conv_strided_and_rect_kernels(native_lib):
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(2, 17, 15, 32, generator=g)
+    for (kh, kw, s, pad) in [(1, 1, 1, (0, 0)), (1, 7, 1, (0, 3)), (7, 1, 1, (3, 0)), (3, 3, 2, (0, 0)),
+                             (1, 1, 2, (0, 0)), (5, 5, 1, (2, 2)), (7, 7, 2, (3, 3))]:
+        cw = _cw(64, 32, kh, kw)
+        ref, got = _cmp_conv(x, cw, stride=s, pad=pad)
+        assert got.shape == ref.shape, (kh, kw, s)
+        assert _rel(got, ref) < 1e-2, (kh, kw, s)
+
+
+def test_conv_f32_out_and_accumulate(native_lib):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 10, 12, 64, generator=g)
+    cw = _cw(3, 64, bias=False)
+    ref, got = _cmp_conv(x, cw, relu=True, epilogue="f32", use_bias=False)
+    assert got.dtype == torch.float32 and _rel(got, ref) < 1e-3
+    base = torch.randn(2, 10, 12, 64, generator=g)
+    cw2 = _cw(64, 64)
+    out_d = base.to(torch.bfloat16).to(DEV)
+    ops.conv2d(x.to(torch.bfloat16).to(DEV), cw2.to_device(DEV), relu=False, out=out_d, accumulate=True)
+    out_r = base.to(torch.bfloat16).float().clone()
+    ops.conv2d(_bf(x), cw2, relu=False, out=out_r, accumulate=True)
+    assert _rel(out_d, out_r) < 1e-2
+
+
+def test_conv_pool_epilogue(native_lib):
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 16, 14, 64, generator=g)
+    cw = _cw(128, 64)
+    (rp, rc), (gp, gc) = _cmp_conv(x, cw, epilogue="pool")
+    assert gp.shape == (2, 8, 7, 128) and gc.dtype == torch.uint8
+    assert _rel(gp, rp) < 1e-2
+    # switch codes must agree wherever the window max is not a near-tie
+    full = ops.conv2d(_bf(x), cw).float()
+    win = full.view(2, 8, 2, 7, 2, 128).permute(0, 1, 3, 2, 4, 5).reshape(2, 8, 7, 4, 128)
+    top2 = win.topk(2, dim=3).values
+    clear = (top2[:, :, :, 0] - top2[:, :, :, 1]) > 0.02 * top2[:, :, :, 0].abs().clamp_min(1e-3)
+    agree = (gc.cpu() == rc)[clear]
+    assert agree.float().mean() > 0.999
+
+
+def test_conv_unpool_gather(native_lib):
+    g = torch.Generator().manual_seed(5)
+    K = 2
+    p = torch.randn(4, 6, 7, 64, generator=g)  # B*K signals at pooled res
+    code = torch.randint(0, 4, (2, 6, 7, 64), generator=g, dtype=torch.uint8)
+    cw = _cw(32, 64, bias=False)
+    kw = dict(relu=True, relu_in=True, in_mode="unpool", code=code, code_div=K, use_bias=False)
+    ref = ops.conv2d(_bf(p), cw, **kw)
+    got = ops.conv2d(p.to(torch.bfloat16).to(DEV), cw.to_device(DEV),
+                     **{**kw, "code": code.to(DEV)})
+    assert got.shape == (4, 12, 14, 32) and _rel(got, ref) < 1e-2
+
+
+def test_conv_mask_and_transpose(native_lib):
+    g = torch.Generator().manual_seed(6)
+    dy = torch.randn(2, 8, 9, 64, generator=g)
+    mask = torch.randn(2, 8, 9, 64, generator=g)
+    cw = _cw(64, 32, 3, 3, kind="transpose", bias=False)  # forward conv 32 -> 64, its dgrad
+    for s, pad in [(2, (0, 0)), (2, (1, 1)), (1, (1, 1))]:
+        out_hw = ((8 - 1) * s - 2 * pad[0] + 3, (9 - 1) * s - 2 * pad[1] + 3)
+        kw = dict(relu=False, in_mode="transpose", stride=s, pad=pad, out_hw=out_hw, use_bias=False)
+        ref = ops.conv2d(_bf(dy), cw, mask=_bf(mask), **kw)
+        got = ops.conv2d(dy.to(torch.bfloat16).to(DEV), cw.to_device(DEV),
+                         mask=mask.to(torch.bfloat16).to(DEV), **kw)
+        assert got.shape == ref.shape and _rel(got, ref) < 1e-2, (s, pad)
+    # transpose == autograd input-gradient of the strided forward conv
+    x = torch.randn(1, 11, 11, 32, generator=g, requires_grad=True)
+    wf = cw.w_oihw
+    y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), wf, stride=2)
+    gy = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(y, x, gy)
+    got = ops.conv2d(gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV), cw.to_device(DEV),
+                     relu=False, in_mode="transpose", stride=2, pad=(0, 0), out_hw=(11, 11), use_bias=False)
+    assert _rel(got, gx) < 2e-2
+
+
+def test_conv_channel_slices(native_lib):
+    """input/output as channel-slice views of wider tensors (concat without copies)."""
+    g = torch.Generator().manual_seed(7)
+    big = torch.randn(2, 9, 9, 96, generator=g).to(torch.bfloat16)
+    x = big[..., 32:96]
+    cw = _cw(40, 64)
+    ref = ops.conv2d(x.float(), cw)
+    out = torch.zeros(2, 9, 9, 128, dtype=torch.bfloat16, device=DEV)
+    ops.conv2d(big.to(DEV)[..., 32:96], cw.to_device(DEV), out=out[..., 16:56])
+    assert _rel(out[..., 16:56], ref) < 1e-2
+    assert out[..., :16].abs().sum() == 0 and out[..., 56:].abs().sum() == 0
+
+
+def test_channel_sum_topk(native_lib):
+    g = torch.Generator().manual_seed(8)
+    x = torch.relu(torch.randn(5, 14, 14, 512, generator=g)).to(torch.bfloat16)
+    s_ref = x.float().sum(dim=(1, 2))
+    s = ops.channel_sum(x.to(DEV))
+    torch.testing.assert_close(s.cpu(), s_ref, rtol=1e-4, atol=1e-2)
+    v = torch.randint(-3, 4, (7, 1000), generator=g).float()
+    v[3] = -1.0
+    i_ref, v_ref = ops.topk_positive(v, 8)
+    i_got, v_got = ops.topk_positive(v.to(DEV), 8)
+    assert torch.equal(i_got.cpu(), i_ref) and torch.equal(v_got.cpu(), v_ref)
+    big = torch.randn(3, 25088, generator=g)
+    assert torch.equal(ops.topk_positive(big.to(DEV), 8)[0].cpu(), ops.topk_positive(big, 8)[0])
+
+
+def test_seed_deconv(native_lib):
+    g = torch.Generator().manual_seed(9)
+    S = torch.relu(torch.randn(6, 14, 14, generator=g))
+    f = torch.tensor([0, 5, 511, -1, 7, 3], dtype=torch.int32)
+    wt = torch.randn(512, 3, 3, 512, generator=g).to(torch.bfloat16) * 0.05
+    ref = ops.seed_deconv3x3(S, f, wt)
+    got = ops.seed_deconv3x3(S.to(DEV), f.to(DEV), wt.to(DEV))
+    assert _rel(got, ref) < 1e-2
+    assert got[3].abs().sum() == 0
+
+
+def test_deprocess_mosaic(native_lib):
+    g = torch.Generator().manual_seed(10)
+    r = torch.relu(torch.randn(8, 224, 224, 3, generator=g)) * 3
+    ref = ops.deprocess_mosaic(r)
+    got = ops.deprocess_mosaic(r.to(DEV)).cpu()
+    d = (got.int() - ref.int()).abs()
+    assert got.shape == (2, 448, 448, 3) and d.max() <= 1 and (d > 0).float().mean() < 1e-3
+
+
+def test_resize_preprocess_exact(native_lib):
+    rng = np.random.default_rng(0)
+    for hs, ws in [(300, 400), (448, 448), (224, 224), (100, 57), (1000, 224)]:
+        img = rng.integers(0, 256, size=(hs, ws, 3), dtype=np.uint8)
+        out = torch.empty(224, 224, 8, dtype=torch.bfloat16, device=DEV)
+        ops.resize_preprocess(torch.from_numpy(img).to(DEV), out)
+        ref = ops.preprocess_ref(ops.resize_u8_ref(img))
+        assert torch.equal(out.cpu(), ref), (hs, ws)
+
+
+def test_pool_unpool_standalone(native_lib):
+    g = torch.Generator().manual_seed(11)
+    x = torch.relu(torch.randint(-2, 3, (2, 12, 10, 64), generator=g).float()).to(torch.bfloat16)  # ties
+    v, c = ops.maxpool2x2(x.to(DEV))
+    rv, rc = ops.maxpool2x2(x)
+    assert torch.equal(v.cpu(), rv) and torch.equal(c.cpu(), rc)
+    p = torch.randn(4, 6, 5, 64, generator=g).to(torch.bfloat16)
+    u = ops.unpool2x2(p.to(DEV), c, code_div=2, relu=True)
+    assert torch.equal(u.cpu(), ops.unpool2x2(p, c.cpu(), code_div=2, relu=True))
+
+
+def test_conv_deterministic(native_lib):
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(4, 28, 28, 256, generator=g).to(torch.bfloat16).to(DEV)
+    cw = _cw(512, 256).to_device(DEV)
+    a = ops.conv2d(x, cw)
+    b = ops.conv2d(x, cw)
+    assert torch.equal(a, b)
