@@ -1,0 +1,96 @@
+"""Image codec for the HTTP API: data-URL parsing, decode to RGB uint8, JPEG encode, data URL.
+
+Reference behaviour being reproduced (rashanarshad/deconv_api):
+  * ``readb64`` (app/main.py:35-39): ``uri.split(',')[1]``, lenient ``base64.b64decode`` (characters
+    outside the alphabet are discarded), ``cv2.imdecode(..., IMREAD_COLOR)`` -> 3-channel 8-bit.
+    Here PIL decodes (libjpeg-turbo / libpng / libwebp), EXIF orientation is applied like OpenCV's
+    IMREAD_COLOR does, alpha is dropped and greyscale is expanded; the array is RGB, which is the
+    slot order the reference's BGR decode + channel reversal produced.
+  * encode (app/main.py:73-76): ``cv2.imencode('.jpg')`` (quality 95, 4:2:0), base64, then
+    ``'data:image/webp;base64,' + urllib.parse.quote(b64)`` — the MIME type says webp but the
+    payload is JPEG (quirk Q2) and ``quote`` escapes '+' and '=' (quirk Q3). The mosaic handed to
+    the encoder is already channel-reversed on device (quirk Q4), so an RGB encoder writes the same
+    colours OpenCV's BGR encoder wrote.
+"""
+from __future__ import annotations
+
+import base64
+import binascii
+import io
+from urllib.parse import quote
+
+import numpy as np
+from PIL import Image, ImageOps, UnidentifiedImageError
+
+DATA_URL_PREFIX = "data:image/webp;base64,"
+JPEG_QUALITY = 95
+
+
+class ImageDecodeError(ValueError):
+    pass
+
+
+def split_data_url(uri: str) -> str:
+    parts = uri.split(",")
+    if len(parts) < 2:
+        raise ImageDecodeError("file must be a data URL ('data:<mime>;base64,<payload>')")
+    return parts[1]
+
+
+def b64decode_lenient(payload: str) -> bytes:
+    try:
+        return base64.b64decode(payload)  # validate=False: non-alphabet characters are discarded
+    except (binascii.Error, ValueError) as e:
+        raise ImageDecodeError(f"bad base64 payload: {e}") from e
+
+
+def decode_image(data: bytes) -> np.ndarray:
+    """bytes -> HxWx3 uint8 RGB."""
+    try:
+        im = Image.open(io.BytesIO(data))
+        im = ImageOps.exif_transpose(im)
+        if im.mode in ("I;16", "I;16B", "I;16L", "I"):
+            arr = np.asarray(im, dtype=np.float64)
+            arr = np.clip(arr / 257.0, 0, 255).astype(np.uint8)
+            im = Image.fromarray(arr)
+        im = im.convert("RGB")
+        arr = np.asarray(im, dtype=np.uint8)
+    except (UnidentifiedImageError, OSError, SyntaxError, ValueError) as e:
+        raise ImageDecodeError(f"undecodable image: {e}") from e
+    if arr.ndim != 3 or arr.shape[2] != 3 or arr.shape[0] < 1 or arr.shape[1] < 1:
+        raise ImageDecodeError("decoded image has an unexpected shape")
+    return np.ascontiguousarray(arr)
+
+
+def read_data_url(uri: str) -> np.ndarray:
+    """The reference's ``readb64``."""
+    return decode_image(b64decode_lenient(split_data_url(uri)))
+
+
+def encode_jpeg(rgb: np.ndarray, quality: int = JPEG_QUALITY) -> bytes:
+    buf = io.BytesIO()
+    Image.fromarray(np.ascontiguousarray(rgb)).save(buf, format="JPEG", quality=quality, subsampling=2)
+    return buf.getvalue()
+
+
+def to_data_url(jpeg: bytes) -> str:
+    return DATA_URL_PREFIX + quote(base64.b64encode(jpeg).decode("ascii"))
+
+
+def encode_data_url(rgb: np.ndarray, quality: int = JPEG_QUALITY) -> str:
+    return to_data_url(encode_jpeg(rgb, quality))
+
+
+def parse_result_data_url(s: str) -> np.ndarray:
+    """Inverse of ``encode_data_url`` (tests / clients)."""
+    from urllib.parse import unquote
+
+    assert s.startswith(DATA_URL_PREFIX)
+    return decode_image(base64.b64decode(unquote(s[len(DATA_URL_PREFIX):])))
+
+
+def make_data_url(rgb: np.ndarray, fmt: str = "PNG") -> str:
+    """Client helper: an image -> 'data:image/<fmt>;base64,...' as a browser would send it."""
+    buf = io.BytesIO()
+    Image.fromarray(rgb).save(buf, format=fmt)
+    return f"data:image/{fmt.lower()};base64," + base64.b64encode(buf.getvalue()).decode("ascii")

@@ -2,8 +2,8 @@
 // storage extents (an out-of-bounds kernel access can take down the whole GPU node), then
 // calls the raw launchers on the current HIP stream (so torch.cuda graphs capture them).
 #include <torch/extension.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "kernels.h"
 
@@ -11,7 +11,8 @@ namespace {
 
 using at::Tensor;
 
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+// torch-ROCm exposes HIP devices as device type "cuda": use the masquerading guard/stream
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 void check_cuda(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -41,7 +42,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   check_cuda(x, "x");
   check_cuda(w, "w");
   check_cuda(out, "out");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   dv::ConvArgs a{};
   a.N = (int)g[0]; a.H = (int)g[1]; a.W = (int)g[2]; a.C = (int)g[3];
   a.OH = (int)g[4]; a.OW = (int)g[5]; a.OC = (int)g[6]; a.OCpad = (int)g[7];
@@ -111,7 +112,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
 
 void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
   check_cuda(x, "x");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "channel_sum: x bf16 contiguous");
   TORCH_CHECK(sums.scalar_type() == at::kFloat && sums.is_contiguous(), "channel_sum: sums fp32");
   need(x, N * HW * C * 2, "x");
@@ -123,7 +124,7 @@ void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
 
 void topk_pos(Tensor v, Tensor idx, Tensor val, int64_t k) {
   check_cuda(v, "v");
-  c10::hip::HIPGuard guard(v.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(v.device());
   TORCH_CHECK(v.dim() == 2 && v.scalar_type() == at::kFloat && v.is_contiguous(), "topk: v [N, C] fp32");
   const int64_t N = v.size(0), C = v.size(1);
   TORCH_CHECK(idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.numel() == N * k, "topk: idx [N, k] int32");
@@ -135,7 +136,7 @@ void topk_pos(Tensor v, Tensor idx, Tensor val, int64_t k) {
 
 void seed_deconv3x3(Tensor S, Tensor f, Tensor wt, Tensor out) {
   check_cuda(S, "S");
-  c10::hip::HIPGuard guard(S.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
   TORCH_CHECK(S.dim() == 3 && S.scalar_type() == at::kFloat && S.is_contiguous(), "seed: S [B,H,W] fp32");
   const int64_t B = S.size(0), H = S.size(1), W = S.size(2);
   TORCH_CHECK(f.scalar_type() == at::kInt && f.numel() == B && f.is_contiguous(), "seed: f [B] int32");
@@ -155,7 +156,7 @@ void seed_deconv3x3(Tensor S, Tensor f, Tensor wt, Tensor out) {
 
 void deprocess_mosaic(Tensor recon, Tensor out, int64_t tiles, bool reverse) {
   check_cuda(recon, "recon");
-  c10::hip::HIPGuard guard(recon.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(recon.device());
   TORCH_CHECK(recon.dim() == 4 && recon.size(3) == 3 && recon.scalar_type() == at::kFloat && recon.is_contiguous(),
               "deprocess: recon [B*tiles, H, W, 3] fp32");
   const int64_t BT = recon.size(0), H = recon.size(1), W = recon.size(2);
@@ -171,7 +172,7 @@ void deprocess_mosaic(Tensor recon, Tensor out, int64_t tiles, bool reverse) {
 
 void resize_preprocess(Tensor img, Tensor out, int64_t mode) {
   check_cuda(img, "img");
-  c10::hip::HIPGuard guard(img.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(img.device());
   TORCH_CHECK(img.dim() == 4 && img.size(3) == 3 && img.scalar_type() == at::kByte && img.is_contiguous(),
               "resize_preprocess: img [B, H, W, 3] u8");
   TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.size(0) == img.size(0),
@@ -189,7 +190,7 @@ void resize_preprocess(Tensor img, Tensor out, int64_t mode) {
 
 void maxpool2x2(Tensor x, Tensor out, Tensor code) {
   check_cuda(x, "x");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "maxpool: x NHWC bf16");
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == N * (H / 2) * (W / 2) * C,
@@ -203,7 +204,7 @@ void maxpool2x2(Tensor x, Tensor out, Tensor code) {
 
 void unpool2x2(Tensor p, Tensor code, Tensor out, int64_t code_div, bool relu) {
   check_cuda(p, "p");
-  c10::hip::HIPGuard guard(p.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
   TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16 && out.is_contiguous(), "unpool: out NHWC bf16");
   const int64_t N = out.size(0), H = out.size(1), W = out.size(2), C = out.size(3);
   TORCH_CHECK(p.scalar_type() == at::kBFloat16 && p.is_contiguous() && p.numel() == N * (H / 2) * (W / 2) * C,
