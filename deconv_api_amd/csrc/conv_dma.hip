@@ -1,0 +1,309 @@
+// LDS-DMA implicit-GEMM convolution for gfx950 (MI355X): the high-throughput path for plain
+// (non-unpool) conv forward and transposed-conv dgrad.
+//
+// Differences from conv_igemm.hip (the register-staged kernel that also handles the
+// unpool-gather and ReLU-mask prologues):
+//   * operands are staged global -> LDS by `buffer_load_dwordx4 ... lds` (LDS-DMA): no VGPR
+//     round trip and no ds_write issue cost. Conv zero padding, the M tail and the K tail come
+//     for free from the buffer descriptor's range check (an out-of-range offset returns 0);
+//   * 8 waves per workgroup, each owning a (16*FM) x (16*FN) C tile (up to 128 x 64, i.e.
+//     256 x 256 per workgroup), so each ds_read_b128 fragment feeds FN (or FM) MFMAs;
+//   * the LDS image is lane-linear per DMA instruction (8 rows x 128 B); the st_16x32-style XOR
+//     swizzle (chunk ^ (row & 7)) is applied to the per-lane SOURCE address and to the fragment
+//     read address, never to the DMA destination (cdna_hip_programming.md rule 21);
+//   * two LDS stages, one barrier per 64-deep K tile: the DMA for tile t+1 is in flight while
+//     the MFMAs of tile t run (raw s_barrier + explicit vmcnt, so the prefetch is not drained).
+#include "common.h"
+#include "kernels.h"
+
+namespace dv {
+
+namespace {
+
+constexpr int kBK = 64;
+constexpr uint32_t kOOB = 0x80000000u;  // any offset >= num_records reads as zero
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t* lds_dst, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds_dst, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
+  const uint32_t nrec = bytes > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nrec, 0x00020000);
+}
+
+}  // namespace
+
+template <int FM, int FN, int EPI, bool accum>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane);
+
+template <int WM, int WN, int FM, int FN, int AMODE, int EPI, bool CALIGNED>
+__global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a, int tiles_n) {
+  constexpr int NW = WM * WN;
+  constexpr int NT = NW * 64;
+  constexpr int BM = WM * FM * 16;
+  constexpr int BN = WN * FN * 16;
+  constexpr int A_BYTES = BM * 128;
+  constexpr int B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_I = BM / 8 / NW;                  // A DMA instructions per wave per K tile
+  constexpr int B_ROWGROUPS = BN / 8;               // 8-row groups of the B tile
+  constexpr int B_I = (B_ROWGROUPS + NW - 1) / NW;  // B DMA instructions per wave (some waves idle)
+  static_assert(A_I >= 1 && BM % (8 * NW) == 0, "BM must cover every wave");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = wgid % tiles_n;
+  const int tile_m = wgid / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int H = a.H, W = a.W, C = a.C;
+
+  // ---- tile base image: every A source offset is relative to it (32-bit voffsets) ----
+  int n_base;
+  {
+    const int g = m0 < a.M ? m0 : a.M - 1;
+    int pix = g;
+    if constexpr (EPI == CONV_E_POOL) pix = g >> 2;
+    const int per_img = (EPI == CONV_E_POOL) ? (a.OH >> 1) * (a.OW >> 1) : a.OH * a.OW;
+    n_base = pix / per_img;
+  }
+  const long long img_elems = (long long)H * W * a.x_ld;
+  const uint16_t* xb = a.x + (long long)n_base * img_elems;
+  const long long x_total = (long long)a.N * img_elems;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(xb, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
+
+  // lane -> (row within its 8-row group, logical 16-B chunk): the DMA writes position lane&7 of
+  // row lane>>3; the swizzled image stores logical chunk c at position c ^ (row & 7).
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;
+
+  // ---- per-row A gather state (rows fixed for the whole K loop) ----
+  int r_off[A_I], r_h[A_I], r_w[A_I];
+#pragma unroll
+  for (int j = 0; j < A_I; ++j) {
+    const int row = (j * NW + wave) * 8 + lrow;
+    const int gm = m0 + row;
+    int n, oh, ow;
+    const int g = gm < a.M ? gm : 0;
+    if constexpr (EPI == CONV_E_POOL) {
+      const int PWo = a.OW >> 1, PHo = a.OH >> 1;
+      const int sub = g & 3;
+      int pix = g >> 2;
+      const int pw = pix % PWo;
+      pix /= PWo;
+      const int ph = pix % PHo;
+      n = pix / PHo;
+      oh = 2 * ph + (sub >> 1);
+      ow = 2 * pw + (sub & 1);
+    } else {
+      ow = g % a.OW;
+      const int t = g / a.OW;
+      oh = t % a.OH;
+      n = t / a.OH;
+    }
+    if constexpr (AMODE == CONV_A_TRANSPOSE) {
+      r_h[j] = oh + a.pad_h;
+      r_w[j] = ow + a.pad_w;
+    } else {
+      r_h[j] = oh * a.stride - a.pad_h;
+      r_w[j] = ow * a.stride - a.pad_w;
+    }
+    r_off[j] = (n - n_base) * H * W;  // pixel index of the image's first pixel, relative to base
+    if (gm >= a.M) r_h[j] = -(1 << 28);  // never in bounds
+  }
+
+  auto issue = [&](int kt, int buf) {
+    uint8_t* As = smem + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+    // K coordinates of this lane's chunk
+    int kh, kw, ch;
+    bool kval;
+    if constexpr (CALIGNED) {
+      const int k0 = kt * kBK;
+      const int tap = k0 / C;  // wave-uniform
+      kh = tap / a.KW;
+      kw = tap - kh * a.KW;
+      ch = k0 - tap * C + lchunk * 8;
+      kval = tap < a.KH * a.KW;
+    } else {
+      const int k = kt * kBK + lchunk * 8;
+      const int tap = k / C;
+      kh = tap / a.KW;
+      kw = tap - kh * a.KW;
+      ch = k - tap * C;
+      kval = k < a.K;
+    }
+#pragma unroll
+    for (int j = 0; j < A_I; ++j) {
+      int ih, iw;
+      bool ok;
+      if constexpr (AMODE == CONV_A_TRANSPOSE) {
+        const int th = r_h[j] - kh, tw = r_w[j] - kw;
+        const int s = a.stride;
+        ih = th / s;
+        iw = tw / s;
+        ok = th >= 0 && tw >= 0 && ih * s == th && iw * s == tw && ih < H && iw < W;
+      } else {
+        ih = r_h[j] + kh;
+        iw = r_w[j] + kw;
+        ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      }
+      ok = ok && kval;
+      const uint32_t voff =
+          ok ? (uint32_t)((((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch) * 2) : kOOB;
+      dma16(xr, As + (j * NW + wave) * 1024, voff);
+    }
+#pragma unroll
+    for (int j = 0; j < B_I; ++j) {
+      const int grp = j * NW + wave;
+      if (grp < B_ROWGROUPS) {
+        const int row = grp * 8 + lrow;
+        const uint32_t voff = (uint32_t)((((long long)(n0 + row)) * a.Kpad + kt * kBK + lchunk * 8) * 2);
+        dma16(wr, Bs + grp * 1024, voff);
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets: row = base + (lane & 15) -> swizzle term is lane & 7
+  const int a_row0 = wm * FM * 16 + (lane & 15);
+  const int b_row0 = wn * FN * 16 + (lane & 15);
+  int sw[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) sw[s] = (((s * 4 + (lane >> 4)) ^ (lane & 7)) << 4);
+
+  const int nk = a.Kpad / kBK;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const uint8_t* As = smem + cur * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (b_row0 + j * 16) * 128 + sw[s]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (a_row0 + i * 16) * 128 + sw[s]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue ----
+  if (a.accumulate)
+    epilogue<FM, FN, EPI, true>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+  else
+    epilogue<FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+}
+
+template <int FM, int FN, int EPI, bool accum>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane) {
+  const int row_l = (lane >> 4) * 4;
+  const int col_l = lane & 15;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = nw + j * 16 + col_l;
+    if (col >= a.OC) continue;
+    const float bias = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int rowb = mw + i * 16 + row_l;
+      if (rowb >= a.M) continue;
+      if constexpr (EPI == CONV_E_POOL) {
+        float best = -INFINITY;
+        int code = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bias;
+          if (a.relu) v = fmaxf(v, 0.f);
+          v = bf2f(f2bf(v));
+          if (v > best) {
+            best = v;
+            code = r;
+          }
+        }
+        const long long prow = rowb >> 2;
+        reinterpret_cast<uint16_t*>(a.out)[prow * a.out_ld + col] = f2bf(best);
+        a.out_code[prow * a.OC + col] = (uint8_t)code;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rowb + r;
+          if (row >= a.M) continue;
+          float v = acc[i][j][r] + bias;
+          if (a.relu) v = fmaxf(v, 0.f);
+          const long long o = (long long)row * a.out_ld + col;
+          if constexpr (EPI == CONV_E_F32) {
+            float* out = reinterpret_cast<float*>(a.out);
+            if (accum) v += out[o];
+            out[o] = v;
+          } else {
+            uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+            if (accum) v += bf2f(out[o]);
+            out[o] = f2bf(v);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int FM, int FN, int AMODE, int EPI>
+static int dma_cfg(const ConvArgs& a, hipStream_t s) {
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int tiles_n = a.OCpad / BN;
+  const long long nwg = (long long)tiles_m * tiles_n;
+  if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
+  const bool aligned = (a.C % kBK) == 0;
+  if (aligned)
+    hipLaunchKernelGGL((conv_dma_kernel<WM, WN, FM, FN, AMODE, EPI, true>), dim3((unsigned)nwg),
+                       dim3(WM * WN * 64), 0, s, a, tiles_n);
+  else
+    hipLaunchKernelGGL((conv_dma_kernel<WM, WN, FM, FN, AMODE, EPI, false>), dim3((unsigned)nwg),
+                       dim3(WM * WN * 64), 0, s, a, tiles_n);
+  return (int)hipGetLastError();
+}
+
+template <int AMODE, int EPI>
+static int dma_bn(const ConvArgs& a, hipStream_t s) {
+  if (a.OCpad % 256 == 0 && a.OC > 128) return dma_cfg<2, 4, 8, 4, AMODE, EPI>(a, s);   // 256 x 256
+  if (a.OCpad % 128 == 0 && a.OC > 64) return dma_cfg<4, 2, 4, 4, AMODE, EPI>(a, s);    // 256 x 128
+  if (a.OCpad % 64 == 0 && a.OC > 16) return dma_cfg<8, 1, 4, 4, AMODE, EPI>(a, s);     // 512 x 64
+  if (a.OCpad % 16 == 0) return dma_cfg<8, 1, 4, 1, AMODE, EPI>(a, s);                  // 512 x 16
+  return -3;
+}
+
+int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t s) {
+  if (a.C % 8 != 0 || a.Kpad % kBK != 0 || a.mask != nullptr || a.x_ld % 8 != 0) return -4;
+  if (amode == CONV_A_FWD) {
+    if (epi == CONV_E_BF16) return dma_bn<CONV_A_FWD, CONV_E_BF16>(a, s);
+    if (epi == CONV_E_POOL) return dma_bn<CONV_A_FWD, CONV_E_POOL>(a, s);
+    if (epi == CONV_E_F32) return dma_bn<CONV_A_FWD, CONV_E_F32>(a, s);
+  } else if (amode == CONV_A_TRANSPOSE) {
+    if (epi == CONV_E_BF16) return dma_bn<CONV_A_TRANSPOSE, CONV_E_BF16>(a, s);
+  }
+  return -1;
+}
+
+}  // namespace dv

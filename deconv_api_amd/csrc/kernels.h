@@ -40,6 +40,8 @@ struct ConvArgs {
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
+// LDS-DMA variant (FWD / TRANSPOSE, no mask): 8-wave 128x64-per-wave tiles
+int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
 
 // ---- misc kernels (misc.hip) ----
 // per-(image, channel) sums of a NHWC bf16 tensor: sums[n][c] = sum_{hw} x[n][hw][c]
@@ -61,4 +63,10 @@ int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, in
 int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int N, int H, int W,
                      int C, int code_div, int relu, hipStream_t s);
 
+}  // namespace dv
+
+namespace dv {
+// halo-tile 3x3/s1/p1 conv for OC <= 16 (fp32 out), C == 64
+int conv3x3_smalln_launch(const uint16_t* x, const uint16_t* w, float* out, int N, int H, int W, int C, int OC,
+                          int Kpad, int relu_in, int relu, long long out_ld, hipStream_t s);
 }  // namespace dv

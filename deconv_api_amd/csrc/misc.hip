@@ -381,9 +381,60 @@ __global__ void __launch_bounds__(256) unpool2x2_kernel(const uint16_t* __restri
   }
 }
 
+// Vectorized unpool: one thread per (pooled pixel, 8-channel chunk): one 16-B pooled load, one
+// 8-B code load, four 16-B stores (the 2x2 window); consecutive threads write consecutive chunks.
+__global__ void __launch_bounds__(256) unpool2x2_vec_kernel(const uint16_t* __restrict__ p,
+                                                            const uint8_t* __restrict__ code,
+                                                            uint16_t* __restrict__ out, int N, int H, int W, int C,
+                                                            int code_div, int relu) {
+  const int PH = H >> 1, PW = W >> 1, cpp = C >> 3;
+  const long long total = (long long)N * PH * PW * cpp;
+  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total; g += (long long)gridDim.x * 256) {
+    const int chunk = (int)(g % cpp);
+    const long long pix = g / cpp;
+    const int pw = (int)(pix % PW);
+    const long long t = pix / PW;
+    const int ph = (int)(t % PH);
+    const long long n = t / PH;
+    uint4 v = *reinterpret_cast<const uint4*>(p + pix * C + chunk * 8);
+    if (relu) {
+      v.x = relu_bf2(v.x);
+      v.y = relu_bf2(v.y);
+      v.z = relu_bf2(v.z);
+      v.w = relu_bf2(v.w);
+    }
+    const long long cpix = ((n / code_div) * PH + ph) * PW + pw;
+    const uint2 cd = *reinterpret_cast<const uint2*>(code + cpix * C + chunk * 8);
+    const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t sel4 = (uint32_t)s * 0x01010101u;
+      const uint32_t e0 = cd.x ^ sel4, e1 = cd.y ^ sel4;
+      uint32_t o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t e = q < 2 ? e0 : e1;
+        const int b0 = (q & 1) * 2;
+        const uint32_t lo = ((e >> (8 * b0)) & 0xFFu) == 0u ? 0xFFFFu : 0u;
+        const uint32_t hi = ((e >> (8 * (b0 + 1))) & 0xFFu) == 0u ? 0xFFFF0000u : 0u;
+        o[q] = vw[q] & (lo | hi);
+      }
+      const int h = 2 * ph + (s >> 1), w = 2 * pw + (s & 1);
+      *reinterpret_cast<uint4*>(out + ((n * H + h) * W + w) * C + chunk * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
 int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int N, int H, int W, int C, int code_div,
                      int relu, hipStream_t s) {
   if (((H | W) & 1) || code_div <= 0) return -1;
+  if (C % 8 == 0) {
+    const long long total = (long long)N * (H / 2) * (W / 2) * (C / 8);
+    const long long blocks = std::min<long long>((total + 255) / 256, 256LL * 32);
+    hipLaunchKernelGGL(unpool2x2_vec_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, code, out, N, H, W, C,
+                       code_div, relu);
+    return (int)hipGetLastError();
+  }
   const long long total = (long long)N * H * W * C;
   const long long blocks = std::min<long long>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(unpool2x2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, code, out, N, H, W, C, code_div,

@@ -13,6 +13,18 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True, params=["dma", "reg"])
+def conv_impl(request):
+    """Run every test against both conv kernels (LDS-DMA and register-staged)."""
+    from deconv_api_amd.ops import conv as C
+
+    old = C.get_policy()
+    C.set_policy(impl="auto" if request.param == "dma" else "reg",
+                 unpool="split" if request.param == "dma" else "fused")
+    yield request.param
+    C.set_policy(**old)
+
+
 def _bf(t):
     return t.to(torch.bfloat16).float()
 
