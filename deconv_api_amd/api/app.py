@@ -1,0 +1,157 @@
+"""FastAPI application with the reference's HTTP surface (app/main.py:19-78):
+
+  GET  /health-check -> {"healthy": "true"}                                   (main.py:41-43)
+  POST /             form fields ``file`` (image data URL) and ``layer`` -> JSON string
+                     ``"data:image/webp;base64,<quoted base64 JPEG>"`` of the 2x2 mosaic
+                     of the top-4 deconvnet reconstructions                    (main.py:45-78)
+  CORS: every origin, no credentials, all methods/headers                    (main.py:22-32)
+  /docs, /redoc, /openapi.json (FastAPI built-ins; the form body is declared by hand because
+  ``Form(...)`` needs python-multipart, which is not installed)
+
+Extensions: GET /ready (per-device status), GET /metrics (Prometheus text), GET /layers,
+POST /deepdream (when the DeepDream engine is available).
+
+Error handling differs deliberately from the reference (which 500s on all of these):
+missing fields -> 422 (FastAPI's own validation shape), undecodable image / malformed data URL /
+unknown layer -> 400, queue full -> 503; fewer than 4 positive filters -> black tiles.
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+from fastapi import FastAPI, Request
+from fastapi.middleware.cors import CORSMiddleware
+from fastapi.responses import JSONResponse, PlainTextResponse
+
+from ..codec import ImageDecodeError
+from ..config import Config
+from ..engine.deconvnet import UnknownLayerError
+from ..utils import metrics as M
+from ..utils.logging import get_logger, new_request_id, setup
+from .forms import FormError, parse_form
+
+log = get_logger("deconv_api_amd.api")
+
+_FORM_SCHEMA = {
+    "requestBody": {
+        "required": True,
+        "content": {
+            ct: {"schema": {"title": "Body_return_deconv__post", "type": "object", "required": ["file", "layer"],
+                            "properties": {"file": {"title": "File", "type": "string"},
+                                           "layer": {"title": "Layer", "type": "string"}}}}
+            for ct in ("application/x-www-form-urlencoded", "multipart/form-data")
+        },
+    }
+}
+
+
+def _missing(fields):
+    return JSONResponse(status_code=422, content={"detail": [
+        {"loc": ["body", f], "msg": "field required", "type": "value_error.missing"} for f in fields]})
+
+
+def create_app(service=None, cfg: Optional[Config] = None, dream_service=None) -> FastAPI:
+    cfg = cfg or Config.from_env()
+    setup(cfg.log_json)
+    app = FastAPI()
+    app.add_middleware(CORSMiddleware, allow_origins=list(cfg.cors_origins), allow_credentials=False,
+                       allow_methods=["*"], allow_headers=["*"])
+    state = {"service": service, "dream": dream_service}
+
+    def get_service():
+        if state["service"] is None:
+            from ..serve.service import DeconvService
+
+            state["service"] = DeconvService(cfg)
+        return state["service"]
+
+    app.state.get_service = get_service
+
+    @app.get("/health-check")
+    def healthcheck():
+        M.REQUESTS.inc(route="/health-check", status="200")
+        return {"healthy": "true"}
+
+    @app.post("/", openapi_extra=_FORM_SCHEMA)
+    async def return_deconv(request: Request):
+        rid = new_request_id()
+        t0 = time.perf_counter()
+        status, layer = "200", "-"
+        try:
+            try:
+                form = parse_form(await request.body(), request.headers.get("content-type"))
+            except FormError as e:
+                status = "400"
+                return JSONResponse(status_code=400, content={"detail": str(e)})
+            missing = [f for f in ("file", "layer") if f not in form]
+            if missing:
+                status = "422"
+                return _missing(missing)
+            layer = form["layer"]
+            svc = get_service()
+            try:
+                url = await svc.deconv(form["file"], layer)
+            except UnknownLayerError as e:
+                status = "400"
+                return JSONResponse(status_code=400, content={"detail": str(e).strip('"')})
+            except ImageDecodeError as e:
+                status = "400"
+                return JSONResponse(status_code=400, content={"detail": str(e)})
+            except Exception as e:  # noqa: BLE001
+                from ..serve.service import ServiceOverloaded
+
+                if isinstance(e, ServiceOverloaded):
+                    status = "503"
+                    return JSONResponse(status_code=503, content={"detail": str(e)})
+                status = "500"
+                log.exception("deconv request failed", extra={"fields": {"request_id": rid}})
+                return JSONResponse(status_code=500, content={"detail": "internal error"})
+            return JSONResponse(content=url)
+        finally:
+            M.REQUESTS.inc(route="/", status=status)
+            M.LATENCY.observe(time.perf_counter() - t0, route="/", layer=layer)
+
+    @app.get("/ready")
+    def ready():
+        svc = state["service"]
+        if svc is None:
+            return JSONResponse(status_code=503, content={"ready": False, "reason": "service not started"})
+        st = svc.status()
+        ok = st.get("worker_alive", False)
+        return JSONResponse(status_code=200 if ok else 503, content={"ready": ok, **st})
+
+    @app.get("/metrics")
+    def metrics():
+        return PlainTextResponse(M.REGISTRY.render(), media_type="text/plain; version=0.0.4")
+
+    @app.get("/layers")
+    def layers():
+        svc = get_service()
+        return {"layers": [s.name for s in svc.engine.specs[1:]]}
+
+    @app.post("/deepdream", openapi_extra=_FORM_SCHEMA)
+    async def deepdream(request: Request):
+        """Extension (not in the reference): DeepDream of the uploaded image. Form fields: file,
+        optional model (inception_v3 | resnet50), octaves, steps. Same data-URL conventions."""
+        form = parse_form(await request.body(), request.headers.get("content-type"))
+        if "file" not in form:
+            return _missing(["file"])
+        ds = state["dream"]
+        if ds is None:
+            from ..serve.dream_service import DreamService
+
+            ds = state["dream"] = DreamService(cfg)
+        try:
+            url = await ds.dream(form["file"], form.get("model", "inception_v3"), int(form.get("octaves", 4)),
+                                 int(form.get("steps", 20)))
+        except (ImageDecodeError, ValueError) as e:
+            return JSONResponse(status_code=400, content={"detail": str(e)})
+        return JSONResponse(content=url)
+
+    return app
+
+
+def main_app() -> FastAPI:
+    """uvicorn entry: ``uvicorn deconv_api_amd.api.app:main_app --factory``."""
+    return create_app()

@@ -1,0 +1,63 @@
+"""Single frozen configuration with ``DV_*`` environment overrides.
+
+The reference hard-codes every setting (app/main.py:16-17,53,64,67-69,73; Dockerfile:10,15);
+the defaults below reproduce those values."""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field
+from typing import Tuple
+
+
+def _env(name: str, default, cast):
+    v = os.environ.get(name)
+    if v is None or v == "":
+        return default
+    if cast is bool:
+        return v.lower() in ("1", "true", "yes", "on")
+    if cast is tuple:
+        return tuple(x.strip() for x in v.split(",") if x.strip())
+    return cast(v)
+
+
+@dataclass(frozen=True)
+class Config:
+    model: str = "vgg16"                  # reference: vgg16.VGG16 (app/main.py:17)
+    weights: str = ""                     # path to .safetensors/.pt/.h5; empty = seeded random init
+    seed: int = 0
+    dtype: str = "bf16"
+    device: str = "auto"                  # auto | cuda | cpu
+    image_size: int = 224                 # app/main.py:53
+    filters: int = 4                      # tiles in the mosaic (app/main.py:67-69)
+    top: int = 8                          # find_top_filters default (app/deepdream.py:369)
+    mode: str = "all"                     # visualize_mode (app/main.py:64)
+    jpeg_quality: int = 95                # OpenCV imencode default (app/main.py:73)
+    max_batch: int = 64                   # request batcher
+    batch_timeout_ms: float = 4.0
+    max_queue: int = 4096                 # backpressure: 503 beyond this many pending requests
+    request_timeout_s: float = 120.0
+    codec_workers: int = 8
+    cors_origins: Tuple[str, ...] = ("*",)  # app/main.py:22-32
+    host: str = "0.0.0.0"
+    port: int = 80                        # Dockerfile:10,15
+    hip_graphs: bool = True
+    log_json: bool = True
+
+    @classmethod
+    def from_env(cls, **overrides) -> "Config":
+        kw = {}
+        for f in dataclasses.fields(cls):
+            cast = {int: int, float: float, bool: bool, str: str}.get(type(f.default), tuple)
+            if isinstance(f.default, tuple):
+                cast = tuple
+            kw[f.name] = _env("DV_" + f.name.upper(), f.default, cast)
+        kw.update(overrides)
+        return cls(**kw)
+
+    def resolve_device(self) -> str:
+        if self.device != "auto":
+            return self.device
+        import torch
+
+        return "cuda" if torch.cuda.is_available() else "cpu"

@@ -107,11 +107,39 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   }
   need(out, ((out_rows - 1) * a.out_ld + a.OC) * (int64_t)out.element_size(), "out");
   a.out = out.data_ptr();
-  // impl: 0 auto (LDS-DMA kernel when the op allows it), 1 register-staged, 2 LDS-DMA
-  const bool dma_ok = (amode == dv::CONV_A_FWD || (amode == dv::CONV_A_TRANSPOSE && epi == dv::CONV_E_BF16)) &&
-                      !mask.has_value();
-  TORCH_CHECK(impl != 2 || dma_ok, "conv: LDS-DMA kernel does not support this mode");
-  if (dma_ok && impl != 1) {
+  // Kernel choice. impl: 0 auto, 1 register-staged (conv_igemm), 2 LDS-DMA (conv_dma), 3 halo-tile.
+  //  * halo-tile (3x3 s1 p1, OC tile <= 64, >= 56x56 maps): input staged once per tile, unpool fused
+  //  * LDS-DMA: FWD / TRANSPOSE without mask; an unpool input is first materialized (vector kernel)
+  //  * register-staged: everything else (ReLU-mask prologue, fused unpool gather)
+  const bool halo_ok = (amode == dv::CONV_A_FWD || amode == dv::CONV_A_UNPOOL) && a.KH == 3 && a.KW == 3 &&
+                       a.stride == 1 && a.pad_h == 1 && a.pad_w == 1 && a.C % 32 == 0 && a.H == a.OH &&
+                       a.W == a.OW && !a.accumulate && !mask.has_value() &&
+                       (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad % 64 == 0);
+  // measured on MI355X (profiles/layers_r1_*.txt): the per-tile weight restage makes the halo kernel
+  // slower than LDS-DMA on every VGG shape so far, so it is opt-in (impl 3) until it is persistent
+  const bool halo_auto = false;
+  if (impl == 3 || (impl == 0 && halo_auto)) {
+    TORCH_CHECK(halo_ok, "conv: halo-tile kernel does not support this shape/mode");
+    check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream()), "conv_halo");
+    return;
+  }
+  const bool dma_mode = (amode == dv::CONV_A_FWD || amode == dv::CONV_A_UNPOOL ||
+                         (amode == dv::CONV_A_TRANSPOSE && epi == dv::CONV_E_BF16)) && !mask.has_value();
+  TORCH_CHECK(impl != 2 || dma_mode, "conv: LDS-DMA kernel does not support this mode");
+  if (dma_mode && impl != 1) {
+    Tensor unpooled;
+    if (amode == dv::CONV_A_UNPOOL) {  // materialize the unpooled map, then a plain DMA conv
+      TORCH_CHECK(a.x_ld == a.C, "conv unpool (split): pooled input must be channel-dense");
+      unpooled = at::empty({a.N, a.H, a.W, a.C}, x.options());
+      check_rc(dv::unpool2x2_launch(a.x, a.code, reinterpret_cast<uint16_t*>(unpooled.data_ptr()), a.N, a.H, a.W,
+                                    a.C, a.code_div, a.relu_in, cur_stream()),
+               "unpool2x2");
+      a.x = reinterpret_cast<const uint16_t*>(unpooled.data_ptr());
+      a.x_ld = a.C;
+      a.relu_in = 0;
+      a.code = nullptr;
+      amode = dv::CONV_A_FWD;
+    }
     // the DMA kernel addresses A with 32-bit offsets relative to the tile's first image
     const int64_t imgs_per_tile = 512 / std::max(1, a.OH * a.OW) + 2;
     TORCH_CHECK((int64_t)a.H * a.W * a.x_ld * 2 * imgs_per_tile < 0x7FFFFFF0LL, "conv dma: image too large");
@@ -119,28 +147,6 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   } else {
     check_rc(dv::conv_igemm_launch(a, (int)amode, (int)epi, cur_stream()), "conv_igemm");
   }
-}
-
-void conv3x3_smalln(Tensor x, Tensor w, Tensor out, int64_t OC, bool relu_in, bool relu) {
-  check_cuda(x, "x");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.size(3) == 64,
-              "conv3x3_smalln: x [N,H,W,64] bf16 contiguous");
-  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  TORCH_CHECK(w.dim() == 2 && w.size(0) == 16 && w.size(1) >= 9 * C && w.scalar_type() == at::kBFloat16 &&
-                  w.is_contiguous(),
-              "conv3x3_smalln: w [16, Kpad] bf16");
-  TORCH_CHECK(OC >= 1 && OC <= 16, "conv3x3_smalln: OC <= 16");
-  TORCH_CHECK(out.scalar_type() == at::kFloat && out.dim() == 4 && out.stride(3) == 1 && out.size(0) == N &&
-                  out.size(1) == H && out.size(2) == W && out.stride(1) == W * out.stride(2) &&
-                  out.stride(0) == H * W * out.stride(2),
-              "conv3x3_smalln: out [N,H,W,>=OC] fp32 dense pixels");
-  need(out, ((N * H * W - 1) * out.stride(2) + OC) * 4, "out");
-  check_rc(dv::conv3x3_smalln_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                                     reinterpret_cast<const uint16_t*>(w.data_ptr()), out.data_ptr<float>(), (int)N,
-                                     (int)H, (int)W, (int)C, (int)OC, (int)w.size(1), relu_in ? 1 : 0, relu ? 1 : 0,
-                                     out.stride(2), cur_stream()),
-           "conv3x3_smalln");
 }
 
 void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
@@ -256,7 +262,6 @@ void unpool2x2(Tensor p, Tensor code, Tensor out, int64_t code_div, bool relu) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "deconv_api_amd gfx950 (MI355X) HIP kernels";
   m.def("conv", &conv, "MFMA implicit-GEMM conv (fwd / unpool-gather / transposed; bf16/pool/f32 epilogues)");
-  m.def("conv3x3_smalln", &conv3x3_smalln, "halo-tile 3x3 conv for OC <= 16 (fp32 out)");
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);
   m.def("seed_deconv3x3", &seed_deconv3x3);

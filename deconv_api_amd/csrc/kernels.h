@@ -66,7 +66,6 @@ int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int 
 }  // namespace dv
 
 namespace dv {
-// halo-tile 3x3/s1/p1 conv for OC <= 16 (fp32 out), C == 64
-int conv3x3_smalln_launch(const uint16_t* x, const uint16_t* w, float* out, int N, int H, int W, int C, int OC,
-                          int Kpad, int relu_in, int relu, long long out_ld, hipStream_t s);
+// halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
+int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s);
 }  // namespace dv

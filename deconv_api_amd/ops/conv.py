@@ -23,21 +23,19 @@ from . import native
 
 AMODE = {"plain": 0, "unpool": 1, "transpose": 2}
 EPI = {"bf16": 0, "pool": 1, "f32": 2}
-IMPL = {"auto": 0, "reg": 1, "dma": 2}
+IMPL = {"auto": 0, "reg": 1, "dma": 2, "halo": 3}
 
-# Kernel selection policy (A/B testing): DV_CONV_IMPL = auto | reg | dma ;
-# DV_UNPOOL = fused (unpool gather inside the register-staged conv) | split (standalone unpool
-# kernel, then the LDS-DMA conv).
-_policy = {"impl": os.environ.get("DV_CONV_IMPL", "auto"), "unpool": os.environ.get("DV_UNPOOL", "split")}
+# Kernel selection policy (A/B testing), DV_CONV_IMPL = auto | reg | dma | halo. 'auto' lets the
+# binding pick per shape (bindings.cpp: halo-tile for narrow 3x3 layers at large maps, LDS-DMA
+# elsewhere, register-staged for the ReLU-mask prologue); 'reg' forces the register-staged kernel
+# with its fused unpool gather.
+_policy = {"impl": os.environ.get("DV_CONV_IMPL", "auto")}
 
 
-def set_policy(impl: Optional[str] = None, unpool: Optional[str] = None) -> None:
+def set_policy(impl: Optional[str] = None) -> None:
     if impl is not None:
         assert impl in IMPL
         _policy["impl"] = impl
-    if unpool is not None:
-        assert unpool in ("fused", "split")
-        _policy["unpool"] = unpool
 
 
 def get_policy() -> dict:
@@ -259,19 +257,7 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
                 epilogue, out, accumulate, use_bias):
     lib = native.lib()
     assert x.dtype == torch.bfloat16 and x.stride(3) == 1, "conv2d(hip): x must be bf16 NHWC (channel stride 1)"
-    if in_mode == "unpool" and _policy["unpool"] == "split" and _policy["impl"] != "reg":
-        from .misc import unpool2x2
-
-        x = unpool2x2(x, code, code_div, relu=relu_in)
-        in_mode, code, code_div, relu_in = "plain", None, 1, False
     assert cw.w_gemm is not None, "conv2d(hip): weights not packed for the device (ConvWeights.to_device)"
-    if (OC <= 16 and C == 64 and cw.KH == 3 and cw.KW == 3 and stride == 1 and tuple(pad) == (1, 1)
-            and in_mode == "plain" and epilogue == "f32" and mask is None and not accumulate
-            and x.is_contiguous() and _policy["impl"] != "reg" and not (use_bias and cw.bias is not None)):
-        if out is None:
-            out = torch.empty(N, OH, OW, OC, dtype=torch.float32, device=x.device)
-        lib.conv3x3_smalln(x, cw.w_gemm, out, OC, bool(relu_in), bool(relu))
-        return out
     x_ld = x.stride(2)
     if in_mode != "unpool":
         assert x.stride(1) == W * x_ld and x.stride(0) == H * W * x_ld, "conv2d(hip): x pixels must be dense"

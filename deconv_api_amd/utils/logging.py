@@ -1,0 +1,45 @@
+"""Structured (JSON) logging with request ids (the reference only ``print``s:
+app/deepdream.py:419-420,438,445-447,459)."""
+from __future__ import annotations
+
+import contextvars
+import json
+import logging
+import sys
+import time
+import uuid
+
+request_id: contextvars.ContextVar[str] = contextvars.ContextVar("request_id", default="-")
+
+
+class JsonFormatter(logging.Formatter):
+    def format(self, rec: logging.LogRecord) -> str:
+        d = {"ts": round(time.time(), 6), "level": rec.levelname, "logger": rec.name, "msg": rec.getMessage(),
+             "request_id": request_id.get()}
+        extra = getattr(rec, "fields", None)
+        if isinstance(extra, dict):
+            d.update(extra)
+        if rec.exc_info:
+            d["exc"] = self.formatException(rec.exc_info)
+        return json.dumps(d, default=str)
+
+
+def setup(json_format: bool = True, level: int = logging.INFO) -> logging.Logger:
+    log = logging.getLogger("deconv_api_amd")
+    if not log.handlers:
+        h = logging.StreamHandler(sys.stderr)
+        h.setFormatter(JsonFormatter() if json_format else logging.Formatter("%(asctime)s %(levelname)s %(message)s"))
+        log.addHandler(h)
+        log.setLevel(level)
+        log.propagate = False
+    return log
+
+
+def new_request_id() -> str:
+    rid = uuid.uuid4().hex[:16]
+    request_id.set(rid)
+    return rid
+
+
+def get_logger(name: str = "deconv_api_amd") -> logging.Logger:
+    return logging.getLogger(name)

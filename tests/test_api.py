@@ -1,0 +1,176 @@
+"""CPU: HTTP surface parity with app/main.py (routes, form fields, CORS, response format)."""
+import base64
+import io
+import json
+from urllib.parse import quote
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from deconv_api_amd import ops
+from deconv_api_amd.api.app import create_app
+from deconv_api_amd.api.forms import encode_multipart, parse_form, parse_multipart, parse_urlencoded
+from deconv_api_amd.codec import DATA_URL_PREFIX, make_data_url, parse_result_data_url, read_data_url
+from deconv_api_amd.config import Config
+from deconv_api_amd.engine.deconvnet import DeconvNet
+from deconv_api_amd.models.vgg16 import VGG16
+from deconv_api_amd.serve.service import DeconvService
+
+pytestmark = pytest.mark.filterwarnings("ignore::DeprecationWarning")
+
+
+@pytest.fixture(scope="module")
+def client(small_specs):
+    from fastapi.testclient import TestClient
+
+    cfg = Config.from_env(device="cpu", image_size=32, max_batch=8, batch_timeout_ms=1.0, codec_workers=2)
+    eng = DeconvNet(VGG16.random(0, specs=small_specs).build("cpu", torch.float32))
+    svc = DeconvService(cfg, engine=eng)
+    app = create_app(svc, cfg)
+    with TestClient(app) as c:
+        yield c, svc
+    svc.close()
+
+
+def _img(h=40, w=50, seed=0):
+    return np.random.default_rng(seed).integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+
+
+def test_health_check(client):
+    c, _ = client
+    r = c.get("/health-check")
+    assert r.status_code == 200 and r.json() == {"healthy": "true"}
+
+
+def test_cors(client):
+    c, _ = client
+    r = c.get("/health-check", headers={"Origin": "http://example.com"})
+    assert r.headers["access-control-allow-origin"] == "*"
+    pre = c.options("/", headers={"Origin": "http://x.y", "Access-Control-Request-Method": "POST",
+                                  "Access-Control-Request-Headers": "content-type"})
+    assert pre.status_code == 200 and pre.headers["access-control-allow-origin"] == "*"
+
+
+def _check_url(s, size=64):
+    assert isinstance(s, str) and s.startswith(DATA_URL_PREFIX)
+    payload = s[len(DATA_URL_PREFIX):]
+    assert "+" not in payload and "=" not in payload  # quote() escapes them (quirk Q3)
+    rgb = parse_result_data_url(s)
+    assert rgb.shape == (size, size, 3)
+    return rgb
+
+
+def test_post_urlencoded_and_multipart(client):
+    c, _ = client
+    url = make_data_url(_img(), "PNG")
+    r = c.post("/", data={"file": url, "layer": "block3_conv1"})
+    assert r.status_code == 200 and r.headers["content-type"].startswith("application/json")
+    a = _check_url(r.json())
+    body, ct = encode_multipart({"file": url, "layer": "block3_conv1"})
+    r2 = c.post("/", content=body, headers={"content-type": ct})
+    assert r2.status_code == 200
+    b = _check_url(r2.json())
+    assert np.array_equal(a, b)
+
+
+def test_post_matches_engine(client):
+    """The HTTP result equals the engine's mosaic for the same image (up to JPEG)."""
+    c, svc = client
+    img = _img(32, 32, seed=3)
+    r = c.post("/", data={"file": make_data_url(img, "PNG"), "layer": "block2_pool"})
+    got = _check_url(r.json()).astype(int)
+    x = svc.preprocess([img])
+    want = svc.engine.run(x, "block2_pool", k=4).mosaic[0].numpy()
+    from deconv_api_amd.codec import encode_data_url
+
+    assert np.array_equal(got, parse_result_data_url(encode_data_url(want)).astype(int))
+
+
+def test_errors(client):
+    c, _ = client
+    r = c.post("/", data={"layer": "block1_conv1"})
+    assert r.status_code == 422 and r.json()["detail"][0]["loc"] == ["body", "file"]
+    r = c.post("/", data={"file": make_data_url(_img(), "PNG"), "layer": "nope"})
+    assert r.status_code == 400 and "unknown layer" in r.json()["detail"]
+    r = c.post("/", data={"file": "no-comma-here", "layer": "block1_conv1"})
+    assert r.status_code == 400
+    r = c.post("/", data={"file": "data:image/png;base64," + base64.b64encode(b"junk").decode(), "layer": "fc1"})
+    assert r.status_code == 400
+    r = c.post("/", data={"file": make_data_url(_img(), "PNG"), "layer": "input_1"})
+    assert r.status_code == 400
+
+
+def test_openapi_form_schema(client):
+    c, _ = client
+    spec = c.get("/openapi.json").json()
+    body = spec["paths"]["/"]["post"]["requestBody"]["content"]
+    for ct in ("application/x-www-form-urlencoded", "multipart/form-data"):
+        assert sorted(body[ct]["schema"]["required"]) == ["file", "layer"]
+    assert "/health-check" in spec["paths"]
+    assert c.get("/docs").status_code == 200
+
+
+def test_metrics_ready_layers(client):
+    c, _ = client
+    c.post("/", data={"file": make_data_url(_img(), "JPEG"), "layer": "block1_conv1"})
+    m = c.get("/metrics").text
+    assert "dv_requests_total" in m and "dv_request_latency_seconds_bucket" in m
+    rd = c.get("/ready")
+    assert rd.status_code == 200 and rd.json()["ready"] is True
+    assert "block5_conv3" in c.get("/layers").json()["layers"]
+
+
+def test_concurrent_requests_batch(client):
+    """Concurrent requests are coalesced into engine batches and each gets its own answer."""
+    import concurrent.futures as cf
+
+    c, svc = client
+    before = svc.batches
+    imgs = [_img(30 + i, 30, seed=i) for i in range(6)]
+    with cf.ThreadPoolExecutor(6) as ex:
+        rs = list(ex.map(lambda im: c.post("/", data={"file": make_data_url(im, "PNG"), "layer": "block4_conv1"}), imgs))
+    assert all(r.status_code == 200 for r in rs)
+    outs = [_check_url(r.json()) for r in rs]
+    assert not np.array_equal(outs[0], outs[1])
+    assert svc.batches - before <= 6
+
+
+def test_form_parsers():
+    assert parse_urlencoded(b"a=1+2&b=%2B%3D&a=3") == {"a": "1 2", "b": "+="}
+    body, ct = encode_multipart({"file": "data:x;base64,AAA+/=", "layer": "fc1"})
+    assert parse_multipart(body, ct) == {"file": "data:x;base64,AAA+/=", "layer": "fc1"}
+    assert parse_form(body, ct)["layer"] == "fc1"
+    raw = (b"--B\r\nContent-Disposition: form-data; name=\"layer\"\r\n\r\nblock1_pool\r\n"
+           b"--B\r\nContent-Disposition: form-data; name=\"file\"; filename=\"x.txt\"\r\nContent-Type: text/plain\r\n\r\n"
+           b"abc\r\n--B--\r\n")
+    assert parse_form(raw, 'multipart/form-data; boundary="B"') == {"layer": "block1_pool", "file": "abc"}
+
+
+def test_codec_quirks():
+    img = _img(10, 12)
+    url = make_data_url(img, "PNG")
+    # lenient base64: characters outside the alphabet are dropped like base64.b64decode does
+    assert np.array_equal(read_data_url(url.replace("base64,", "base64,\n")), img)
+    gray = Image.fromarray(img[..., 0])
+    buf = io.BytesIO()
+    gray.save(buf, "PNG")
+    g3 = read_data_url("data:image/png;base64," + base64.b64encode(buf.getvalue()).decode())
+    assert g3.shape == (10, 12, 3)
+    rgba = Image.fromarray(np.dstack([img, np.full((10, 12), 7, np.uint8)]), "RGBA")
+    buf = io.BytesIO()
+    rgba.save(buf, "PNG")
+    assert np.array_equal(read_data_url("data:image/png;base64," + base64.b64encode(buf.getvalue()).decode()), img)
+    assert quote("ab+c/d=") == "ab%2Bc/d%3D"
+
+
+def test_resize_oracle_properties():
+    img = _img(448, 448)
+    r = ops.resize_u8_ref(img)  # exact 2x: INTER_AREA fast path
+    ref = ((img[0::2, 0::2].astype(int) + img[0::2, 1::2] + img[1::2, 0::2] + img[1::2, 1::2] + 2) >> 2)
+    assert np.array_equal(r, ref)
+    const = np.full((300, 500, 3), 77, np.uint8)
+    assert (ops.resize_u8_ref(const) == 77).all()
+    up = ops.resize_u8_ref(_img(100, 57))
+    assert up.shape == (224, 224, 3) and up.dtype == np.uint8

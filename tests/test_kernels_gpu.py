@@ -13,14 +13,14 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=["dma", "reg"])
+@pytest.fixture(autouse=True, params=["auto", "reg", "dma"])
 def conv_impl(request):
-    """Run every test against both conv kernels (LDS-DMA and register-staged)."""
+    """Run every test against the automatic kernel choice and the forced register-staged and
+    LDS-DMA kernels (the halo-tile kernel has dedicated tests below)."""
     from deconv_api_amd.ops import conv as C
 
     old = C.get_policy()
-    C.set_policy(impl="auto" if request.param == "dma" else "reg",
-                 unpool="split" if request.param == "dma" else "fused")
+    C.set_policy(impl=request.param)
     yield request.param
     C.set_policy(**old)
 
@@ -117,7 +117,9 @@ def test_conv_unpool_gather(native_lib):
     assert got.shape == (4, 12, 14, 32) and _rel(got, ref) < 1e-2
 
 
-def test_conv_mask_and_transpose(native_lib):
+def test_conv_mask_and_transpose(native_lib, conv_impl):
+    if conv_impl == "dma":
+        pytest.skip("the LDS-DMA kernel has no ReLU-mask prologue (auto routes masks to conv_igemm)")
     g = torch.Generator().manual_seed(6)
     dy = torch.randn(2, 8, 9, 64, generator=g)
     mask = torch.randn(2, 8, 9, 64, generator=g)
@@ -138,6 +140,33 @@ def test_conv_mask_and_transpose(native_lib):
     got = ops.conv2d(gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV), cw.to_device(DEV),
                      relu=False, in_mode="transpose", stride=2, pad=(0, 0), out_hw=(11, 11), use_bias=False)
     assert _rel(got, gx) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,W,C,OC,unpool,epi", [(2, 20, 40, 64, 64, False, "bf16"), (1, 9, 33, 128, 64, True, "bf16"),
+                                                    (3, 16, 64, 64, 3, False, "f32"), (1, 8, 30, 32, 128, True, "bf16"),
+                                                    (2, 12, 12, 64, 16, True, "f32")])
+def test_conv_halo_kernel(native_lib, N, H, W, C, OC, unpool, epi):
+    from deconv_api_amd.ops import conv as Cm
+
+    g = torch.Generator().manual_seed(13)
+    cw = _cw(OC, C, bias=not unpool)
+    kw = dict(relu=True, relu_in=True, epilogue=epi, use_bias=not unpool)
+    if unpool:
+        x = torch.randn(N, H // 2, W // 2, C, generator=g)
+        code = torch.randint(0, 4, (N, H // 2, W // 2, C), generator=g, dtype=torch.uint8)
+        kw.update(in_mode="unpool", code=code)
+    else:
+        x = torch.randn(N, H, W, C, generator=g)
+    ref = ops.conv2d(_bf(x), cw, **kw)
+    if unpool:
+        kw["code"] = code.to(DEV)
+    old = Cm.get_policy()
+    Cm.set_policy(impl="halo")
+    try:
+        got = ops.conv2d(x.to(torch.bfloat16).to(DEV), cw.to_device(DEV), **kw)
+    finally:
+        Cm.set_policy(**old)
+    assert got.shape == ref.shape and _rel(got, ref) < 1e-2
 
 
 def test_conv_channel_slices(native_lib):
