@@ -1,0 +1,15 @@
+# MI355X (gfx950) image for the deconvnet service. The reference's image is python:3.7 + CPU
+# TensorFlow running `uvicorn main:app --port 80` (reference Dockerfile:1-15); this one builds the
+# HIP kernels in-tree and starts one process per visible GPU (rank 0 serves HTTP on port 80).
+FROM rocm/pytorch:latest
+
+ENV HSA_ENABLE_IPC_MODE_LEGACY=0 \
+    PYTORCH_ROCM_ARCH=gfx950 \
+    DV_PORT=80
+WORKDIR /app
+COPY . /app
+RUN python -m deconv_api_amd._build --force
+
+EXPOSE 80
+CMD ["python", "-m", "torch.distributed.run", "--standalone", "--nproc-per-node", "gpu", \
+     "-m", "deconv_api_amd.serve.launch"]

@@ -57,9 +57,12 @@ def load_model(cfg: Config) -> VGG16:
 
 
 class DeconvService:
-    def __init__(self, cfg: Optional[Config] = None, engine: Optional[DeconvNet] = None):
+    def __init__(self, cfg: Optional[Config] = None, engine: Optional[DeconvNet] = None, runner=None):
+        """``runner``: optional parallel.sharded.ShardedRunner (world > 1): batches are then split
+        across all ranks' GPUs and the mosaics all-gathered over RCCL."""
         self.cfg = cfg or Config.from_env()
-        dev = self.cfg.resolve_device()
+        self.runner = runner
+        dev = self.cfg.resolve_device() if runner is None else str(runner.info.device)
         self.device = torch.device(dev)
         if engine is None:
             model = load_model(self.cfg)
@@ -163,9 +166,12 @@ class DeconvService:
 
     def run_batch(self, layer: str, images: List[np.ndarray]) -> np.ndarray:
         t0 = time.perf_counter()
-        x = self.preprocess(images)
-        res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
-        mos = res.mosaic.cpu().numpy()
+        if self.runner is not None:
+            mos = self.runner.run(layer, images)
+        else:
+            x = self.preprocess(images)
+            res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
+            mos = res.mosaic.cpu().numpy()
         dt = time.perf_counter() - t0
         self.batches += 1
         self.images += len(images)
