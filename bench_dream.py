@@ -1,0 +1,90 @@
+#!/usr/bin/env python
+"""DeepDream benchmarks (BASELINE configs 3 and 5; extensions beyond the reference).
+
+  config 3: python bench_dream.py --model inception_v3 --batch 64 --size 299 --octaves 4 --steps 20
+  config 5: python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+                bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 8
+
+One timed run = the whole octave loop (octaves x steps gradient-ascent iterations + octave
+resizes/detail re-injection) over the batch. Prints ONE JSON line (rank 0). Synthetic uint8
+images, seeded random-init weights, bf16 compute.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+
+import torch
+
+from deconv_api_amd import ops
+from deconv_api_amd.engine.deepdream import (RESNET_LAYERS, DeepDream, DreamSettings, TiledDeepDream,
+                                             inception_preprocess)
+from deconv_api_amd.parallel import dist as pdist
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="inception_v3", choices=["inception_v3", "resnet50"])
+    ap.add_argument("--batch", type=int, default=64, help="images (per GPU for untiled; total for tiled)")
+    ap.add_argument("--size", type=int, default=299)
+    ap.add_argument("--octaves", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--tile", type=int, default=0, help="tile size (0 = untiled, hipGraph per octave)")
+    ap.add_argument("--runs", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-graphs", action="store_true")
+    a = ap.parse_args(argv)
+
+    info = pdist.init()
+    dev = info.device
+    ops.native.load()
+    if a.model == "inception_v3":
+        from deconv_api_amd.models.inception_v3 import InceptionV3
+
+        net = InceptionV3(0).build(dev)
+        s = DreamSettings(octaves=a.octaves, iterations=a.steps)
+    else:
+        from deconv_api_amd.models.resnet50 import ResNet50
+
+        net = ResNet50(0).build(dev)
+        s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=a.octaves, iterations=a.steps)
+    if a.tile:
+        dd = TiledDeepDream(net, s, tile=a.tile, info=info)
+    else:
+        dd = DeepDream(net, s, use_graphs=not a.no_graphs)
+    g = torch.Generator(device=dev).manual_seed(7 + info.rank * (0 if a.tile else 1))
+    img = torch.randint(0, 256, (a.batch, a.size, a.size, 3), dtype=torch.uint8, device=dev, generator=g)
+    x = inception_preprocess(img)
+    t0 = time.perf_counter()
+    for _ in range(a.warmup):
+        dd.run(x)
+    torch.cuda.synchronize()
+    print(f"[rank {info.rank}] warmup (incl. graph capture) {time.perf_counter() - t0:.1f}s", file=sys.stderr)
+    pdist.barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.runs):
+        out = dd.run(x)
+    torch.cuda.synchronize()
+    pdist.barrier(info)
+    el = pdist.all_reduce_max(time.perf_counter() - t0, info)
+    per_run = el / a.runs
+    imgs = a.batch * (1 if a.tile else info.world)
+    if info.is_main:
+        print(json.dumps({
+            "metric": f"DeepDream images/sec ({a.model}, {a.octaves} octaves x {a.steps} steps)",
+            "value": round(imgs / per_run, 3), "unit": "images/s", "n_gpus": info.world,
+            "s_per_dream_batch": round(per_run, 3), "runs": a.runs, "warmup": a.warmup,
+            "higher_is_better": True, "scaling": "strong" if a.tile else "weak", "dtype": "bf16",
+            "data": "synthetic uint8 images, seeded random-init weights", "hip_graphs": not a.no_graphs and not a.tile,
+            "finite": bool(torch.isfinite(out).all()),
+            "config": {"model": a.model, "batch": a.batch, "image_size": a.size, "tile": a.tile,
+                       "parallelism": f"{'tiles' if a.tile else 'dp'}{info.world}"},
+        }), flush=True)
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

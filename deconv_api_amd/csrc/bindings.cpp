@@ -149,6 +149,31 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   }
 }
 
+// kind 0 max / 1 avg; dir 0 fwd (in=x, out=y) / 1 bwd (in=gy, out=gx); geom = N,H,W,C,OH,OW,k,s,pad
+void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_t dir, std::vector<int64_t> g) {
+  check_cuda(in, "in");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(in.device());
+  TORCH_CHECK(g.size() == 9, "pool: geometry");
+  const int64_t N = g[0], H = g[1], W = g[2], C = g[3], OH = g[4], OW = g[5], k = g[6], s = g[7], pad = g[8];
+  TORCH_CHECK(C % 8 == 0 && k >= 1 && s >= 1 && pad >= 0 && pad < k, "pool: C%8, k, s, pad");
+  TORCH_CHECK(OH == (H + 2 * pad - k) / s + 1 && OW == (W + 2 * pad - k) / s + 1, "pool: output size");
+  TORCH_CHECK(in.scalar_type() == at::kBFloat16 && in.is_contiguous() && out.scalar_type() == at::kBFloat16 &&
+                  out.is_contiguous(),
+              "pool: bf16 contiguous tensors");
+  const int64_t small = N * OH * OW * C, big = N * H * W * C;
+  TORCH_CHECK(in.numel() == (dir == 0 ? big : small) && out.numel() == (dir == 0 ? small : big), "pool: sizes");
+  uint8_t* ip = nullptr;
+  if (kind == 0) {
+    TORCH_CHECK(idx.has_value() && idx->scalar_type() == at::kByte && idx->is_contiguous() && idx->numel() == small,
+                "maxpool: idx [N,OH,OW,C] u8");
+    ip = idx->data_ptr<uint8_t>();
+  }
+  check_rc(dv::pool_launch((int)kind, (int)dir, reinterpret_cast<const uint16_t*>(in.data_ptr()),
+                           reinterpret_cast<uint16_t*>(out.data_ptr()), ip, (int)N, (int)H, (int)W, (int)C, (int)OH,
+                           (int)OW, (int)k, (int)s, (int)pad, cur_stream()),
+           "pool");
+}
+
 void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -262,6 +287,7 @@ void unpool2x2(Tensor p, Tensor code, Tensor out, int64_t code_div, bool relu) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "deconv_api_amd gfx950 (MI355X) HIP kernels";
   m.def("conv", &conv, "MFMA implicit-GEMM conv (fwd / unpool-gather / transposed; bf16/pool/f32 epilogues)");
+  m.def("pool", &pool, "k x k max/avg pooling forward/backward");
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);
   m.def("seed_deconv3x3", &seed_deconv3x3);

@@ -66,6 +66,10 @@ int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int 
 }  // namespace dv
 
 namespace dv {
+// k x k pooling (pool.hip). kind 0 max (idx = uint8 window position), 1 avg (count_include_pad=0);
+// dir 0 forward (in = x [N,H,W,C], out = y [N,OH,OW,C]), 1 backward (in = gy, out = gx)
+int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C,
+                int OH, int OW, int k, int s, int pad, hipStream_t st);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s);
 }  // namespace dv

@@ -1,0 +1,201 @@
+// k x k pooling forward/backward for the DeepDream networks (InceptionV3 / ResNet-50), NHWC bf16,
+// one thread per (pixel, 8-channel chunk): 16-B loads/stores throughout.
+//   maxpool fwd: first-max (row-major) argmax kept as a uint8 window position per element;
+//   maxpool bwd: gather form (no atomics): each input pixel sums the gradients of the (at most
+//                ceil(k/s)^2) windows that contain it and chose it;
+//   avgpool fwd/bwd: count_include_pad = false (TF/Keras 'same' semantics).
+#include "common.h"
+#include "kernels.h"
+
+namespace dv {
+
+struct PoolGeom {
+  int N, H, W, C, OH, OW, k, s, pad;
+};
+
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, PoolGeom g) {
+  const int cpp = g.C >> 3;
+  const long long total = (long long)g.N * g.OH * g.OW * cpp;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int ch = (int)(t % cpp);
+    const long long pix = t / cpp;
+    const int ow = (int)(pix % g.OW);
+    const int oh = (int)((pix / g.OW) % g.OH);
+    const long long n = pix / ((long long)g.OW * g.OH);
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      bi[e] = 0;
+    }
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int ih = oh * g.s - g.pad + kh;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int iw = ow * g.s - g.pad + kw;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.C + ch * 8);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        const int pos = kh * g.k + kw;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = bf2f((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+          if (f > best[e]) {
+            best[e] = f;
+            bi[e] = pos;
+          }
+        }
+      }
+    }
+    uint4 o;
+    o.x = pack_bf2(best[0], best[1]);
+    o.y = pack_bf2(best[2], best[3]);
+    o.z = pack_bf2(best[4], best[5]);
+    o.w = pack_bf2(best[6], best[7]);
+    *reinterpret_cast<uint4*>(y + pix * g.C + ch * 8) = o;
+    uint2 ix;
+    ix.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    ix.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(idx + pix * g.C + ch * 8) = ix;
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __restrict__ gy, const uint8_t* __restrict__ idx,
+                                                          uint16_t* __restrict__ gx, PoolGeom g) {
+  const int cpp = g.C >> 3;
+  const long long total = (long long)g.N * g.H * g.W * cpp;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int ch = (int)(t % cpp);
+    const long long pix = t / cpp;
+    const int w = (int)(pix % g.W);
+    const int h = (int)((pix / g.W) % g.H);
+    const long long n = pix / ((long long)g.W * g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // windows containing (h, w): oh*s - pad <= h <= oh*s - pad + k - 1
+    const int oh_lo = max(0, (h + g.pad - g.k + g.s) / g.s), oh_hi = min(g.OH - 1, (h + g.pad) / g.s);
+    const int ow_lo = max(0, (w + g.pad - g.k + g.s) / g.s), ow_hi = min(g.OW - 1, (w + g.pad) / g.s);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int kh = h + g.pad - oh * g.s;
+      if (kh < 0 || kh >= g.k) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int kw = w + g.pad - ow * g.s;
+        if (kw < 0 || kw >= g.k) continue;
+        const uint32_t pos = (uint32_t)(kh * g.k + kw);
+        const long long o = ((n * g.OH + oh) * g.OW + ow) * g.C + ch * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(gy + o);
+        const uint2 ix = *reinterpret_cast<const uint2*>(idx + o);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t ie = ((e < 4 ? ix.x : ix.y) >> (8 * (e & 3))) & 0xFFu;
+          if (ie == pos) acc[e] += bf2f((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+        }
+      }
+    }
+    uint4 o;
+    o.x = pack_bf2(acc[0], acc[1]);
+    o.y = pack_bf2(acc[2], acc[3]);
+    o.z = pack_bf2(acc[4], acc[5]);
+    o.w = pack_bf2(acc[6], acc[7]);
+    *reinterpret_cast<uint4*>(gx + pix * g.C + ch * 8) = o;
+  }
+}
+
+__device__ __forceinline__ int win_count(int o, int s, int pad, int k, int L) {
+  const int lo = max(0, o * s - pad), hi = min(L - 1, o * s - pad + k - 1);
+  return hi - lo + 1;
+}
+
+__global__ void __launch_bounds__(256) avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                          PoolGeom g) {
+  const int cpp = g.C >> 3;
+  const long long total = (long long)g.N * g.OH * g.OW * cpp;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int ch = (int)(t % cpp);
+    const long long pix = t / cpp;
+    const int ow = (int)(pix % g.OW);
+    const int oh = (int)((pix / g.OW) % g.OH);
+    const long long n = pix / ((long long)g.OW * g.OH);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int ih = oh * g.s - g.pad + kh;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int iw = ow * g.s - g.pad + kw;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.C + ch * 8);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf2f((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+      }
+    }
+    const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, g.k, g.H) * win_count(ow, g.s, g.pad, g.k, g.W));
+    uint4 o;
+    o.x = pack_bf2(acc[0] * inv, acc[1] * inv);
+    o.y = pack_bf2(acc[2] * inv, acc[3] * inv);
+    o.z = pack_bf2(acc[4] * inv, acc[5] * inv);
+    o.w = pack_bf2(acc[6] * inv, acc[7] * inv);
+    *reinterpret_cast<uint4*>(y + pix * g.C + ch * 8) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __restrict__ gy, uint16_t* __restrict__ gx,
+                                                          PoolGeom g) {
+  const int cpp = g.C >> 3;
+  const long long total = (long long)g.N * g.H * g.W * cpp;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int ch = (int)(t % cpp);
+    const long long pix = t / cpp;
+    const int w = (int)(pix % g.W);
+    const int h = (int)((pix / g.W) % g.H);
+    const long long n = pix / ((long long)g.W * g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int oh_lo = max(0, (h + g.pad - g.k + g.s) / g.s), oh_hi = min(g.OH - 1, (h + g.pad) / g.s);
+    const int ow_lo = max(0, (w + g.pad - g.k + g.s) / g.s), ow_hi = min(g.OW - 1, (w + g.pad) / g.s);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int kh = h + g.pad - oh * g.s;
+      if (kh < 0 || kh >= g.k) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int kw = w + g.pad - ow * g.s;
+        if (kw < 0 || kw >= g.k) continue;
+        const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, g.k, g.H) * win_count(ow, g.s, g.pad, g.k, g.W));
+        const uint4 v = *reinterpret_cast<const uint4*>(gy + ((n * g.OH + oh) * g.OW + ow) * g.C + ch * 8);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += inv * bf2f((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+      }
+    }
+    uint4 o;
+    o.x = pack_bf2(acc[0], acc[1]);
+    o.y = pack_bf2(acc[2], acc[3]);
+    o.z = pack_bf2(acc[4], acc[5]);
+    o.w = pack_bf2(acc[6], acc[7]);
+    *reinterpret_cast<uint4*>(gx + pix * g.C + ch * 8) = o;
+  }
+}
+
+static unsigned grid_for(long long total) {
+  return (unsigned)std::min<long long>((total + 255) / 256, 256LL * 32);
+}
+
+int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C, int OH,
+                int OW, int k, int s, int pad, hipStream_t st) {
+  if (C % 8 != 0 || k <= 0 || s <= 0 || k > 15) return -1;
+  PoolGeom g{N, H, W, C, OH, OW, k, s, pad};
+  const long long out_total = (long long)N * OH * OW * (C / 8), in_total = (long long)N * H * W * (C / 8);
+  if (kind == 0 && dir == 0)
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(out_total)), dim3(256), 0, st, in, out, idx, g);
+  else if (kind == 0 && dir == 1)
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(in_total)), dim3(256), 0, st, in, idx, out, g);
+  else if (kind == 1 && dir == 0)
+    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for(out_total)), dim3(256), 0, st, in, out, g);
+  else if (kind == 1 && dir == 1)
+    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(in_total)), dim3(256), 0, st, in, out, g);
+  else
+    return -2;
+  return (int)hipGetLastError();
+}
+
+}  // namespace dv

@@ -1,0 +1,222 @@
+"""DeepDream octave gradient ascent (BASELINE configs 3 and 5; NOT in the reference — the file
+named deepdream.py there holds the deconvnet). Specification from the canonical
+Keras ``examples/deep_dream.py``:
+
+  loss  = sum_l coeff_l * sum(act_l[:, 2:-2, 2:-2, :]^2) / numel(act_l)   (per image)
+  grad  = d loss / d x, normalized by max(mean|grad|, 1e-7)                (per image)
+  x    += step * grad   (step 0.01, 20 iterations per octave, max_loss 10 early stop)
+  octaves: successive shapes original / 1.4^i (smallest first); after each octave the detail
+  lost by downscaling is re-injected: x += resize(orig, s) - resize(resize(orig, s0), s).
+
+MI355X design:
+  * the network runs on the HIP kernels through differentiable units (ops/autograd.py): conv
+    fwd with ReLU epilogue, dgrad with the ReLU mask fused into the A prologue, pooling fwd/bwd;
+    only the input gradient is computed (weights frozen);
+  * one gradient-ascent step (forward, loss, backward, normalization, masked update) is captured
+    into a hipGraph per octave shape (torch.cuda.CUDAGraph) and replayed ``iterations`` times —
+    no host work or sync inside an octave;
+  * ``max_loss`` is evaluated on device: an image stops updating once its loss exceeded it
+    (the per-image equivalent of the example's ``break``), so the graph has no host branch.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
+
+
+@dataclass
+class DreamSettings:
+    layers: Dict[str, float] = field(default_factory=lambda: dict(DEFAULT_LAYERS))
+    step: float = 0.01
+    octaves: int = 4
+    octave_scale: float = 1.4
+    iterations: int = 20
+    max_loss: Optional[float] = 10.0
+    border: int = 2  # act[:, 2:-2, 2:-2, :]
+
+
+def resize(x: torch.Tensor, hw: Tuple[int, int]) -> torch.Tensor:
+    """NHWC bilinear resize with corner alignment (scipy.ndimage.zoom order=1 in the example)."""
+    if tuple(x.shape[1:3]) == tuple(hw):
+        return x
+    y = F.interpolate(x.permute(0, 3, 1, 2), size=hw, mode="bilinear", align_corners=True)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def inception_preprocess(img_u8: torch.Tensor) -> torch.Tensor:
+    return img_u8.float() / 127.5 - 1.0
+
+
+def inception_deprocess(x: torch.Tensor) -> torch.Tensor:
+    return ((x / 2.0 + 0.5) * 255.0).clamp(0, 255).to(torch.uint8)
+
+
+class DeepDream:
+    def __init__(self, net, settings: Optional[DreamSettings] = None, use_graphs: bool = True, dtype=None):
+        self.net = net
+        self.s = settings or DreamSettings()
+        self.device = net.device
+        self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self._graphs: Dict[tuple, tuple] = {}
+
+    # ------------------------------------------------------------------ one step
+    def _net_input(self, x: torch.Tensor) -> torch.Tensor:
+        return F.pad(x, (0, 5)).to(self.dtype)
+
+    def loss(self, acts: Dict[str, torch.Tensor]) -> torch.Tensor:
+        b = self.s.border
+        total = None
+        for name, coeff in self.s.layers.items():
+            a = acts[name]
+            core = a[:, b:a.shape[1] - b, b:a.shape[2] - b, :].float()
+            term = coeff * (core * core).sum(dim=(1, 2, 3)) / float(a[0].numel())
+            total = term if total is None else total + term
+        return total
+
+    def loss_and_grad(self, x: torch.Tensor):
+        """x: fp32 [B, H, W, 3] (preprocessed). Returns (loss [B], normalized grad [B, H, W, 3])."""
+        xin = self._net_input(x).requires_grad_(True)
+        acts = self.net.forward(xin, list(self.s.layers.keys()))
+        loss = self.loss(acts)
+        (g,) = torch.autograd.grad(loss.sum(), xin)
+        g = g[..., :3].float()
+        g = g / g.abs().mean(dim=(1, 2, 3), keepdim=True).clamp_min(1e-7)
+        return loss.detach(), g
+
+    def _step(self, x: torch.Tensor, done: torch.Tensor) -> torch.Tensor:
+        loss, g = self.loss_and_grad(x)
+        if self.s.max_loss is not None:
+            done |= loss > self.s.max_loss
+        x.add_(g * ((~done).to(g.dtype) * self.s.step).view(-1, 1, 1, 1))
+        return loss
+
+    # ------------------------------------------------------------------ hipGraph per shape
+    def _graph(self, B: int, hw: Tuple[int, int]):
+        key = (B, tuple(hw))
+        if key in self._graphs:
+            return self._graphs[key]
+        x = torch.zeros(B, *hw, 3, device=self.device)
+        done = torch.zeros(B, dtype=torch.bool, device=self.device)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up allocator / autograd on a side stream before capture
+                self._step(x, done)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self._step(x, done)
+        self._graphs[key] = (g, x, done, loss)
+        return self._graphs[key]
+
+    def gradient_ascent(self, x: torch.Tensor) -> torch.Tensor:
+        B, H, W, _ = x.shape
+        if self.use_graphs:
+            g, gx, gdone, gloss = self._graph(B, (H, W))
+            gx.copy_(x)
+            gdone.zero_()
+            for _ in range(self.s.iterations):
+                g.replay()
+            return gx.clone()
+        x = x.clone()
+        done = torch.zeros(B, dtype=torch.bool, device=x.device)
+        for _ in range(self.s.iterations):
+            self._step(x, done)
+        return x
+
+    # ------------------------------------------------------------------ octaves
+    def octave_shapes(self, H: int, W: int) -> List[Tuple[int, int]]:
+        shapes = [(H, W)]
+        for i in range(1, self.s.octaves):
+            shapes.append((int(H / self.s.octave_scale ** i), int(W / self.s.octave_scale ** i)))
+        return shapes[::-1]
+
+    def run(self, x: torch.Tensor) -> torch.Tensor:
+        """x: preprocessed fp32 [B, H, W, 3] on the engine device -> dreamed fp32 image."""
+        shapes = self.octave_shapes(x.shape[1], x.shape[2])
+        original = x
+        shrunk = resize(original, shapes[0])
+        img = x
+        for hw in shapes:
+            img = resize(img, hw)
+            img = self.gradient_ascent(img)
+            upscaled = resize(shrunk, hw)
+            same = resize(original, hw)
+            img = img + (same - upscaled)
+            shrunk = resize(original, hw)
+        return img
+
+    def dream_u8(self, img_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 RGB [B, H, W, 3] -> uint8 dreamed image."""
+        x = inception_preprocess(img_u8.to(self.device))
+        return inception_deprocess(self.run(x))
+
+
+RESNET_LAYERS = {"conv3_block4_out": 0.5, "conv4_block3_out": 1.0, "conv4_block6_out": 1.5}
+
+
+class TiledDeepDream(DeepDream):
+    """Large-image DeepDream: every gradient step rolls the image by a random offset (shared seed,
+    identical on every rank), cuts it into ``tile`` x ``tile`` tiles, computes each tile's input
+    gradient independently (tiles are assigned round-robin to ranks — the image-domain analogue of
+    context parallelism), assembles the full gradient with one all-reduce (each tile
+    has exactly one owner, so the sum is the stitch), un-rolls it, normalizes it by the global
+    per-image mean |g| and applies the same update on every rank."""
+
+    def __init__(self, net, settings: Optional[DreamSettings] = None, tile: int = 512, info=None, seed: int = 0,
+                 dtype=None):
+        super().__init__(net, settings, use_graphs=False, dtype=dtype)
+        self.tile = tile
+        self.info = info
+        self.gen = torch.Generator().manual_seed(seed)
+
+    def _tiles(self, H: int, W: int):
+        t = self.tile
+        out = []
+        for y in range(0, H, t):
+            for x in range(0, W, t):
+                out.append((y, min(y + t, H), x, min(x + t, W)))
+        return out
+
+    def gradient_ascent(self, x: torch.Tensor) -> torch.Tensor:
+        import torch.distributed as dist
+
+        from ..parallel.dist import barrier  # noqa: F401  (imported for side-effect free use)
+
+        B, H, W, _ = x.shape
+        x = x.clone()
+        done = torch.zeros(B, dtype=torch.bool, device=x.device)
+        world = self.info.world if self.info is not None else 1
+        rank = self.info.rank if self.info is not None else 0
+        tiles = self._tiles(H, W)
+        for _ in range(self.s.iterations):
+            sy = int(torch.randint(-self.tile // 2, self.tile // 2 + 1, (1,), generator=self.gen))
+            sx = int(torch.randint(-self.tile // 2, self.tile // 2 + 1, (1,), generator=self.gen))
+            rolled = torch.roll(x, shifts=(sy, sx), dims=(1, 2))
+            grad = torch.zeros_like(x)
+            loss = torch.zeros(B, device=x.device)
+            for ti, (y0, y1, x0, x1) in enumerate(tiles):
+                if ti % world != rank:
+                    continue
+                xt = rolled[:, y0:y1, x0:x1].contiguous()
+                xin = self._net_input(xt).requires_grad_(True)
+                acts = self.net.forward(xin, list(self.s.layers.keys()))
+                lt = self.loss(acts)
+                (g,) = torch.autograd.grad(lt.sum(), xin)
+                grad[:, y0:y1, x0:x1] = g[..., :3].float()
+                loss += lt.detach()
+            if world > 1:
+                dist.all_reduce(grad)
+                dist.all_reduce(loss)
+            grad = torch.roll(grad, shifts=(-sy, -sx), dims=(1, 2))
+            grad = grad / grad.abs().mean(dim=(1, 2, 3), keepdim=True).clamp_min(1e-7)
+            if self.s.max_loss is not None:
+                done |= loss > self.s.max_loss * len(tiles)
+            x.add_(grad * ((~done).to(grad.dtype) * self.s.step).view(-1, 1, 1, 1))
+        return x

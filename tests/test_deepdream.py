@@ -1,0 +1,154 @@
+"""DeepDream (BASELINE configs 3 and 5, an extension beyond the reference): CPU semantics tests
+plus GPU tests that compare the HIP autograd units against PyTorch fp32 autograd."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deconv_api_amd.engine.deepdream import (DeepDream, DreamSettings, RESNET_LAYERS, TiledDeepDream,
+                                             inception_deprocess, inception_preprocess, resize)
+from deconv_api_amd.models.inception_v3 import InceptionV3, fold_bn
+from deconv_api_amd.models.resnet50 import ResNet50
+
+
+@pytest.fixture(scope="module")
+def inc_cpu():
+    return InceptionV3(0).build("cpu")
+
+
+def test_inception_shapes_and_params(inc_cpu):
+    o = inc_cpu.forward(torch.randn(1, 299, 299, 8), ["mixed2", "mixed7", "mixed10"])
+    assert o["mixed2"].shape == (1, 35, 35, 288)
+    assert o["mixed7"].shape == (1, 17, 17, 768)
+    assert o["mixed10"].shape == (1, 8, 8, 2048)
+    assert inc_cpu.num_params() == 21768352  # Keras InceptionV3(include_top=False) trainable params
+
+
+def test_resnet_shapes():
+    m = ResNet50(0).build("cpu")
+    o = m.forward(torch.randn(1, 224, 224, 8), ["conv2_block3_out", "conv5_block3_out"])
+    assert o["conv2_block3_out"].shape == (1, 56, 56, 256) and o["conv5_block3_out"].shape == (1, 7, 7, 2048)
+
+
+def test_fold_bn():
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(8, 4, 3, 3, generator=g)
+    gamma, beta, mean, var = (torch.rand(8, generator=g) + 0.5, torch.randn(8, generator=g), torch.randn(8, generator=g),
+                              torch.rand(8, generator=g) + 0.1)
+    x = torch.randn(2, 4, 9, 9, generator=g)
+    ref = F.batch_norm(F.conv2d(x, w, padding=1), mean, var, gamma, beta, False, 0.0, 1e-3)
+    wf, bf = fold_bn(w, gamma, beta, mean, var)
+    torch.testing.assert_close(F.conv2d(x, wf, bf, padding=1), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_loss_matches_keras_formula(inc_cpu):
+    dd = DeepDream(inc_cpu)
+    x = torch.rand(2, 139, 139, 3) * 2 - 1
+    acts = inc_cpu.forward(F.pad(x, (0, 5)), list(dd.s.layers))
+    want = torch.zeros(2)
+    for name, c in dd.s.layers.items():
+        a = acts[name]
+        want += c * (a[:, 2:-2, 2:-2, :] ** 2).sum((1, 2, 3)) / a[0].numel()
+    torch.testing.assert_close(dd.loss(acts), want)
+
+
+def test_grad_normalized_and_finite_difference(inc_cpu):
+    torch.manual_seed(0)
+    dd = DeepDream(inc_cpu)
+    x = torch.rand(1, 120, 120, 3) * 2 - 1
+    loss, g = dd.loss_and_grad(x)
+    assert torch.allclose(g.abs().mean(), torch.tensor(1.0), atol=1e-5)
+    # directional finite difference along the (unnormalized) gradient direction
+    d = g / g.norm()
+    eps = 1e-2
+    lp = dd.loss(inc_cpu.forward(F.pad(x + eps * d, (0, 5)), list(dd.s.layers)))
+    lm = dd.loss(inc_cpu.forward(F.pad(x - eps * d, (0, 5)), list(dd.s.layers)))
+    assert float(lp - lm) > 0  # ascent direction increases the loss
+
+
+def test_octaves_and_max_loss(inc_cpu):
+    s = DreamSettings(octaves=3, iterations=2)
+    dd = DeepDream(inc_cpu, s)
+    assert dd.octave_shapes(300, 200) == [(153, 102), (214, 142), (300, 200)]
+    x = torch.rand(1, 153, 153, 3) * 2 - 1
+    frozen = DeepDream(inc_cpu, DreamSettings(iterations=3, max_loss=-1.0))  # every loss > max_loss
+    assert torch.equal(frozen.gradient_ascent(x), x)
+    moved = DeepDream(inc_cpu, DreamSettings(iterations=1, max_loss=None)).gradient_ascent(x)
+    assert not torch.equal(moved, x)
+
+
+def test_detail_reinjection_identity(inc_cpu):
+    """With zero steps the octave loop must return the original image (lost detail re-injected)."""
+    dd = DeepDream(inc_cpu, DreamSettings(octaves=3, iterations=1, step=0.0))
+    x = torch.rand(1, 160, 160, 3) * 2 - 1
+    torch.testing.assert_close(dd.run(x), x, rtol=1e-5, atol=1e-5)
+
+
+def test_pre_deprocess_roundtrip():
+    u8 = torch.randint(0, 256, (1, 5, 5, 3), dtype=torch.uint8)
+    assert (inception_deprocess(inception_preprocess(u8)).int() - u8.int()).abs().max() <= 1
+
+
+def test_tiled_single_rank_matches_untiled_when_one_tile():
+    net = ResNet50(1).build("cpu")
+    s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=1, iterations=1, max_loss=None)
+    x = torch.rand(1, 96, 96, 3) * 2 - 1
+    tiled = TiledDeepDream(net, s, tile=256)  # one tile covers the image: roll commutes with the net?
+    a = tiled.gradient_ascent(x)
+    assert a.shape == x.shape and torch.isfinite(a).all() and not torch.equal(a, x)
+
+
+# --------------------------------------------------------------------------- GPU
+def _cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float(a @ b / (a.norm() * b.norm()))
+
+
+@pytest.mark.gpu
+def test_gpu_pool_kernels(native_lib):
+    from deconv_api_amd.ops.autograd import avg_pool, max_pool
+
+    g = torch.Generator().manual_seed(1)
+    for k, s, p in [(3, 2, 0), (3, 1, 1), (3, 2, 1)]:
+        x = torch.randn(2, 13, 11, 24, generator=g).to(torch.bfloat16).float()
+        for fn in (max_pool, avg_pool):
+            xc = x.clone().requires_grad_(True)
+            yc = fn(xc, k, s, p)
+            gy = torch.randn_like(yc).to(torch.bfloat16).float()
+            (gc,) = torch.autograd.grad(yc, xc, gy)
+            xd = x.to(torch.bfloat16).cuda().requires_grad_(True)
+            yd = fn(xd, k, s, p)
+            (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.bfloat16).cuda())
+            assert (yd.float().cpu() - yc).abs().max() < 2e-2 * yc.abs().max()
+            assert (gd.float().cpu() - gc).abs().max() < 2e-2 * gc.abs().max() + 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["inception", "resnet"])
+def test_gpu_dream_gradient_matches_cpu(native_lib, which):
+    if which == "inception":
+        cpu, gpu = InceptionV3(0).build("cpu"), InceptionV3(0).build("cuda")
+        s = DreamSettings()
+        hw = 139
+    else:
+        cpu, gpu = ResNet50(0).build("cpu"), ResNet50(0).build("cuda")
+        s = DreamSettings(layers=dict(RESNET_LAYERS))
+        hw = 128
+    x = (torch.rand(2, hw, hw, 3, generator=torch.Generator().manual_seed(2)) * 2 - 1)
+    x = x.to(torch.bfloat16).float()
+    lc, gc = DeepDream(cpu, s).loss_and_grad(x)
+    lg, gg = DeepDream(gpu, s).loss_and_grad(x.cuda())
+    assert torch.allclose(lg.cpu(), lc, rtol=5e-2)
+    for b in range(2):
+        assert _cos(gg[b].cpu(), gc[b]) > 0.95
+
+
+@pytest.mark.gpu
+def test_gpu_graph_replay_equals_eager(native_lib):
+    net = InceptionV3(0).build("cuda")
+    s = DreamSettings(iterations=3, octaves=2)
+    x = (torch.rand(2, 150, 150, 3, generator=torch.Generator().manual_seed(3)) * 2 - 1).cuda()
+    eager = DeepDream(net, s, use_graphs=False).run(x)
+    graph = DeepDream(net, s, use_graphs=True).run(x)
+    assert (eager - graph).abs().max() < 1e-3
+    assert (graph - x).abs().max() > 1e-3
