@@ -112,12 +112,11 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   //  * LDS-DMA: FWD / TRANSPOSE without mask; an unpool input is first materialized (vector kernel)
   //  * register-staged: everything else (ReLU-mask prologue, fused unpool gather)
   const bool halo_ok = (amode == dv::CONV_A_FWD || amode == dv::CONV_A_UNPOOL) && a.KH == 3 && a.KW == 3 &&
-                       a.stride == 1 && a.pad_h == 1 && a.pad_w == 1 && a.C % 32 == 0 && a.H == a.OH &&
+                       a.stride == 1 && a.pad_h == 1 && a.pad_w == 1 && a.C == 64 && a.H == a.OH &&
                        a.W == a.OW && !a.accumulate && !mask.has_value() &&
-                       (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad % 64 == 0);
-  // measured on MI355X (profiles/layers_r1_*.txt): the per-tile weight restage makes the halo kernel
-  // slower than LDS-DMA on every VGG shape so far, so it is opt-in (impl 3) until it is persistent
-  const bool halo_auto = false;
+                       (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad == 64);
+  // persistent weight-resident halo kernel: 64-channel inputs at large maps (block1 of VGG16)
+  const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112;
   if (impl == 3 || (impl == 0 && halo_auto)) {
     TORCH_CHECK(halo_ok, "conv: halo-tile kernel does not support this shape/mode");
     check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream()), "conv_halo");

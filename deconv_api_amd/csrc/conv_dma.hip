@@ -8,19 +8,24 @@
 //     for free from the buffer descriptor's range check (an out-of-range offset returns 0);
 //   * 8 waves per workgroup, each owning a (16*FM) x (16*FN) C tile (up to 128 x 64, i.e.
 //     256 x 256 per workgroup), so each ds_read_b128 fragment feeds FN (or FM) MFMAs;
-//   * the LDS image is lane-linear per DMA instruction (8 rows x 128 B); the st_16x32-style XOR
-//     swizzle (chunk ^ (row & 7)) is applied to the per-lane SOURCE address and to the fragment
-//     read address, never to the DMA destination (cdna_hip_programming.md rule 21);
-//   * two LDS stages, one barrier per 64-deep K tile: the DMA for tile t+1 is in flight while
-//     the MFMAs of tile t run (raw s_barrier + explicit vmcnt, so the prefetch is not drained).
+//   * the LDS image is lane-linear per DMA instruction (1 KiB = 1024/(2*BK) rows); the XOR
+//     swizzle is applied to the per-lane SOURCE chunk and to the fragment read address, never
+//     to the DMA destination (cdna_hip_programming.md rule 21). BK=64 rows (128 B): chunk ^
+//     (row & 7). BK=32 rows (64 B): chunk ^ ((4 - ((row >> 2) & 3)) & 3), which puts the 16
+//     rows x 4 chunks of every ds_read_b128 lane group of a 16x16x32 fragment read on distinct
+//     16-B bank slots (derivation in docs/KERNELS.md);
+//   * STAGES-deep LDS ring, one barrier per K tile: the DMA for tile t+STAGES-1 is issued right
+//     after the barrier of tile t and a counted `s_waitcnt vmcnt(N)` leaves the younger tiles in
+//     flight across the barrier (raw s_barrier, never __syncthreads, so nothing drains them).
 #include "common.h"
 #include "kernels.h"
+
+#include <cstdlib>
 
 namespace dv {
 
 namespace {
 
-constexpr int kBK = 64;
 constexpr uint32_t kOOB = 0x80000000u;  // any offset >= num_records reads as zero
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -34,25 +39,42 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nrec, 0x00020000);
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// swizzle term of LDS row `row` for a BK-wide tile
+template <int BK>
+__device__ __forceinline__ int row_xor(int row) {
+  if constexpr (BK == 64)
+    return row & 7;
+  else
+    return (4 - ((row >> 2) & 3)) & 3;
+}
+
 }  // namespace
 
 template <int FM, int FN, int EPI, bool accum>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane);
 
-template <int WM, int WN, int FM, int FN, int AMODE, int EPI, bool CALIGNED>
+template <int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED>
 __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a, int tiles_n) {
   constexpr int NW = WM * WN;
-  constexpr int NT = NW * 64;
   constexpr int BM = WM * FM * 16;
   constexpr int BN = WN * FN * 16;
-  constexpr int A_BYTES = BM * 128;
-  constexpr int B_BYTES = BN * 128;
+  constexpr int ROWB = BK * 2;              // LDS bytes per row
+  constexpr int CPR = BK / 8;               // 16-B chunks per row
+  constexpr int RPI = 1024 / ROWB;          // rows per DMA instruction
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int B_BYTES = BN * ROWB;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int A_I = BM / 8 / NW;                  // A DMA instructions per wave per K tile
-  constexpr int B_ROWGROUPS = BN / 8;               // 8-row groups of the B tile
-  constexpr int B_I = (B_ROWGROUPS + NW - 1) / NW;  // B DMA instructions per wave (some waves idle)
-  static_assert(A_I >= 1 && BM % (8 * NW) == 0, "BM must cover every wave");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+  constexpr int A_I = BM / RPI / NW;        // A DMA instructions per wave per K tile
+  constexpr int B_GROUPS = BN / RPI;        // RPI-row groups of the B tile
+  constexpr int B_FULL = B_GROUPS / NW, B_REM = B_GROUPS % NW;
+  static_assert(A_I >= 1 && BM % (RPI * NW) == 0, "BM must cover every wave");
+  static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[STAGES * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -79,16 +101,15 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(xb, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
 
-  // lane -> (row within its 8-row group, logical 16-B chunk): the DMA writes position lane&7 of
-  // row lane>>3; the swizzled image stores logical chunk c at position c ^ (row & 7).
-  const int lrow = lane >> 3;
-  const int lchunk = (lane & 7) ^ lrow;
+  // lane -> (row within its DMA row group, logical 16-B chunk at LDS position lane % CPR)
+  const int lrow = lane / CPR;
+  const int lchunk = (lane % CPR) ^ row_xor<BK>(lrow);  // group bases are multiples of 16 rows
 
   // ---- per-row A gather state (rows fixed for the whole K loop) ----
   int r_off[A_I], r_h[A_I], r_w[A_I];
 #pragma unroll
   for (int j = 0; j < A_I; ++j) {
-    const int row = (j * NW + wave) * 8 + lrow;
+    const int row = (j * NW + wave) * RPI + lrow;
     const int gm = m0 + row;
     int n, oh, ow;
     const int g = gm < a.M ? gm : 0;
@@ -118,28 +139,57 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
     r_off[j] = (n - n_base) * H * W;  // pixel index of the image's first pixel, relative to base
     if (gm >= a.M) r_h[j] = -(1 << 28);  // never in bounds
   }
+  // Fast path (forward convs with <= 32 taps): per row, a tap-validity bitmask and the element
+  // offset of tap (0,0); per K tile the gather is then mask-test + add (the uniform tap delta).
+  // measured: neutral on K>=2304 layers, and its per-row prologue costs 20-40% on K=576 layers
+  // (profiles/layers_r1_fastmask.txt), so it is compiled out
+  constexpr bool FAST = false;
+  const bool fast = FAST && a.KH * a.KW <= 32;
+  uint32_t r_mask[A_I];
+  int r_base[A_I];
+#pragma unroll
+  for (int j = 0; j < A_I; ++j) {
+    uint32_t m = 0;
+    if (fast) {
+      for (int kh = 0; kh < a.KH; ++kh) {
+        const bool okh = (unsigned)(r_h[j] + kh) < (unsigned)H;
+        for (int kw = 0; kw < a.KW; ++kw)
+          if (okh && (unsigned)(r_w[j] + kw) < (unsigned)W) m |= 1u << (kh * a.KW + kw);
+      }
+    }
+    r_mask[j] = m;
+    r_base[j] = m ? (int)(((long long)r_off[j] + (long long)r_h[j] * W + r_w[j]) * a.x_ld) : 0;
+  }
 
   auto issue = [&](int kt, int buf) {
     uint8_t* As = smem + buf * STAGE;
     uint8_t* Bs = As + A_BYTES;
-    // K coordinates of this lane's chunk
-    int kh, kw, ch;
+    int kh, kw, ch, tap;
     bool kval;
     if constexpr (CALIGNED) {
-      const int k0 = kt * kBK;
-      const int tap = k0 / C;  // wave-uniform
+      const int k0 = kt * BK;
+      tap = k0 / C;  // wave-uniform
       kh = tap / a.KW;
       kw = tap - kh * a.KW;
       ch = k0 - tap * C + lchunk * 8;
       kval = tap < a.KH * a.KW;
     } else {
-      const int k = kt * kBK + lchunk * 8;
-      const int tap = k / C;
+      const int k = kt * BK + lchunk * 8;
+      tap = k / C;
       kh = tap / a.KW;
       kw = tap - kh * a.KW;
       ch = k - tap * C;
       kval = k < a.K;
     }
+    if (FAST && fast) {
+      const int delta = (kh * W + kw) * (int)a.x_ld + ch;
+      const uint32_t tbit = kval ? (1u << tap) : 0u;
+#pragma unroll
+      for (int j = 0; j < A_I; ++j) {
+        const uint32_t voff = (r_mask[j] & tbit) ? (uint32_t)(r_base[j] + delta) * 2u : kOOB;
+        dma16(xr, As + (j * NW + wave) * 1024, voff);
+      }
+    } else {
 #pragma unroll
     for (int j = 0; j < A_I; ++j) {
       int ih, iw;
@@ -160,14 +210,28 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
           ok ? (uint32_t)((((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch) * 2) : kOOB;
       dma16(xr, As + (j * NW + wave) * 1024, voff);
     }
+    }
 #pragma unroll
-    for (int j = 0; j < B_I; ++j) {
+    for (int j = 0; j < B_FULL + (B_REM ? 1 : 0); ++j) {
       const int grp = j * NW + wave;
-      if (grp < B_ROWGROUPS) {
-        const int row = grp * 8 + lrow;
-        const uint32_t voff = (uint32_t)((((long long)(n0 + row)) * a.Kpad + kt * kBK + lchunk * 8) * 2);
+      if (grp < B_GROUPS) {
+        const int row = grp * RPI + lrow;
+        const uint32_t voff = (uint32_t)((((long long)(n0 + row)) * a.Kpad + kt * BK + lchunk * 8) * 2);
         dma16(wr, Bs + grp * 1024, voff);
       }
+    }
+  };
+
+  // wait until this wave's DMAs of the current tile landed, leaving `pend` younger tiles in flight
+  auto wait_tiles = [&](int pend) {
+    constexpr int PT_LO = A_I + B_FULL, PT_HI = A_I + B_FULL + 1;
+    const bool hi = B_REM && wave < B_REM;
+    if (pend <= 0) {
+      wait_vm<0>();
+    } else if (pend == 1) {
+      if (hi) wait_vm<PT_HI>(); else wait_vm<PT_LO>();
+    } else {
+      if (hi) wait_vm<2 * PT_HI>(); else wait_vm<2 * PT_LO>();
     }
   };
 
@@ -177,31 +241,35 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment read offsets: row = base + (lane & 15) -> swizzle term is lane & 7
+  // fragment read offsets: row = 16-aligned base + (lane & 15)
   const int a_row0 = wm * FM * 16 + (lane & 15);
   const int b_row0 = wn * FN * 16 + (lane & 15);
-  int sw[2];
+  const int rx = row_xor<BK>(lane & 15);
+  int sw[BK / 32];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) sw[s] = (((s * 4 + (lane >> 4)) ^ (lane & 7)) << 4);
+  for (int s = 0; s < BK / 32; ++s) sw[s] = (((s * 4 + (lane >> 4)) ^ rx) << 4);
 
-  const int nk = a.Kpad / kBK;
-  issue(0, 0);
+  const int nk = a.Kpad / BK;
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nk) issue(p, p);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cur = kt % STAGES;
+    const int pend = min(STAGES - 2, nk - 1 - kt);
+    wait_tiles(pend);
     __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const uint8_t* As = smem + cur * STAGE;
     const uint8_t* Bs = As + A_BYTES;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BK / 32; ++s) {
       bf16x8 bfr[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (b_row0 + j * 16) * 128 + sw[s]);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (b_row0 + j * 16) * ROWB + sw[s]);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (a_row0 + i * 16) * 128 + sw[s]);
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (a_row0 + i * 16) * ROWB + sw[s]);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
@@ -268,34 +336,56 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
   }
 }
 
-template <int WM, int WN, int FM, int FN, int AMODE, int EPI>
+template <int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI>
 static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   const int tiles_m = (a.M + BM - 1) / BM;
   const int tiles_n = a.OCpad / BN;
   const long long nwg = (long long)tiles_m * tiles_n;
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
-  const bool aligned = (a.C % kBK) == 0;
+  const bool aligned = (a.C % BK) == 0;
   if (aligned)
-    hipLaunchKernelGGL((conv_dma_kernel<WM, WN, FM, FN, AMODE, EPI, true>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<WM, WN, FM, FN, BK, ST, AMODE, EPI, true>), dim3((unsigned)nwg),
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   else
-    hipLaunchKernelGGL((conv_dma_kernel<WM, WN, FM, FN, AMODE, EPI, false>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<WM, WN, FM, FN, BK, ST, AMODE, EPI, false>), dim3((unsigned)nwg),
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   return (int)hipGetLastError();
 }
 
+// DV_DMA_VARIANT: 0 (default) 2-stage BK64 except 256x128 (3-stage); 1: all 2-stage BK64;
+// 2: BK32 x 4-stage rings for 256x256 and 512x64 (A/B testing).
+static int dma_variant() {
+  static int v = [] {
+    const char* e = std::getenv("DV_DMA_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int AMODE, int EPI>
 static int dma_bn(const ConvArgs& a, hipStream_t s) {
-  if (a.OCpad % 256 == 0 && a.OC > 128) return dma_cfg<2, 4, 8, 4, AMODE, EPI>(a, s);   // 256 x 256
-  if (a.OCpad % 128 == 0 && a.OC > 64) return dma_cfg<4, 2, 4, 4, AMODE, EPI>(a, s);    // 256 x 128
-  if (a.OCpad % 64 == 0 && a.OC > 16) return dma_cfg<8, 1, 4, 4, AMODE, EPI>(a, s);     // 512 x 64
-  if (a.OCpad % 16 == 0) return dma_cfg<8, 1, 4, 1, AMODE, EPI>(a, s);                  // 512 x 16
+  // measured (profiles/layers_r1_pipeline.txt): BK=32 x 4-stage rings lose to 2-stage BK=64 on the
+  // 256x256 and 512x64 tiles; the 3-stage BK=64 ring wins slightly on 256x128.
+  const int v = dma_variant();
+  if (a.OCpad % 256 == 0 && a.OC > 128) {
+    if (v == 2) return dma_cfg<2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
+    return dma_cfg<2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 256
+  }
+  if (a.OCpad % 128 == 0 && a.OC > 64) {
+    if (v == 1) return dma_cfg<4, 2, 4, 4, 64, 2, AMODE, EPI>(a, s);
+    return dma_cfg<4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 256 x 128
+  }
+  if (a.OCpad % 64 == 0 && a.OC > 16) {
+    if (v == 2) return dma_cfg<8, 1, 4, 4, 32, 4, AMODE, EPI>(a, s);
+    return dma_cfg<8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s);  // 512 x 64
+  }
+  if (a.OCpad % 16 == 0) return dma_cfg<8, 1, 4, 1, 64, 2, AMODE, EPI>(a, s);  // 512 x 16
   return -3;
 }
 
 int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t s) {
-  if (a.C % 8 != 0 || a.Kpad % kBK != 0 || a.mask != nullptr || a.x_ld % 8 != 0) return -4;
+  if (a.C % 8 != 0 || a.Kpad % 64 != 0 || a.mask != nullptr || a.x_ld % 8 != 0) return -4;
   if (amode == CONV_A_FWD) {
     if (epi == CONV_E_BF16) return dma_bn<CONV_A_FWD, CONV_E_BF16>(a, s);
     if (epi == CONV_E_POOL) return dma_bn<CONV_A_FWD, CONV_E_POOL>(a, s);

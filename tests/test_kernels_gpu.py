@@ -142,9 +142,9 @@ def test_conv_mask_and_transpose(native_lib, conv_impl):
     assert _rel(got, gx) < 2e-2
 
 
-@pytest.mark.parametrize("N,H,W,C,OC,unpool,epi", [(2, 20, 40, 64, 64, False, "bf16"), (1, 9, 33, 128, 64, True, "bf16"),
-                                                    (3, 16, 64, 64, 3, False, "f32"), (1, 8, 30, 32, 128, True, "bf16"),
-                                                    (2, 12, 12, 64, 16, True, "f32")])
+@pytest.mark.parametrize("N,H,W,C,OC,unpool,epi", [(2, 20, 40, 64, 64, False, "bf16"), (1, 18, 34, 64, 64, True, "bf16"),
+                                                    (3, 16, 64, 64, 3, False, "f32"), (1, 40, 30, 64, 48, True, "bf16"),
+                                                    (2, 12, 12, 64, 16, True, "f32"), (5, 33, 17, 64, 3, False, "f32")])
 def test_conv_halo_kernel(native_lib, N, H, W, C, OC, unpool, epi):
     from deconv_api_amd.ops import conv as Cm
 
