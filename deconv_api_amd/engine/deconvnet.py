@@ -28,6 +28,7 @@ import torch
 
 from .. import ops
 from ..models.vgg16 import VGG16Runtime, LayerSpec
+from ..utils import tracing
 
 VALID_MODES = ("all", "max")
 
@@ -223,13 +224,17 @@ class DeconvNet:
             batch_topk: str = "per_image", mosaic: bool = True) -> DeconvResult:
         if mode not in VALID_MODES:
             raise ValueError(f"Illegal visualize mode {mode!r}; use 'all' or 'max'")
-        st = self.forward(x, layer)
-        idx, val = self.select_filters(st.out, k, batch_topk)
-        recon = self.backward(st, idx, mode, batch_topk)
+        with tracing.range_("dv.forward"):
+            st = self.forward(x, layer)
+        with tracing.range_("dv.select"):
+            idx, val = self.select_filters(st.out, k, batch_topk)
+        with tracing.range_("dv.backward"):
+            recon = self.backward(st, idx, mode, batch_topk)
         res = DeconvResult(recon, idx, val)
         if mosaic and k == 4:
             B = recon.shape[0]
-            res.mosaic = ops.deprocess_mosaic(recon.reshape(B * 4, *recon.shape[2:]).contiguous(), 4, True)
+            with tracing.range_("dv.deprocess"):
+                res.mosaic = ops.deprocess_mosaic(recon.reshape(B * 4, *recon.shape[2:]).contiguous(), 4, True)
         return res
 
 

@@ -8,10 +8,15 @@ Rank 0 owns the request batch. Per batch:
   3. data plane (RCCL over xGMI): one ``all_gather_into_tensor`` of the uint8 mosaics
      (602 KB per image) returns the whole batch in rank order; rank 0 drops the padding.
 Followers sit in ``follow()`` until rank 0 sends ``stop``.
+
+Failure handling: the per-batch control broadcast doubles as a heartbeat
+(``ping()`` when idle). If a control or gather collective fails (a follower died: Gloo reports the
+closed peer, or the group timeout fires), rank 0 marks the runner degraded, stops using the
+process group and recomputes the batch - and every later one - on its own GPU, so requests keep
+being answered while the pool is re-formed by the orchestrator.
 """
 from __future__ import annotations
 
-import time
 from typing import List, Optional
 
 import numpy as np
@@ -19,7 +24,11 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..utils.faults import FaultInjector
+from ..utils.logging import get_logger
 from .dist import DistInfo, all_gather_rows, shard_sizes
+
+log = get_logger("deconv_api_amd.sharded")
 
 
 class ShardedRunner:
@@ -31,6 +40,13 @@ class ShardedRunner:
         self.mode = mode
         self.group = info.ctrl_group  # gloo side group (None -> default group, e.g. gloo on CPU)
         self.batches = 0
+        self.degraded = False
+        self.last_error: Optional[str] = None
+        self.faults = FaultInjector.from_env(info.rank)
+
+    @property
+    def world(self) -> int:
+        return 1 if self.degraded else self.info.world
 
     # ----------------------------------------------------------------- shared compute
     def _prep(self, images: List[np.ndarray]) -> torch.Tensor:
@@ -46,34 +62,61 @@ class ShardedRunner:
             x[b] = ops.preprocess_ref(ops.resize_u8_ref(img, S, S), 8, torch.float32)
         return x
 
+    def _local(self, layer: str, images: List[np.ndarray]) -> torch.Tensor:
+        return self.engine.run(self._prep(images), layer, k=self.k, mode=self.mode).mosaic
+
     def _compute(self, layer: str, images: List[np.ndarray], n: int, per: int) -> torch.Tensor:
+        self.faults.on_batch()
         r = self.info.rank
         shard = images[r * per:(r + 1) * per]
         pad = per - len(shard)
         if pad:
             shard = list(shard) + [np.zeros((self.S, self.S, 3), np.uint8)] * pad
-        x = self._prep(shard)
-        res = self.engine.run(x, layer, k=self.k, mode=self.mode)
-        return all_gather_rows(res.mosaic.contiguous(), self.info)
+        mos = self._local(layer, shard)
+        return all_gather_rows(mos.contiguous(), self.info)
 
     # ----------------------------------------------------------------- rank 0
     def run(self, layer: str, images: List[np.ndarray]) -> np.ndarray:
         assert self.info.rank == 0
         n = len(images)
-        per = shard_sizes(n, self.info.world)[0]
-        if self.info.world > 1:
-            dist.broadcast_object_list([{"op": "run", "layer": layer, "n": n, "per": per}, images], src=0,
-                                       group=self.group)
-        out = self._compute(layer, images, n, per)
         self.batches += 1
-        return out[:n].cpu().numpy()
+        if not self.degraded and self.info.world > 1:
+            per = shard_sizes(n, self.info.world)[0]
+            try:
+                dist.broadcast_object_list([{"op": "run", "layer": layer, "n": n, "per": per}, images], src=0,
+                                           group=self.group)
+                out = self._compute(layer, images, n, per)
+                return out[:n].cpu().numpy()
+            except RuntimeError as e:  # a peer died / the group timed out
+                self._degrade(e)
+        self.faults.on_batch() if self.info.world == 1 else None
+        return self._local(layer, images).cpu().numpy()
+
+    def ping(self) -> bool:
+        """Heartbeat over the control group; False (and degraded) if any follower is gone."""
+        if self.degraded or self.info.world == 1:
+            return not self.degraded
+        try:
+            dist.broadcast_object_list([{"op": "ping"}, None], src=0, group=self.group)
+            return True
+        except RuntimeError as e:
+            self._degrade(e)
+            return False
+
+    def _degrade(self, e: BaseException) -> None:
+        self.degraded = True
+        self.last_error = repr(e)
+        log.error("follower failure, continuing on rank 0 only", extra={"fields": {"error": repr(e)}})
 
     def stop(self):
-        if self.info.world > 1 and self.info.rank == 0:
-            dist.broadcast_object_list([{"op": "stop"}, None], src=0, group=self.group)
+        if self.info.world > 1 and self.info.rank == 0 and not self.degraded:
+            try:
+                dist.broadcast_object_list([{"op": "stop"}, None], src=0, group=self.group)
+            except RuntimeError as e:
+                self._degrade(e)
 
     # ----------------------------------------------------------------- followers
-    def follow(self, poll_timeout: Optional[float] = None) -> int:
+    def follow(self) -> int:
         """Serve rank 0's batches until 'stop'. Returns the number of batches run."""
         assert self.info.rank != 0
         done = 0
@@ -83,5 +126,7 @@ class ShardedRunner:
             msg, images = box
             if msg["op"] == "stop":
                 return done
+            if msg["op"] == "ping":
+                continue
             self._compute(msg["layer"], images, msg["n"], msg["per"])
             done += 1

@@ -28,6 +28,7 @@ from ..config import Config
 from ..engine.deconvnet import DeconvNet, UnknownLayerError, VALID_MODES
 from ..models.vgg16 import VGG16
 from ..utils import metrics as M
+from ..utils.faults import FaultInjector
 from ..utils.logging import get_logger
 
 log = get_logger("deconv_api_amd.serve")
@@ -75,8 +76,20 @@ class DeconvService:
         self.images = 0
         self.last_error: Optional[str] = None
         self._stop = threading.Event()
+        self.faults = FaultInjector.from_env()
+        self._batch_t0: Optional[float] = None
+        self.stalled = False
         self._thread = threading.Thread(target=self._worker, name="dv-gpu-worker", daemon=True)
         self._thread.start()
+        self._watchdog = threading.Thread(target=self._watch, name="dv-watchdog", daemon=True)
+        self._watchdog.start()
+
+    def _watch(self):
+        """Marks the service not-ready while a batch runs longer than the request timeout (a hung
+        kernel or a dead peer); clears when batches complete again."""
+        while not self._stop.wait(0.5):
+            t0 = self._batch_t0
+            self.stalled = t0 is not None and time.perf_counter() - t0 > self.cfg.request_timeout_s
 
     # ------------------------------------------------------------------ front end
     def validate_layer(self, layer: str) -> None:
@@ -99,9 +112,12 @@ class DeconvService:
         return await loop.run_in_executor(self.codec.ex, encode_data_url, mosaic, self.cfg.jpeg_quality)
 
     def status(self) -> dict:
-        st = {"device": str(self.device), "worker_alive": self._thread.is_alive(), "queue_depth": self.q.qsize(),
+        st = {"device": str(self.device), "worker_alive": self._thread.is_alive() and not self.stalled,
+              "stalled": self.stalled, "queue_depth": self.q.qsize(),
               "batches": self.batches, "images": self.images, "last_error": self.last_error,
               "native": ops.native.available() if self.device.type == "cuda" else None}
+        if self.runner is not None:
+            st.update(world=self.runner.world, degraded=self.runner.degraded, runner_error=self.runner.last_error)
         if self.device.type == "cuda":
             st["gpu"] = torch.cuda.get_device_name(self.device)
         return st
@@ -132,10 +148,15 @@ class DeconvService:
     def _worker(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        last_beat = time.perf_counter()
         while not self._stop.is_set():
             jobs = self._collect()
             if not jobs:
+                if self.runner is not None and time.perf_counter() - last_beat > 10.0:
+                    self.runner.ping()  # idle heartbeat to the follower ranks
+                    last_beat = time.perf_counter()
                 continue
+            last_beat = time.perf_counter()
             M.QUEUE_DEPTH.set(self.q.qsize())
             by_layer = {}
             for j in jobs:
@@ -144,12 +165,12 @@ class DeconvService:
                 try:
                     mos = self.run_batch(layer, [j.image for j in group])
                     for j, m in zip(group, mos):
-                        j.loop.call_soon_threadsafe(_set_result, j.future, m)
+                        _deliver(j.loop, _set_result, j.future, m)
                 except Exception as e:  # noqa: BLE001 - delivered to every waiting request
                     self.last_error = repr(e)
                     log.exception("batch failed")
                     for j in group:
-                        j.loop.call_soon_threadsafe(_set_exc, j.future, e)
+                        _deliver(j.loop, _set_exc, j.future, e)
 
     def preprocess(self, images: List[np.ndarray]) -> torch.Tensor:
         B, S = len(images), self.cfg.image_size
@@ -166,12 +187,17 @@ class DeconvService:
 
     def run_batch(self, layer: str, images: List[np.ndarray]) -> np.ndarray:
         t0 = time.perf_counter()
-        if self.runner is not None:
-            mos = self.runner.run(layer, images)
-        else:
-            x = self.preprocess(images)
-            res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
-            mos = res.mosaic.cpu().numpy()
+        self._batch_t0 = t0
+        try:
+            if self.runner is not None:
+                mos = self.runner.run(layer, images)
+            else:
+                self.faults.on_batch()
+                x = self.preprocess(images)
+                res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
+                mos = res.mosaic.cpu().numpy()
+        finally:
+            self._batch_t0 = None
         dt = time.perf_counter() - t0
         self.batches += 1
         self.images += len(images)
@@ -179,6 +205,13 @@ class DeconvService:
         M.ENGINE_TIME.observe(dt, stage="batch")
         M.IMAGES.inc(len(images), layer=layer)
         return mos
+
+
+def _deliver(loop: asyncio.AbstractEventLoop, fn, fut, v):
+    try:
+        loop.call_soon_threadsafe(fn, fut, v)
+    except RuntimeError:  # the requester's event loop is gone (client timed out / shut down)
+        pass
 
 
 def _set_result(fut: asyncio.Future, v):

@@ -109,6 +109,64 @@ def test_sharded_deconv_matches_single():
     assert r1[1] == 2, r1
 
 
+def _worker_failover(rank, world, port, q):
+    try:
+        os.environ["DV_FAULT"] = "exit@2/rank=1"  # rank 1 dies when its 2nd batch arrives
+        from deconv_api_amd.engine.deconvnet import DeconvNet
+        from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
+        from deconv_api_amd.parallel.sharded import ShardedRunner
+
+        info = _init(rank, world, port)
+        specs = vgg16_specs(width_div=8, image_size=32, fc=64, classes=10)
+        eng = DeconvNet(VGG16.random(0, specs=specs).build("cpu", torch.float32))
+        runner = ShardedRunner(eng, info, image_size=32)
+        if rank == 0:
+            rng = np.random.default_rng(1)
+            imgs = [rng.integers(0, 256, (32, 32, 3), dtype=np.uint8) for _ in range(4)]
+            a = runner.run("block2_conv1", imgs)       # sharded over both ranks
+            b = runner.run("block2_conv1", imgs)       # rank 1 exits mid-batch -> failover
+            c = runner.run("block2_conv1", imgs[:2])   # degraded: rank 0 alone
+            want = runner._local("block2_conv1", imgs).numpy()
+            q.put((rank, bool(np.array_equal(a, want)), bool(np.array_equal(b, want)), runner.degraded,
+                   c.shape))
+        else:
+            runner.follow()
+            q.put((rank, "follower returned", None, None, None))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None, None))
+
+
+def test_follower_failure_failover():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_failover, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    r0 = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=60)
+    assert r0[0] == 0, r0
+    assert r0[1] is True and r0[2] is True and r0[3] is True and r0[4] == (2, 64, 64, 3), r0
+    assert ps[1].exitcode == 17
+
+
+def test_fault_spec_parse():
+    from deconv_api_amd.utils.faults import FaultInjector, InjectedFault, parse
+
+    fs = parse("raise@2,hang@3:0.01/rank=0,exit@9/rank=4")
+    assert [(f.action, f.batch, f.rank) for f in fs] == [("raise", 2, None), ("hang", 3, 0), ("exit", 9, 4)]
+    inj = FaultInjector(fs, rank=0)
+    inj.on_batch()
+    with pytest.raises(InjectedFault):
+        inj.on_batch()
+    inj.on_batch()  # hang 10 ms
+    with pytest.raises(ValueError):
+        parse("explode@1")
+
+
 def test_shard_sizes():
     from deconv_api_amd.parallel.dist import shard_counts, shard_sizes
 
