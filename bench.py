@@ -4,27 +4,30 @@
 One timed step = what the reference's ``POST /`` computes for a batch of images (app/main.py:
 45-78), minus only the host JPEG encode: preprocess (uint8 -> caffe bf16 NHWC), VGG16 forward to
 the target with fused pool+switch, per-image top-4 filter selection, 4 deconv chains per image
-to the input (unpool fused into the conv-down gather), 2x2 mosaic + deprocess to uint8, and with
-N > 1 an RCCL all-gather of every rank's uint8 mosaics over xGMI (weak scaling: 256 img/GPU).
+to the input (unpool fused or split), 2x2 mosaic + deprocess to uint8, and with N > 1 an RCCL
+all-gather of every rank's uint8 mosaics over xGMI (weak scaling: 256 img/GPU). The all-gather
+of step i runs asynchronously on RCCL's stream and overlaps step i+1's compute (double-buffered
+output); the clock stops only after the last gather completed on every rank.
 
 Run: ``python bench.py [--gpus N --steps K --warmup W]``; for N > 1 under
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
 Rank 0 prints ONE JSON line. Weights: seeded random-init VGG16 (no network for ImageNet
-weights); data: synthetic uint8 images.
+weights); data: synthetic uint8 images. ``--device cpu --tiny`` is a functional rehearsal of the
+same code path (gloo, scaled model) used by the CPU test-suite.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 import time
 
 import torch
+import torch.distributed as dist
 
 from deconv_api_amd import ops
 from deconv_api_amd.engine.deconvnet import DeconvNet
-from deconv_api_amd.models.vgg16 import VGG16
+from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
 from deconv_api_amd.parallel import dist as pdist
 
 # BASELINE.md: the reference's implied end-to-end rate for layer=block5_conv3 is ~0.03-0.04 img/s
@@ -42,6 +45,8 @@ def parse(argv=None):
     ap.add_argument("--layer", default="block5_conv3")
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--tiny", action="store_true", help="scaled VGG16 at 32px (CPU rehearsal only)")
     ap.add_argument("--breakdown", action="store_true", help="per-phase timing to stderr (extra syncs)")
     return ap.parse_args(argv)
 
@@ -50,65 +55,98 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class _Sync:
+    def __init__(self, dev):
+        self.cuda = dev.type == "cuda"
+
+    def __call__(self):
+        if self.cuda:
+            torch.cuda.synchronize()
+
+
 def main(argv=None):
     args = parse(argv)
-    info = pdist.init()
+    info = pdist.init(device_type=args.device)
     if info.world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={info.world}; using WORLD_SIZE")
     dev = info.device
-    if dev.type != "cuda":
-        raise SystemExit("bench.py needs a GPU (MI355X)")
-    ops.native.load()
+    sync = _Sync(dev)
+    if dev.type == "cuda":
+        ops.native.load()
+    elif not args.tiny:
+        raise SystemExit("bench.py on CPU is a rehearsal: pass --tiny")
+    specs = vgg16_specs(width_div=8, image_size=32, fc=64, classes=10) if args.tiny else None
+    S = 32 if args.tiny else 224
+    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
 
     # ---- weights: built on rank 0, broadcast once over RCCL ----
     t0 = time.time()
-    model = VGG16.random(args.seed) if info.is_main else VGG16.random(args.seed + 12345)
+    model = VGG16.random(args.seed if info.is_main else args.seed + 12345, specs=specs)
     if info.world > 1:
         sd = pdist.broadcast_state(model.state_dict(), info)
-        model = VGG16.from_state_dict(sd)
-    rt = model.build(dev, torch.bfloat16)
-    eng = DeconvNet(rt)
+        model = VGG16.from_state_dict(sd, specs=specs)
+    eng = DeconvNet(model.build(dev, dtype))
     log(f"[rank {info.rank}] weights ready in {time.time() - t0:.1f}s ({model.num_params() / 1e6:.1f}M params)")
 
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(1000 + info.rank)
-    images = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
-    xbuf = torch.empty(B, 224, 224, 8, dtype=torch.bfloat16, device=dev)
-    gathered = torch.empty(info.world * B, 448, 448, 3, dtype=torch.uint8, device=dev) if info.world > 1 else None
+    images = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=dev, generator=g)
+    xbuf = torch.empty(B, S, S, 8, dtype=dtype, device=dev)
+    gathered = [torch.empty(info.world * B, 2 * S, 2 * S, 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+    pending = [None, None]
 
-    def step():
+    def step(i):
         ops.resize_preprocess(images, xbuf)
         res = eng.run(xbuf, args.layer, k=args.k)
-        out = pdist.all_gather_rows(res.mosaic, info, gathered)
-        return res, out
+        if info.world > 1:
+            slot = i % 2
+            if pending[slot] is not None:
+                pending[slot].wait()  # the gather that last used this buffer (step i-2)
+            pending[slot] = dist.all_gather_into_tensor(gathered[slot], res.mosaic.contiguous(), async_op=True)
+        return res
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    def drain():
+        for s in (0, 1):
+            if pending[s] is not None:
+                pending[s].wait()
+                pending[s] = None
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
+    sync()
 
     if args.breakdown and info.is_main:
-        _breakdown(eng, images, xbuf, args)
+        _breakdown(eng, images, xbuf, args, sync)
 
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    cuda = dev.type == "cuda"
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if cuda else None
     pdist.barrier(info)
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
-    evs[0].record()
+    if cuda:
+        evs[0].record()
+    host_steps = []
     for i in range(args.steps):
-        step()
-        evs[i + 1].record()
-    torch.cuda.synchronize()
+        ts = time.perf_counter()
+        res = step(i)
+        if cuda:
+            evs[i + 1].record()
+        host_steps.append(time.perf_counter() - ts)
+    drain()
+    sync()
     pdist.barrier(info)
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t_start
     elapsed = pdist.all_reduce_max(elapsed, info)
-    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
-    p50 = per_step[len(per_step) // 2]
-    p50 = pdist.all_reduce_max(p50, info)
+    if cuda:
+        per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    else:
+        per_step = sorted(1e3 * t for t in host_steps)
+    p50 = pdist.all_reduce_max(per_step[len(per_step) // 2], info)
 
     ms = elapsed / args.steps * 1e3
-    total_imgs = B * info.world * args.steps
-    value = total_imgs / elapsed
+    value = B * info.world * args.steps / elapsed
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -122,23 +160,26 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": round(value / REF_IMG_PER_S, 1),
         "baseline_img_per_s": REF_IMG_PER_S,
-        "dtype": "bf16",
+        "dtype": "bf16" if cuda else "fp32",
         "data": "synthetic uint8 224x224 images, seeded random-init VGG16 weights",
-        "config": {"model": f"vgg16_deconvnet_{args.layer}", "global_batch": B * info.world, "seq_len": 224,
-                   "image_size": 224, "filters_per_image": args.k, "parallelism": f"dp{info.world}"},
+        "config": {"model": f"vgg16_deconvnet_{args.layer}", "global_batch": B * info.world, "seq_len": S,
+                   "image_size": S, "filters_per_image": args.k, "parallelism": f"dp{info.world}"},
     }
+    if args.tiny:
+        line["data"] = "REHEARSAL: scaled VGG16 (width/8, 32px) on CPU - not a benchmark"
     if info.is_main:
         print(json.dumps(line), flush=True)
     pdist.shutdown()
+    return line
 
 
-def _breakdown(eng, images, xbuf, args):
+def _breakdown(eng, images, xbuf, args, sync):
     """Per-phase wall time with syncs (diagnostic only, not the reported number)."""
     def t(fn):
-        torch.cuda.synchronize()
+        sync()
         a = time.perf_counter()
         r = fn()
-        torch.cuda.synchronize()
+        sync()
         return r, (time.perf_counter() - a) * 1e3
 
     _, tp = t(lambda: ops.resize_preprocess(images, xbuf))

@@ -167,6 +167,35 @@ def test_fault_spec_parse():
         parse("explode@1")
 
 
+def _worker_bench(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        import bench
+        from deconv_api_amd.parallel import dist as pdist
+
+        # bench.main() initializes its own group from the env; tear ours down first
+        pdist.shutdown()
+        line = bench.main(["--device", "cpu", "--tiny", "--batch", "3", "--steps", "3", "--warmup", "1",
+                           "--gpus", str(world)])
+        q.put((rank, line))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+
+
+def test_bench_rehearsal_dp2():
+    """bench.py's distributed path (weight broadcast, async double-buffered all-gather, max-over-
+    ranks timing, JSON contract) on gloo with world_size 2."""
+    res = _run(_worker_bench, 2)
+    for rank, line in res:
+        assert isinstance(line, dict), line
+        assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 6 and line["steps"] == 3
+        assert line["config"]["parallelism"] == "dp2" and line["value"] > 0 and line["scaling"] == "weak"
+        for k in ("metric", "unit", "ms_per_step", "higher_is_better", "vs_baseline", "dtype", "data", "warmup"):
+            assert k in line
+
+
 def test_shard_sizes():
     from deconv_api_amd.parallel.dist import shard_counts, shard_sizes
 
