@@ -73,8 +73,15 @@ def encode_jpeg(rgb: np.ndarray, quality: int = JPEG_QUALITY) -> bytes:
     return buf.getvalue()
 
 
+def quote_b64(b64: str) -> str:
+    """``urllib.parse.quote`` restricted to base64 text: letters, digits and '/' are kept, so only
+    '+' -> '%2B' and '=' -> '%3D' change. Identical output, C-speed (quote() walks the ~100 KB
+    string in Python and capped the service at ~200 req/s)."""
+    return b64.replace("+", "%2B").replace("=", "%3D")
+
+
 def to_data_url(jpeg: bytes) -> str:
-    return DATA_URL_PREFIX + quote(base64.b64encode(jpeg).decode("ascii"))
+    return DATA_URL_PREFIX + quote_b64(base64.b64encode(jpeg).decode("ascii"))
 
 
 def encode_data_url(rgb: np.ndarray, quality: int = JPEG_QUALITY) -> str:

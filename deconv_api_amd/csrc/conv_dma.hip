@@ -370,6 +370,7 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
   const int v = dma_variant();
   if (a.OCpad % 256 == 0 && a.OC > 128) {
     if (v == 2) return dma_cfg<2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
+    if (v == 3) return dma_cfg<2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
     return dma_cfg<2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 256
   }
   if (a.OCpad % 128 == 0 && a.OC > 64) {

@@ -204,8 +204,12 @@ template <int FN, int EPI, bool UNPOOL>
 static int persist_cfg(const ConvArgs& a, hipStream_t s) {
   const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   if (ntiles <= 0 || ntiles > 0x7fffffffLL) return -2;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  // CU count queried once (keeps the launch path free of runtime queries during graph capture)
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
   const long long grid = std::min<long long>(ntiles, (long long)cus);
   hipLaunchKernelGGL((conv3x3_c64_persist_kernel<FN, EPI, UNPOOL>), dim3((unsigned)grid), dim3(512), 0, s, a);
   return (int)hipGetLastError();

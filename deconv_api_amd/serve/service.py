@@ -1,14 +1,17 @@
-"""Request batching service: async front end -> GPU worker thread -> host codec pool.
+"""Request batching service: async front end -> GPU worker thread -> completion thread -> codec pool.
 
 The reference runs each request to completion on the event-loop thread (``async def`` with
 blocking compute, app/main.py:46), so requests serialize and the server stalls. Here:
   * decode (PIL) and JPEG encode run on a thread pool (they release the GIL);
   * requests are queued and a single GPU worker thread drains them in batches (same target layer,
     up to ``max_batch``, waiting at most ``batch_timeout_ms`` for stragglers); one batch = one
-    engine call over B images x 4 filters;
-  * uploads use pinned host buffers + non_blocking copies on the compute stream; the GPU-side
-    resize+preprocess kernel writes straight into the batch tensor;
-  * backpressure: beyond ``max_queue`` pending requests new ones fail fast (HTTP 503).
+    engine call over B images x 4 filters, replayed from a hipGraph per (layer, batch bucket);
+  * the worker never waits for the GPU: it uploads (pinned, non_blocking), launches, enqueues the
+    mosaic's D2H copy into pinned memory plus an event, and moves on to the next batch; a
+    completion thread waits on the event and hands results to the requests, whose JPEG encode
+    then overlaps the next batch's GPU work;
+  * backpressure: beyond ``max_queue`` pending requests new ones fail fast (HTTP 503);
+  * a watchdog marks the service not-ready while a batch exceeds the request timeout.
 """
 from __future__ import annotations
 
@@ -25,7 +28,7 @@ import torch
 from .. import ops
 from ..codec import CodecPool, encode_data_url, read_data_url
 from ..config import Config
-from ..engine.deconvnet import DeconvNet, UnknownLayerError, VALID_MODES
+from ..engine.deconvnet import DeconvNet, UnknownLayerError
 from ..models.vgg16 import VGG16
 from ..utils import metrics as M
 from ..utils.faults import FaultInjector
@@ -65,13 +68,21 @@ class DeconvService:
         self.runner = runner
         dev = self.cfg.resolve_device() if runner is None else str(runner.info.device)
         self.device = torch.device(dev)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         if engine is None:
             model = load_model(self.cfg)
             dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
             engine = DeconvNet(model.build(self.device, dtype))
         self.engine = engine
+        self.graphs = None
+        if self.device.type == "cuda" and self.cfg.hip_graphs and runner is None:
+            from ..engine.graphs import GraphedDeconv
+
+            self.graphs = GraphedDeconv(engine, self.cfg.image_size, self.cfg.filters, self.cfg.mode)
         self.codec = CodecPool(self.cfg.codec_workers)
         self.q: "queue.Queue[_Job]" = queue.Queue()
+        self.done_q: "queue.Queue" = queue.Queue()
         self.batches = 0
         self.images = 0
         self.last_error: Optional[str] = None
@@ -81,6 +92,8 @@ class DeconvService:
         self.stalled = False
         self._thread = threading.Thread(target=self._worker, name="dv-gpu-worker", daemon=True)
         self._thread.start()
+        self._completer = threading.Thread(target=self._complete, name="dv-completion", daemon=True)
+        self._completer.start()
         self._watchdog = threading.Thread(target=self._watch, name="dv-watchdog", daemon=True)
         self._watchdog.start()
 
@@ -93,10 +106,7 @@ class DeconvService:
 
     # ------------------------------------------------------------------ front end
     def validate_layer(self, layer: str) -> None:
-        try:
-            self.engine._check_layer(layer)
-        except UnknownLayerError:
-            raise
+        self.engine._check_layer(layer)  # raises UnknownLayerError
 
     async def deconv(self, uri: str, layer: str) -> str:
         """The reference's POST / pipeline for one request -> data URL string."""
@@ -115,16 +125,19 @@ class DeconvService:
         st = {"device": str(self.device), "worker_alive": self._thread.is_alive() and not self.stalled,
               "stalled": self.stalled, "queue_depth": self.q.qsize(),
               "batches": self.batches, "images": self.images, "last_error": self.last_error,
-              "native": ops.native.available() if self.device.type == "cuda" else None}
-        if self.runner is not None:
-            st.update(world=self.runner.world, degraded=self.runner.degraded, runner_error=self.runner.last_error)
+              "native": ops.native.available() if self.device.type == "cuda" else None,
+              "graphs": [f"{l}:{b}" for l, b in self.graphs.captured] if self.graphs else None}
         if self.device.type == "cuda":
             st["gpu"] = torch.cuda.get_device_name(self.device)
+        if self.runner is not None:
+            st.update(world=self.runner.world, degraded=self.runner.degraded, runner_error=self.runner.last_error)
         return st
 
     def close(self):
         self._stop.set()
         self._thread.join(timeout=5)
+        self.done_q.put(None)
+        self._completer.join(timeout=5)
         self.codec.shutdown()
 
     # ------------------------------------------------------------------ GPU worker
@@ -134,8 +147,17 @@ class DeconvService:
         except queue.Empty:
             return []
         jobs = [first]
-        deadline = time.perf_counter() + self.cfg.batch_timeout_ms / 1e3
+        # dynamic batching: wait for stragglers only while the GPU still has a batch in flight
+        # (they would queue behind it anyway); an idle GPU starts the batch immediately
+        busy = not self.done_q.empty() or self._batch_t0 is not None
+        deadline = time.perf_counter() + (self.cfg.batch_timeout_ms / 1e3 if busy else 0.0)
         while len(jobs) < self.cfg.max_batch:
+            if not busy:
+                try:
+                    jobs.append(self.q.get_nowait())
+                    continue
+                except queue.Empty:
+                    break
             rem = deadline - time.perf_counter()
             if rem <= 0:
                 break
@@ -162,22 +184,50 @@ class DeconvService:
             for j in jobs:
                 by_layer.setdefault(j.layer, []).append(j)
             for layer, group in by_layer.items():
+                t0 = time.perf_counter()
+                self._batch_t0 = t0
                 try:
-                    mos = self.run_batch(layer, [j.image for j in group])
-                    for j, m in zip(group, mos):
-                        _deliver(j.loop, _set_result, j.future, m)
+                    handle = self.launch_batch(layer, [j.image for j in group])
+                    self.done_q.put((handle, group, layer, t0))
                 except Exception as e:  # noqa: BLE001 - delivered to every waiting request
-                    self.last_error = repr(e)
-                    log.exception("batch failed")
-                    for j in group:
-                        _deliver(j.loop, _set_exc, j.future, e)
+                    self._batch_t0 = None
+                    self._fail(group, e)
 
+    def _complete(self):
+        while True:
+            item = self.done_q.get()
+            if item is None:
+                return
+            handle, group, layer, t0 = item
+            try:
+                mos = self.finish_batch(handle)
+                for j, m in zip(group, mos):
+                    _deliver(j.loop, _set_result, j.future, m)
+                dt = time.perf_counter() - t0
+                self.batches += 1
+                self.images += len(group)
+                M.BATCH_SIZE.observe(len(group))
+                M.ENGINE_TIME.observe(dt, stage="batch")
+                M.IMAGES.inc(len(group), layer=layer)
+            except Exception as e:  # noqa: BLE001
+                self._fail(group, e)
+            finally:
+                if self.done_q.empty():
+                    self._batch_t0 = None
+
+    def _fail(self, group, e):
+        self.last_error = repr(e)
+        log.exception("batch failed", exc_info=e)
+        for j in group:
+            _deliver(j.loop, _set_exc, j.future, e)
+
+    # ------------------------------------------------------------------ batch execution
     def preprocess(self, images: List[np.ndarray]) -> torch.Tensor:
         B, S = len(images), self.cfg.image_size
         if self.device.type == "cuda":
             x = torch.empty(B, S, S, 8, dtype=torch.bfloat16, device=self.device)
             for b, img in enumerate(images):
-                h = torch.from_numpy(np.ascontiguousarray(img)).pin_memory()
+                h = torch.from_numpy(np.require(img, requirements=["C", "W"])).pin_memory()
                 ops.resize_preprocess(h.to(self.device, non_blocking=True), x[b])
             return x
         x = torch.empty(B, S, S, 8, dtype=torch.float32)
@@ -185,26 +235,35 @@ class DeconvService:
             x[b] = ops.preprocess_ref(ops.resize_u8_ref(img, S, S), 8, torch.float32)
         return x
 
+    def launch_batch(self, layer: str, images: List[np.ndarray]):
+        """Enqueue the batch; returns a handle for ``finish_batch`` (GPU work may still run)."""
+        if self.runner is not None:
+            return ("host", self.runner.run(layer, images))
+        self.faults.on_batch()
+        x = self.preprocess(images)
+        n = len(images)
+        if self.graphs is not None:
+            res = self.graphs.run(x, layer)
+        else:
+            res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
+        if self.device.type != "cuda":
+            return ("host", res.mosaic[:n].numpy())
+        host = torch.empty((n, *res.mosaic.shape[1:]), dtype=torch.uint8, pin_memory=True)
+        host.copy_(res.mosaic[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ("event", ev, host)
+
+    def finish_batch(self, handle) -> np.ndarray:
+        if handle[0] == "host":
+            return handle[1]
+        _, ev, host = handle
+        ev.synchronize()
+        return host.numpy()
+
     def run_batch(self, layer: str, images: List[np.ndarray]) -> np.ndarray:
-        t0 = time.perf_counter()
-        self._batch_t0 = t0
-        try:
-            if self.runner is not None:
-                mos = self.runner.run(layer, images)
-            else:
-                self.faults.on_batch()
-                x = self.preprocess(images)
-                res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
-                mos = res.mosaic.cpu().numpy()
-        finally:
-            self._batch_t0 = None
-        dt = time.perf_counter() - t0
-        self.batches += 1
-        self.images += len(images)
-        M.BATCH_SIZE.observe(len(images))
-        M.ENGINE_TIME.observe(dt, stage="batch")
-        M.IMAGES.inc(len(images), layer=layer)
-        return mos
+        """Synchronous batch (tests / tools)."""
+        return self.finish_batch(self.launch_batch(layer, images))
 
 
 def _deliver(loop: asyncio.AbstractEventLoop, fn, fut, v):

@@ -163,6 +163,11 @@ def test_codec_quirks():
     rgba.save(buf, "PNG")
     assert np.array_equal(read_data_url("data:image/png;base64," + base64.b64encode(buf.getvalue()).decode()), img)
     assert quote("ab+c/d=") == "ab%2Bc/d%3D"
+    from deconv_api_amd.codec.image import quote_b64
+
+    for n in (0, 1, 2, 3, 1000, 4097):
+        b = base64.b64encode(np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()).decode()
+        assert quote_b64(b) == quote(b)
 
 
 def test_resize_oracle_properties():

@@ -56,6 +56,51 @@ def test_engine_full_vgg16_block5_conv3(native_lib):
     _compare(m, 2, 224, ["block5_conv3", "block2_pool"], seed=1)
 
 
+def test_graphed_engine_equals_eager(native_lib):
+    from deconv_api_amd.engine.graphs import GraphedDeconv, bucket_for
+
+    m = VGG16.random(0, include_top=False)
+    eng = DeconvNet(m.build("cuda", torch.bfloat16))
+    gd = GraphedDeconv(eng)
+    x = _x8(3, 224, 4).to(torch.bfloat16).cuda()
+    eager = eng.run(x, "block4_pool", k=4)
+    res = gd.run(x, "block4_pool")  # bucket 4, padded with a zero image
+    assert bucket_for(3) == 4 and gd.captured == [("block4_pool", 4)]
+    assert torch.equal(res.mosaic[:3], eager.mosaic) and torch.equal(res.filters[:3], eager.filters)
+    x2 = _x8(3, 224, 5).to(torch.bfloat16).cuda()  # replay with new data
+    assert torch.equal(gd.run(x2, "block4_pool").mosaic[:3], eng.run(x2, "block4_pool", k=4).mosaic)
+
+
+def test_service_end_to_end_gpu(native_lib):
+    """The HTTP path on the GPU: decode -> GPU resize -> graphed engine -> D2H -> JPEG."""
+    import asyncio
+
+    from deconv_api_amd.codec import make_data_url, parse_result_data_url
+    from deconv_api_amd.config import Config
+    from deconv_api_amd.serve.service import DeconvService
+
+    eng = DeconvNet(VGG16.random(0, include_top=False).build("cuda", torch.bfloat16))
+    svc = DeconvService(Config.from_env(device="cuda", max_batch=8, batch_timeout_ms=2.0), engine=eng)
+    try:
+        rng = np.random.default_rng(0)
+        imgs = [rng.integers(0, 256, (300 + 10 * i, 260, 3), dtype=np.uint8) for i in range(5)]
+
+        async def go():
+            return await asyncio.gather(*(svc.deconv(make_data_url(im, "PNG"), "block3_pool") for im in imgs))
+
+        outs = asyncio.run(go())
+        for s in outs:
+            assert parse_result_data_url(s).shape == (448, 448, 3)
+        # the same images through the engine directly give the same mosaics (before JPEG)
+        want = eng.run(svc.preprocess([imgs[0]]), "block3_pool", k=4).mosaic[0].cpu().numpy()
+        from deconv_api_amd.codec import encode_data_url
+
+        assert np.array_equal(parse_result_data_url(outs[0]), parse_result_data_url(encode_data_url(want)))
+        assert svc.status()["graphs"]
+    finally:
+        svc.close()
+
+
 def test_engine_mosaic_and_run(native_lib):
     m = VGG16.random(0, include_top=False)
     gpu = DeconvNet(m.build("cuda", torch.bfloat16))

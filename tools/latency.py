@@ -1,0 +1,104 @@
+"""Latency / serving throughput on one GPU.
+
+1. engine: p50 latency of one deconvnet batch (block5_conv3) for several batch sizes, eager vs
+   hipGraph replay;
+2. service: the full request path (base64 decode, PIL decode, GPU resize+preprocess, batched
+   engine, D2H, JPEG encode, quoted data URL) driven by C concurrent in-process clients:
+   requests/s and p50/p99 request latency.
+Prints one JSON object.
+"""
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from deconv_api_amd import ops  # noqa: E402
+from deconv_api_amd.codec import make_data_url  # noqa: E402
+from deconv_api_amd.config import Config  # noqa: E402
+from deconv_api_amd.engine.deconvnet import DeconvNet  # noqa: E402
+from deconv_api_amd.engine.graphs import GraphedDeconv  # noqa: E402
+from deconv_api_amd.models.vgg16 import VGG16  # noqa: E402
+from deconv_api_amd.serve.service import DeconvService  # noqa: E402
+
+
+def p(xs, q):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(q * len(xs)))]
+
+
+def engine_latency(eng, layer, sizes, reps):
+    dev = eng.rt.device
+    gd = GraphedDeconv(eng)
+    out = {}
+    for B in sizes:
+        x = torch.randn(B, 224, 224, 8, device=dev).mul(50).to(torch.bfloat16)
+        row = {}
+        for mode in ("eager", "graph"):
+            fn = (lambda: eng.run(x, layer)) if mode == "eager" else (lambda: gd.run(x, layer))
+            fn()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append((time.perf_counter() - t) * 1e3)
+            row[mode] = {"p50_ms": round(p(ts, 0.5), 3), "img_per_s": round(B / (p(ts, 0.5) / 1e3), 1)}
+        out[str(B)] = row
+    return out
+
+
+async def serve_load(svc, layer, clients, total, size):
+    rng = np.random.default_rng(0)
+    urls = [make_data_url(rng.integers(0, 256, (size, size, 3), dtype=np.uint8), "JPEG") for _ in range(16)]
+    lat = []
+    sem = asyncio.Semaphore(clients)
+
+    async def one(i):
+        async with sem:
+            t = time.perf_counter()
+            s = await svc.deconv(urls[i % len(urls)], layer)
+            assert s.startswith("data:image/webp;base64,")
+            lat.append((time.perf_counter() - t) * 1e3)
+
+    await one(0)  # warm (graph capture for bucket 1)
+    lat.clear()
+    t0 = time.perf_counter()
+    await asyncio.gather(*(one(i) for i in range(total)))
+    dt = time.perf_counter() - t0
+    return {"clients": clients, "requests": total, "req_per_s": round(total / dt, 1),
+            "p50_ms": round(p(lat, 0.5), 2), "p99_ms": round(p(lat, 0.99), 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layer", default="block5_conv3")
+    ap.add_argument("--sizes", default="1,4,16,64")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--clients", default="1,16,64")
+    ap.add_argument("--requests", type=int, default=256)
+    ap.add_argument("--img", type=int, default=320, help="client image side (resized to 224 on GPU)")
+    a = ap.parse_args()
+    ops.native.load()
+    dev = torch.device("cuda", 0)
+    eng = DeconvNet(VGG16.random(0).build(dev, torch.bfloat16))
+    res = {"engine": engine_latency(eng, a.layer, [int(s) for s in a.sizes.split(",")], a.reps)}
+    cfg = Config.from_env(device="cuda", max_batch=64, batch_timeout_ms=2.0, codec_workers=16)
+    svc = DeconvService(cfg, engine=eng)
+    res["service"] = []
+    for c in (int(x) for x in a.clients.split(",")):
+        res["service"].append(asyncio.run(serve_load(svc, a.layer, c, max(a.requests, c), a.img)))
+    res["graphs"] = svc.status()["graphs"]
+    svc.close()
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
