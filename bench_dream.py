@@ -3,11 +3,11 @@
 
   config 3: python bench_dream.py --model inception_v3 --batch 64 --size 299 --octaves 4 --steps 20
   config 5: python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
-                bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 8
+                bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 8 --dtype fp16
 
 One timed run = the whole octave loop (octaves x steps gradient-ascent iterations + octave
 resizes/detail re-injection) over the batch. Prints ONE JSON line (rank 0). Synthetic uint8
-images, seeded random-init weights, bf16 compute.
+images, seeded random-init weights, bf16 (default) or fp16 compute.
 """
 from __future__ import annotations
 
@@ -35,20 +35,23 @@ def main(argv=None):
     ap.add_argument("--runs", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
+                    help="16-bit storage / MFMA dtype (BASELINE config 5 is quoted in fp16)")
     a = ap.parse_args(argv)
 
     info = pdist.init()
     dev = info.device
     ops.native.load()
+    dt = torch.float16 if a.dtype == "fp16" else torch.bfloat16
     if a.model == "inception_v3":
         from deconv_api_amd.models.inception_v3 import InceptionV3
 
-        net = InceptionV3(0).build(dev)
+        net = InceptionV3(0).build(dev, dt)
         s = DreamSettings(octaves=a.octaves, iterations=a.steps)
     else:
         from deconv_api_amd.models.resnet50 import ResNet50
 
-        net = ResNet50(0).build(dev)
+        net = ResNet50(0).build(dev, dt)
         s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=a.octaves, iterations=a.steps)
     if a.tile:
         dd = TiledDeepDream(net, s, tile=a.tile, info=info)
@@ -77,7 +80,7 @@ def main(argv=None):
             "metric": f"DeepDream images/sec ({a.model}, {a.octaves} octaves x {a.steps} steps)",
             "value": round(imgs / per_run, 3), "unit": "images/s", "n_gpus": info.world,
             "s_per_dream_batch": round(per_run, 3), "runs": a.runs, "warmup": a.warmup,
-            "higher_is_better": True, "scaling": "strong" if a.tile else "weak", "dtype": "bf16",
+            "higher_is_better": True, "scaling": "strong" if a.tile else "weak", "dtype": a.dtype,
             "data": "synthetic uint8 images, seeded random-init weights", "hip_graphs": not a.no_graphs and not a.tile,
             "finite": bool(torch.isfinite(out).all()),
             "config": {"model": a.model, "batch": a.batch, "image_size": a.size, "tile": a.tile,

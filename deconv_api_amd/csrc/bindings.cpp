@@ -51,7 +51,11 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   a.relu = (int)g[16]; a.relu_in = (int)g[17]; a.accumulate = (int)g[18];
   a.code_div = (int)g[19]; a.x_ld = g[20]; a.mask_ld = g[21]; a.out_ld = g[22];
 
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv: x, w must be bf16");
+  const auto dt = x.scalar_type();
+  TORCH_CHECK((dt == at::kBFloat16 || dt == at::kHalf) && w.scalar_type() == dt, "conv: x, w must both be bf16 or fp16");
+  a.dtype = dt == at::kHalf ? dv::DT_F16 : dv::DT_BF16;
+  TORCH_CHECK(a.dtype == dv::DT_BF16 || (epi == dv::CONV_E_BF16 && amode != dv::CONV_A_UNPOOL),
+              "conv: fp16 supports forward / transpose with a 16-bit output");
   TORCH_CHECK(w.is_contiguous() && w.numel() == (int64_t)a.OCpad * a.Kpad, "conv: w must be [OCpad, Kpad]");
   TORCH_CHECK(a.K == a.KH * a.KW * a.C && a.Kpad >= a.K && a.Kpad % 64 == 0, "conv: bad K/Kpad");
   TORCH_CHECK(a.C % 8 == 0 && a.x_ld % 8 == 0 && a.x_ld >= a.C, "conv: C and x_ld must be multiples of 8");
@@ -79,7 +83,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   need(x, ((in_pix - 1) * a.x_ld + a.C) * 2, "x");
   if (mask.has_value()) {
     check_cuda(*mask, "mask");
-    TORCH_CHECK(mask->scalar_type() == at::kBFloat16 && a.mask_ld % 8 == 0, "mask must be bf16, ld%8");
+    TORCH_CHECK(mask->scalar_type() == dt && a.mask_ld % 8 == 0, "mask must have x's dtype, ld%8");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(mask->data_ptr()) % 16 == 0, "mask must be 16-byte aligned");
     need(*mask, ((in_pix - 1) * a.mask_ld + a.C) * 2, "mask");
     a.mask = reinterpret_cast<const uint16_t*>(mask->data_ptr());
@@ -99,11 +103,11 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     TORCH_CHECK(out_code->scalar_type() == at::kByte, "out_code must be uint8");
     need(*out_code, out_rows * a.OC, "out_code");
     a.out_code = reinterpret_cast<uint8_t*>(out_code->data_ptr());
-    TORCH_CHECK(out.scalar_type() == at::kBFloat16, "pool out must be bf16");
+    TORCH_CHECK(out.scalar_type() == dt, "pool out must have x's dtype");
   } else if (epi == dv::CONV_E_F32) {
     TORCH_CHECK(out.scalar_type() == at::kFloat, "f32 epilogue needs fp32 out");
   } else {
-    TORCH_CHECK(out.scalar_type() == at::kBFloat16, "bf16 epilogue needs bf16 out");
+    TORCH_CHECK(out.scalar_type() == dt, "16-bit epilogue needs out of x's dtype");
   }
   need(out, ((out_rows - 1) * a.out_ld + a.OC) * (int64_t)out.element_size(), "out");
   a.out = out.data_ptr();
@@ -113,7 +117,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   //  * register-staged: everything else (ReLU-mask prologue, fused unpool gather)
   const bool halo_ok = (amode == dv::CONV_A_FWD || amode == dv::CONV_A_UNPOOL) && a.KH == 3 && a.KW == 3 &&
                        a.stride == 1 && a.pad_h == 1 && a.pad_w == 1 && a.C == 64 && a.H == a.OH &&
-                       a.W == a.OW && !a.accumulate && !mask.has_value() &&
+                       a.W == a.OW && !a.accumulate && !mask.has_value() && a.dtype == dv::DT_BF16 &&
                        (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad == 64);
   // persistent weight-resident halo kernel: 64-channel inputs at large maps (block1 of VGG16)
   const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112;
@@ -156,9 +160,10 @@ void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_
   const int64_t N = g[0], H = g[1], W = g[2], C = g[3], OH = g[4], OW = g[5], k = g[6], s = g[7], pad = g[8];
   TORCH_CHECK(C % 8 == 0 && k >= 1 && s >= 1 && pad >= 0 && pad < k, "pool: C%8, k, s, pad");
   TORCH_CHECK(OH == (H + 2 * pad - k) / s + 1 && OW == (W + 2 * pad - k) / s + 1, "pool: output size");
-  TORCH_CHECK(in.scalar_type() == at::kBFloat16 && in.is_contiguous() && out.scalar_type() == at::kBFloat16 &&
+  const auto dt = in.scalar_type();
+  TORCH_CHECK((dt == at::kBFloat16 || dt == at::kHalf) && in.is_contiguous() && out.scalar_type() == dt &&
                   out.is_contiguous(),
-              "pool: bf16 contiguous tensors");
+              "pool: bf16 or fp16 contiguous tensors of one dtype");
   const int64_t small = N * OH * OW * C, big = N * H * W * C;
   TORCH_CHECK(in.numel() == (dir == 0 ? big : small) && out.numel() == (dir == 0 ? small : big), "pool: sizes");
   uint8_t* ip = nullptr;
@@ -169,7 +174,7 @@ void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_
   }
   check_rc(dv::pool_launch((int)kind, (int)dir, reinterpret_cast<const uint16_t*>(in.data_ptr()),
                            reinterpret_cast<uint16_t*>(out.data_ptr()), ip, (int)N, (int)H, (int)W, (int)C, (int)OH,
-                           (int)OW, (int)k, (int)s, (int)pad, cur_stream()),
+                           (int)OW, (int)k, (int)s, (int)pad, dt == at::kHalf ? dv::DT_F16 : dv::DT_BF16, cur_stream()),
            "pool");
 }
 

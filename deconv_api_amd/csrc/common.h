@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kernels.h"  // DT_BF16 / DT_F16
+
 namespace dv {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -26,7 +28,40 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
+// ---- 16-bit storage dtype trait: DT 0 = bf16, DT 1 = fp16 (IEEE half) ----
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+
+template <int DT>
+__device__ __forceinline__ float to_f(uint32_t bits16) {
+  if constexpr (DT == DT_BF16) return __uint_as_float(bits16 << 16);
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+}
+template <int DT>
+__device__ __forceinline__ uint16_t from_f(float f) {
+  if constexpr (DT == DT_BF16) return __builtin_bit_cast(uint16_t, (__bf16)f);
+  else return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+template <int DT>
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)from_f<DT>(lo) | ((uint32_t)from_f<DT>(hi) << 16);
+}
+template <int DT>
+struct Vec8 {
+  typedef bf16x8 type;
+};
+template <>
+struct Vec8<DT_F16> {
+  typedef f16x8 type;
+};
+template <int DT>
+__device__ __forceinline__ f32x4 mfma16x16x32(const typename Vec8<DT>::type& a, const typename Vec8<DT>::type& b,
+                                              const f32x4& c) {
+  if constexpr (DT == DT_BF16) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
 // bf16 lane predicates on a packed pair (bits of two bf16 values in one u32)
+// (sign-bit / zero tests: valid for fp16 bit patterns too)
 __device__ __forceinline__ uint32_t relu_bf2(uint32_t v) {
   uint32_t lo = (v & 0x8000u) ? 0u : (v & 0xFFFFu);
   uint32_t hi = (v & 0x80000000u) ? 0u : (v & 0xFFFF0000u);

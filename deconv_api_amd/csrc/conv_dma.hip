@@ -55,10 +55,11 @@ __device__ __forceinline__ int row_xor(int row) {
 
 }  // namespace
 
-template <int FM, int FN, int EPI, bool accum>
+template <int DT, int FM, int FN, int EPI, bool accum>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane);
 
-template <int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED>
+// DT: 16-bit storage/MFMA dtype of x, w and a 16-bit output (DT_BF16 / DT_F16, common.h)
+template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED>
 __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a, int tiles_n) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16;
@@ -263,28 +264,28 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
     const uint8_t* Bs = As + A_BYTES;
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
-      bf16x8 bfr[FN];
+      typedef typename Vec8<DT>::type v8;
+      v8 bfr[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (b_row0 + j * 16) * ROWB + sw[s]);
+        bfr[j] = *reinterpret_cast<const v8*>(Bs + (b_row0 + j * 16) * ROWB + sw[s]);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + (a_row0 + i * 16) * ROWB + sw[s]);
+        const v8 af = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + sw[s]);
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af, bfr[j], acc[i][j]);
       }
     }
   }
 
   // ---- epilogue ----
   if (a.accumulate)
-    epilogue<FM, FN, EPI, true>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+    epilogue<DT, FM, FN, EPI, true>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
   else
-    epilogue<FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+    epilogue<DT, FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
 }
 
-template <int FM, int FN, int EPI, bool accum>
+template <int DT, int FM, int FN, int EPI, bool accum>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane) {
   const int row_l = (lane >> 4) * 4;
   const int col_l = lane & 15;
@@ -304,14 +305,14 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
         for (int r = 0; r < 4; ++r) {
           float v = acc[i][j][r] + bias;
           if (a.relu) v = fmaxf(v, 0.f);
-          v = bf2f(f2bf(v));
+          v = to_f<DT>(from_f<DT>(v));
           if (v > best) {
             best = v;
             code = r;
           }
         }
         const long long prow = rowb >> 2;
-        reinterpret_cast<uint16_t*>(a.out)[prow * a.out_ld + col] = f2bf(best);
+        reinterpret_cast<uint16_t*>(a.out)[prow * a.out_ld + col] = from_f<DT>(best);
         a.out_code[prow * a.OC + col] = (uint8_t)code;
       } else {
 #pragma unroll
@@ -327,8 +328,8 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
             out[o] = v;
           } else {
             uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
-            if (accum) v += bf2f(out[o]);
-            out[o] = f2bf(v);
+            if (accum) v += to_f<DT>(out[o]);
+            out[o] = from_f<DT>(v);
           }
         }
       }
@@ -336,7 +337,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
   }
 }
 
-template <int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI>
+template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI>
 static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   const int tiles_m = (a.M + BM - 1) / BM;
@@ -345,10 +346,10 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
   const bool aligned = (a.C % BK) == 0;
   if (aligned)
-    hipLaunchKernelGGL((conv_dma_kernel<WM, WN, FM, FN, BK, ST, AMODE, EPI, true>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true>), dim3((unsigned)nwg),
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   else
-    hipLaunchKernelGGL((conv_dma_kernel<WM, WN, FM, FN, BK, ST, AMODE, EPI, false>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false>), dim3((unsigned)nwg),
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   return (int)hipGetLastError();
 }
@@ -363,36 +364,45 @@ static int dma_variant() {
   return v;
 }
 
-template <int AMODE, int EPI>
+template <int DT, int AMODE, int EPI>
 static int dma_bn(const ConvArgs& a, hipStream_t s) {
   // measured (profiles/layers_r1_pipeline.txt): BK=32 x 4-stage rings lose to 2-stage BK=64 on the
   // 256x256 and 512x64 tiles; the 3-stage BK=64 ring wins slightly on 256x128.
-  const int v = dma_variant();
+  const int v = DT == DT_BF16 ? dma_variant() : 0;  // A/B variants are bf16-only
   if (a.OCpad % 256 == 0 && a.OC > 128) {
-    if (v == 2) return dma_cfg<2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
-    if (v == 3) return dma_cfg<2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
-    return dma_cfg<2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 256
+    if constexpr (DT == DT_BF16)
+      if (v == 2) return dma_cfg<DT, 2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
+    if constexpr (DT == DT_BF16)
+      if (v == 3) return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
+    return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 256
   }
   if (a.OCpad % 128 == 0 && a.OC > 64) {
-    if (v == 1) return dma_cfg<4, 2, 4, 4, 64, 2, AMODE, EPI>(a, s);
-    return dma_cfg<4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 256 x 128
+    if constexpr (DT == DT_BF16)
+      if (v == 1) return dma_cfg<DT, 4, 2, 4, 4, 64, 2, AMODE, EPI>(a, s);
+    return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 256 x 128
   }
   if (a.OCpad % 64 == 0 && a.OC > 16) {
-    if (v == 2) return dma_cfg<8, 1, 4, 4, 32, 4, AMODE, EPI>(a, s);
-    return dma_cfg<8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s);  // 512 x 64
+    if constexpr (DT == DT_BF16)
+      if (v == 2) return dma_cfg<DT, 8, 1, 4, 4, 32, 4, AMODE, EPI>(a, s);
+    return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s);  // 512 x 64
   }
-  if (a.OCpad % 16 == 0) return dma_cfg<8, 1, 4, 1, 64, 2, AMODE, EPI>(a, s);  // 512 x 16
+  if (a.OCpad % 16 == 0) return dma_cfg<DT, 8, 1, 4, 1, 64, 2, AMODE, EPI>(a, s);  // 512 x 16
   return -3;
 }
 
 int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t s) {
   if (a.C % 8 != 0 || a.Kpad % 64 != 0 || a.mask != nullptr || a.x_ld % 8 != 0) return -4;
+  if (a.dtype == DT_F16) {  // DeepDream fp16 path (BASELINE config 5): forward + dgrad
+    if (amode == CONV_A_FWD && epi == CONV_E_BF16) return dma_bn<DT_F16, CONV_A_FWD, CONV_E_BF16>(a, s);
+    if (amode == CONV_A_TRANSPOSE && epi == CONV_E_BF16) return dma_bn<DT_F16, CONV_A_TRANSPOSE, CONV_E_BF16>(a, s);
+    return -1;
+  }
   if (amode == CONV_A_FWD) {
-    if (epi == CONV_E_BF16) return dma_bn<CONV_A_FWD, CONV_E_BF16>(a, s);
-    if (epi == CONV_E_POOL) return dma_bn<CONV_A_FWD, CONV_E_POOL>(a, s);
-    if (epi == CONV_E_F32) return dma_bn<CONV_A_FWD, CONV_E_F32>(a, s);
+    if (epi == CONV_E_BF16) return dma_bn<DT_BF16, CONV_A_FWD, CONV_E_BF16>(a, s);
+    if (epi == CONV_E_POOL) return dma_bn<DT_BF16, CONV_A_FWD, CONV_E_POOL>(a, s);
+    if (epi == CONV_E_F32) return dma_bn<DT_BF16, CONV_A_FWD, CONV_E_F32>(a, s);
   } else if (amode == CONV_A_TRANSPOSE) {
-    if (epi == CONV_E_BF16) return dma_bn<CONV_A_TRANSPOSE, CONV_E_BF16>(a, s);
+    if (epi == CONV_E_BF16) return dma_bn<DT_BF16, CONV_A_TRANSPOSE, CONV_E_BF16>(a, s);
   }
   return -1;
 }

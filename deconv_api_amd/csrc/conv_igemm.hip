@@ -30,7 +30,7 @@ __device__ __forceinline__ int lds_off(int row, int chunk) {
   return row * 128 + ((chunk ^ (row & 7)) << 4);
 }
 
-template <int WM, int WN, int FM, int FN, int AMODE, int EPI, bool MASK_IN>
+template <int DT, int WM, int WN, int FM, int FN, int AMODE, int EPI, bool MASK_IN>
 __global__ void __launch_bounds__(256, 2) conv_igemm_kernel(const ConvArgs a, int tiles_n) {
   constexpr int BM = WM * FM * 16;
   constexpr int BN = WN * FN * 16;
@@ -227,19 +227,20 @@ __global__ void __launch_bounds__(256, 2) conv_igemm_kernel(const ConvArgs a, in
     const uint8_t* Bs = As + A_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 af[FM], bfr[FN];
+      typedef typename Vec8<DT>::type v8;
+      v8 af[FM], bfr[FN];
       const int chunk = s * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + lds_off(wm * FM * 16 + i * 16 + (lane & 15), chunk));
+        af[i] = *reinterpret_cast<const v8*>(As + lds_off(wm * FM * 16 + i * 16 + (lane & 15), chunk));
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + lds_off(wn * FN * 16 + j * 16 + (lane & 15), chunk));
+        bfr[j] = *reinterpret_cast<const v8*>(Bs + lds_off(wn * FN * 16 + j * 16 + (lane & 15), chunk));
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16x16x32<DT>(af[i], bfr[j], acc[i][j]);
     }
     if (more) store_tile(cur ^ 1);
     __syncthreads();
@@ -264,14 +265,14 @@ __global__ void __launch_bounds__(256, 2) conv_igemm_kernel(const ConvArgs a, in
         for (int r = 0; r < 4; ++r) {
           float v = acc[i][j][r] + bias;
           if (a.relu) v = fmaxf(v, 0.f);
-          v = bf2f(f2bf(v));  // pool on the stored (bf16) values: ties resolve like the stored map
+          v = to_f<DT>(from_f<DT>(v));  // pool on the stored (bf16) values: ties resolve like the stored map
           if (v > best) {     // strict: first max in row-major window order wins
             best = v;
             code = r;
           }
         }
         const long long prow = rowb >> 2;
-        reinterpret_cast<uint16_t*>(a.out)[prow * a.out_ld + col] = f2bf(best);
+        reinterpret_cast<uint16_t*>(a.out)[prow * a.out_ld + col] = from_f<DT>(best);
         a.out_code[prow * a.OC + col] = (uint8_t)code;
       } else {
 #pragma unroll
@@ -287,8 +288,8 @@ __global__ void __launch_bounds__(256, 2) conv_igemm_kernel(const ConvArgs a, in
             out[o] = v;
           } else {
             uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
-            if (a.accumulate) v += bf2f(out[o]);
-            out[o] = f2bf(v);
+            if (a.accumulate) v += to_f<DT>(out[o]);
+            out[o] = from_f<DT>(v);
           }
         }
       }
@@ -296,41 +297,51 @@ __global__ void __launch_bounds__(256, 2) conv_igemm_kernel(const ConvArgs a, in
   }
 }
 
-template <int WM, int WN, int FM, int FN, int AMODE, int EPI, bool MASK_IN>
+template <int DT, int WM, int WN, int FM, int FN, int AMODE, int EPI, bool MASK_IN>
 static int launch_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   const int tiles_m = (a.M + BM - 1) / BM;
   const int tiles_n = a.OCpad / BN;
   const long long nwg = (long long)tiles_m * tiles_n;
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
-  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, FM, FN, AMODE, EPI, MASK_IN>), dim3((unsigned)nwg),
+  hipLaunchKernelGGL((conv_igemm_kernel<DT, WM, WN, FM, FN, AMODE, EPI, MASK_IN>), dim3((unsigned)nwg),
                      dim3(256), 0, s, a, tiles_n);
   return (int)hipGetLastError();
 }
 
-template <int AMODE, int EPI, bool MASK_IN>
+template <int DT, int AMODE, int EPI, bool MASK_IN>
 static int launch_bn(const ConvArgs& a, hipStream_t s) {
-  if (a.OCpad % 128 == 0 && a.OC > 64) return launch_cfg<2, 2, 4, 4, AMODE, EPI, MASK_IN>(a, s);
-  if (a.OCpad % 64 == 0 && a.OC > 16) return launch_cfg<4, 1, 4, 4, AMODE, EPI, MASK_IN>(a, s);
-  if (a.OCpad % 16 == 0) return launch_cfg<4, 1, 4, 1, AMODE, EPI, MASK_IN>(a, s);
+  if (a.OCpad % 128 == 0 && a.OC > 64) return launch_cfg<DT, 2, 2, 4, 4, AMODE, EPI, MASK_IN>(a, s);
+  if (a.OCpad % 64 == 0 && a.OC > 16) return launch_cfg<DT, 4, 1, 4, 4, AMODE, EPI, MASK_IN>(a, s);
+  if (a.OCpad % 16 == 0) return launch_cfg<DT, 4, 1, 4, 1, AMODE, EPI, MASK_IN>(a, s);
   return -3;
 }
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t s) {
   const bool mask = a.mask != nullptr;
   if (a.C % 8 != 0 || a.Kpad % kBK != 0) return -4;
+  if (a.dtype == DT_F16) {  // fp16 DeepDream: forward, and dgrad with/without the ReLU mask
+    if (epi != CONV_E_BF16) return -1;
+    if (amode == CONV_A_FWD)
+      return mask ? launch_bn<DT_F16, CONV_A_FWD, CONV_E_BF16, true>(a, s)
+                  : launch_bn<DT_F16, CONV_A_FWD, CONV_E_BF16, false>(a, s);
+    if (amode == CONV_A_TRANSPOSE)
+      return mask ? launch_bn<DT_F16, CONV_A_TRANSPOSE, CONV_E_BF16, true>(a, s)
+                  : launch_bn<DT_F16, CONV_A_TRANSPOSE, CONV_E_BF16, false>(a, s);
+    return -1;
+  }
   if (amode == CONV_A_FWD) {
-    if (epi == CONV_E_BF16) return mask ? launch_bn<CONV_A_FWD, CONV_E_BF16, true>(a, s)
-                                        : launch_bn<CONV_A_FWD, CONV_E_BF16, false>(a, s);
-    if (epi == CONV_E_POOL && !mask) return launch_bn<CONV_A_FWD, CONV_E_POOL, false>(a, s);
-    if (epi == CONV_E_F32) return mask ? launch_bn<CONV_A_FWD, CONV_E_F32, true>(a, s)
-                                       : launch_bn<CONV_A_FWD, CONV_E_F32, false>(a, s);
+    if (epi == CONV_E_BF16) return mask ? launch_bn<DT_BF16, CONV_A_FWD, CONV_E_BF16, true>(a, s)
+                                        : launch_bn<DT_BF16, CONV_A_FWD, CONV_E_BF16, false>(a, s);
+    if (epi == CONV_E_POOL && !mask) return launch_bn<DT_BF16, CONV_A_FWD, CONV_E_POOL, false>(a, s);
+    if (epi == CONV_E_F32) return mask ? launch_bn<DT_BF16, CONV_A_FWD, CONV_E_F32, true>(a, s)
+                                       : launch_bn<DT_BF16, CONV_A_FWD, CONV_E_F32, false>(a, s);
   } else if (amode == CONV_A_UNPOOL && !mask) {
-    if (epi == CONV_E_BF16) return launch_bn<CONV_A_UNPOOL, CONV_E_BF16, false>(a, s);
-    if (epi == CONV_E_F32) return launch_bn<CONV_A_UNPOOL, CONV_E_F32, false>(a, s);
+    if (epi == CONV_E_BF16) return launch_bn<DT_BF16, CONV_A_UNPOOL, CONV_E_BF16, false>(a, s);
+    if (epi == CONV_E_F32) return launch_bn<DT_BF16, CONV_A_UNPOOL, CONV_E_F32, false>(a, s);
   } else if (amode == CONV_A_TRANSPOSE) {
-    if (epi == CONV_E_BF16) return mask ? launch_bn<CONV_A_TRANSPOSE, CONV_E_BF16, true>(a, s)
-                                        : launch_bn<CONV_A_TRANSPOSE, CONV_E_BF16, false>(a, s);
+    if (epi == CONV_E_BF16) return mask ? launch_bn<DT_BF16, CONV_A_TRANSPOSE, CONV_E_BF16, true>(a, s)
+                                        : launch_bn<DT_BF16, CONV_A_TRANSPOSE, CONV_E_BF16, false>(a, s);
   }
   return -1;  // unsupported combination
 }

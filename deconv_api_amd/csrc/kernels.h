@@ -19,6 +19,9 @@ enum ConvEpi : int {
   CONV_E_F32 = 2,   // (+bias)(ReLU)(+=out) -> fp32
 };
 
+// 16-bit storage dtypes (ConvArgs::dtype, pool_launch)
+enum { DT_BF16 = 0, DT_F16 = 1 };
+
 struct ConvArgs {
   const uint16_t* x;      // NHWC bf16 input (pooled map in UNPOOL mode, dy in TRANSPOSE mode)
   long long x_ld;         // elements between consecutive pixels of x (>= C; concat slices)
@@ -37,6 +40,7 @@ struct ConvArgs {
   int K, Kpad;
   int M;                  // GEMM rows = N*OH*OW
   int relu, relu_in, accumulate;
+  int dtype;              // 16-bit storage dtype of x/w/mask/16-bit out: 0 bf16, 1 fp16
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
@@ -69,7 +73,7 @@ namespace dv {
 // k x k pooling (pool.hip). kind 0 max (idx = uint8 window position), 1 avg (count_include_pad=0);
 // dir 0 forward (in = x [N,H,W,C], out = y [N,OH,OW,C]), 1 backward (in = gy, out = gx)
 int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C,
-                int OH, int OW, int k, int s, int pad, hipStream_t st);
+                int OH, int OW, int k, int s, int pad, int dtype, hipStream_t st);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s);
 }  // namespace dv

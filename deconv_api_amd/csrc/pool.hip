@@ -1,5 +1,5 @@
 // k x k pooling forward/backward for the DeepDream networks (InceptionV3 / ResNet-50), NHWC bf16,
-// one thread per (pixel, 8-channel chunk): 16-B loads/stores throughout.
+// bf16 or fp16 (template DT), one thread per (pixel, 8-channel chunk): 16-B loads/stores throughout.
 //   maxpool fwd: first-max (row-major) argmax kept as a uint8 window position per element;
 //   maxpool bwd: gather form (no atomics): each input pixel sums the gradients of the (at most
 //                ceil(k/s)^2) windows that contain it and chose it;
@@ -13,6 +13,7 @@ struct PoolGeom {
   int N, H, W, C, OH, OW, k, s, pad;
 };
 
+template <int DT>
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeom g) {
   const int cpp = g.C >> 3;
@@ -41,7 +42,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
         const int pos = kh * g.k + kw;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float f = bf2f((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+          const float f = to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
           if (f > best[e]) {
             best[e] = f;
             bi[e] = pos;
@@ -50,10 +51,10 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
       }
     }
     uint4 o;
-    o.x = pack_bf2(best[0], best[1]);
-    o.y = pack_bf2(best[2], best[3]);
-    o.z = pack_bf2(best[4], best[5]);
-    o.w = pack_bf2(best[6], best[7]);
+    o.x = pack2<DT>(best[0], best[1]);
+    o.y = pack2<DT>(best[2], best[3]);
+    o.z = pack2<DT>(best[4], best[5]);
+    o.w = pack2<DT>(best[6], best[7]);
     *reinterpret_cast<uint4*>(y + pix * g.C + ch * 8) = o;
     uint2 ix;
     ix.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
@@ -62,6 +63,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
   }
 }
 
+template <int DT>
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __restrict__ gy, const uint8_t* __restrict__ idx,
                                                           uint16_t* __restrict__ gx, PoolGeom g) {
   const int cpp = g.C >> 3;
@@ -90,15 +92,15 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t ie = ((e < 4 ? ix.x : ix.y) >> (8 * (e & 3))) & 0xFFu;
-          if (ie == pos) acc[e] += bf2f((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+          if (ie == pos) acc[e] += to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
         }
       }
     }
     uint4 o;
-    o.x = pack_bf2(acc[0], acc[1]);
-    o.y = pack_bf2(acc[2], acc[3]);
-    o.z = pack_bf2(acc[4], acc[5]);
-    o.w = pack_bf2(acc[6], acc[7]);
+    o.x = pack2<DT>(acc[0], acc[1]);
+    o.y = pack2<DT>(acc[2], acc[3]);
+    o.z = pack2<DT>(acc[4], acc[5]);
+    o.w = pack2<DT>(acc[6], acc[7]);
     *reinterpret_cast<uint4*>(gx + pix * g.C + ch * 8) = o;
   }
 }
@@ -108,6 +110,7 @@ __device__ __forceinline__ int win_count(int o, int s, int pad, int k, int L) {
   return hi - lo + 1;
 }
 
+template <int DT>
 __global__ void __launch_bounds__(256) avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           PoolGeom g) {
   const int cpp = g.C >> 3;
@@ -128,19 +131,20 @@ __global__ void __launch_bounds__(256) avgpool_fwd_kernel(const uint16_t* __rest
         const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.C + ch * 8);
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += bf2f((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+        for (int e = 0; e < 8; ++e) acc[e] += to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
       }
     }
     const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, g.k, g.H) * win_count(ow, g.s, g.pad, g.k, g.W));
     uint4 o;
-    o.x = pack_bf2(acc[0] * inv, acc[1] * inv);
-    o.y = pack_bf2(acc[2] * inv, acc[3] * inv);
-    o.z = pack_bf2(acc[4] * inv, acc[5] * inv);
-    o.w = pack_bf2(acc[6] * inv, acc[7] * inv);
+    o.x = pack2<DT>(acc[0] * inv, acc[1] * inv);
+    o.y = pack2<DT>(acc[2] * inv, acc[3] * inv);
+    o.z = pack2<DT>(acc[4] * inv, acc[5] * inv);
+    o.w = pack2<DT>(acc[6] * inv, acc[7] * inv);
     *reinterpret_cast<uint4*>(y + pix * g.C + ch * 8) = o;
   }
 }
 
+template <int DT>
 __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __restrict__ gy, uint16_t* __restrict__ gx,
                                                           PoolGeom g) {
   const int cpp = g.C >> 3;
@@ -164,14 +168,14 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __rest
         const uint4 v = *reinterpret_cast<const uint4*>(gy + ((n * g.OH + oh) * g.OW + ow) * g.C + ch * 8);
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += inv * bf2f((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+        for (int e = 0; e < 8; ++e) acc[e] += inv * to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
       }
     }
     uint4 o;
-    o.x = pack_bf2(acc[0], acc[1]);
-    o.y = pack_bf2(acc[2], acc[3]);
-    o.z = pack_bf2(acc[4], acc[5]);
-    o.w = pack_bf2(acc[6], acc[7]);
+    o.x = pack2<DT>(acc[0], acc[1]);
+    o.y = pack2<DT>(acc[2], acc[3]);
+    o.z = pack2<DT>(acc[4], acc[5]);
+    o.w = pack2<DT>(acc[6], acc[7]);
     *reinterpret_cast<uint4*>(gx + pix * g.C + ch * 8) = o;
   }
 }
@@ -180,22 +184,29 @@ static unsigned grid_for(long long total) {
   return (unsigned)std::min<long long>((total + 255) / 256, 256LL * 32);
 }
 
-int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C, int OH,
-                int OW, int k, int s, int pad, hipStream_t st) {
-  if (C % 8 != 0 || k <= 0 || s <= 0 || k > 15) return -1;
-  PoolGeom g{N, H, W, C, OH, OW, k, s, pad};
-  const long long out_total = (long long)N * OH * OW * (C / 8), in_total = (long long)N * H * W * (C / 8);
+template <int DT>
+static int pool_dt(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, const PoolGeom& g,
+                   hipStream_t st) {
+  const long long out_total = (long long)g.N * g.OH * g.OW * (g.C / 8), in_total = (long long)g.N * g.H * g.W * (g.C / 8);
   if (kind == 0 && dir == 0)
-    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(out_total)), dim3(256), 0, st, in, out, idx, g);
+    hipLaunchKernelGGL(maxpool_fwd_kernel<DT>, dim3(grid_for(out_total)), dim3(256), 0, st, in, out, idx, g);
   else if (kind == 0 && dir == 1)
-    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(in_total)), dim3(256), 0, st, in, idx, out, g);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<DT>, dim3(grid_for(in_total)), dim3(256), 0, st, in, idx, out, g);
   else if (kind == 1 && dir == 0)
-    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for(out_total)), dim3(256), 0, st, in, out, g);
+    hipLaunchKernelGGL(avgpool_fwd_kernel<DT>, dim3(grid_for(out_total)), dim3(256), 0, st, in, out, g);
   else if (kind == 1 && dir == 1)
-    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(in_total)), dim3(256), 0, st, in, out, g);
+    hipLaunchKernelGGL(avgpool_bwd_kernel<DT>, dim3(grid_for(in_total)), dim3(256), 0, st, in, out, g);
   else
     return -2;
   return (int)hipGetLastError();
+}
+
+int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C, int OH,
+                int OW, int k, int s, int pad, int dtype, hipStream_t st) {
+  if (C % 8 != 0 || k <= 0 || s <= 0 || k > 15) return -1;
+  const PoolGeom g{N, H, W, C, OH, OW, k, s, pad};
+  return dtype == DT_F16 ? pool_dt<DT_F16>(kind, dir, in, out, idx, g, st)
+                         : pool_dt<DT_BF16>(kind, dir, in, out, idx, g, st);
 }
 
 }  // namespace dv

@@ -61,7 +61,9 @@ class DeepDream:
         self.net = net
         self.s = settings or DreamSettings()
         self.device = net.device
-        self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        if dtype is None:
+            dtype = getattr(net, "dtype", torch.bfloat16) if self.device.type == "cuda" else torch.float32
+        self.dtype = dtype
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self._graphs: Dict[tuple, tuple] = {}
 

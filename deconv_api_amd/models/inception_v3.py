@@ -82,10 +82,12 @@ class InceptionV3:
             cin = 2048
 
     # ----------------------------------------------------------------- runtime
-    def build(self, device) -> "InceptionV3":
+    def build(self, device, dtype=torch.bfloat16) -> "InceptionV3":
+        """Pack weights for ``device``; ``dtype`` is the GPU storage dtype (bf16 or fp16)."""
         self.device = torch.device(device)
+        self.dtype = dtype
         for u in self.units.values():
-            u.build(self.device)
+            u.build(self.device, dtype)
         return self
 
     def num_params(self) -> int:

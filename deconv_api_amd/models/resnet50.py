@@ -51,10 +51,12 @@ class ResNet50:
     def block_names(self) -> List[str]:
         return [b[0] for b in self.blocks]
 
-    def build(self, device) -> "ResNet50":
+    def build(self, device, dtype=torch.bfloat16) -> "ResNet50":
+        """Pack weights for ``device``; ``dtype`` is the GPU storage dtype (bf16 or fp16)."""
         self.device = torch.device(device)
+        self.dtype = dtype
         for u in self.units.values():
-            u.build(self.device)
+            u.build(self.device, dtype)
         return self
 
     def num_params(self) -> int:

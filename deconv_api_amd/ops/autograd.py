@@ -41,20 +41,22 @@ class ConvUnit:
     def cout(self):
         return self.w.shape[0]
 
-    def build(self, device) -> "ConvUnit":
+    def build(self, device, dtype=torch.bfloat16) -> "ConvUnit":
+        """``dtype``: 16-bit storage/MFMA dtype of the GPU path (bf16, or fp16 for config 5)."""
         self.device = torch.device(device)
+        self.dtype = dtype
         w8 = pad_channels_oihw(self.w)
         self.w_dev = w8.to(self.device)
         self.b_dev = None if self.b is None else self.b.to(self.device)
         if self.device.type == "cuda":
-            self.fwd = ConvWeights(w8, self.b, "fwd").to_device(self.device)
+            self.fwd = ConvWeights(w8, self.b, "fwd").to_device(self.device, dtype)
             kh, kw = self.w.shape[2:]
             if self.stride == 1:
                 wd = pad_channels_oihw(w8.flip(2, 3).transpose(0, 1).contiguous())
-                self.bwd = ConvWeights(wd, None, "fwd").to_device(self.device)
+                self.bwd = ConvWeights(wd, None, "fwd").to_device(self.device, dtype)
                 self.bwd_pad = (kh - 1 - self.pad[0], kw - 1 - self.pad[1])
             else:
-                self.bwd = ConvWeights(w8, None, "transpose").to_device(self.device)
+                self.bwd = ConvWeights(w8, None, "transpose").to_device(self.device, dtype)
         return self
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:

@@ -112,13 +112,15 @@ class ConvWeights:
         out[: self.cout, : self.K] = m
         return out
 
-    def to_device(self, device) -> "ConvWeights":
+    def to_device(self, device, dtype=torch.bfloat16) -> "ConvWeights":
+        """Copy to ``device``; on the GPU also pack the [OCpad, Kpad] GEMM matrix in ``dtype``
+        (bf16, or fp16 for the fp16 DeepDream path) and the fp32 padded bias."""
         device = torch.device(device)
         w_oihw = self.w_oihw.to(device)
         bias = None if self.bias is None else self.bias.to(device)
         cw = ConvWeights(w_oihw, bias, self.kind)
         if device.type == "cuda":
-            cw.w_gemm = self.gemm_matrix().to(device=device, dtype=torch.bfloat16).contiguous()
+            cw.w_gemm = self.gemm_matrix().to(device=device, dtype=dtype).contiguous()
             if bias is not None:
                 bp = torch.zeros(self.OCpad, dtype=torch.float32)
                 bp[: self.cout] = self.bias.float().cpu()
@@ -256,8 +258,11 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
 def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
                 epilogue, out, accumulate, use_bias):
     lib = native.lib()
-    assert x.dtype == torch.bfloat16 and x.stride(3) == 1, "conv2d(hip): x must be bf16 NHWC (channel stride 1)"
+    dt = x.dtype
+    assert dt in (torch.bfloat16, torch.float16) and x.stride(3) == 1, \
+        "conv2d(hip): x must be bf16/fp16 NHWC (channel stride 1)"
     assert cw.w_gemm is not None, "conv2d(hip): weights not packed for the device (ConvWeights.to_device)"
+    assert cw.w_gemm.dtype == dt, f"conv2d(hip): weights packed as {cw.w_gemm.dtype}, input is {dt}"
     x_ld = x.stride(2)
     if in_mode != "unpool":
         assert x.stride(1) == W * x_ld and x.stride(0) == H * W * x_ld, "conv2d(hip): x pixels must be dense"
@@ -265,18 +270,18 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
     if epilogue == "pool":
         assert OH % 2 == 0 and OW % 2 == 0
         if out is None:
-            out = torch.empty(N, OH // 2, OW // 2, OC, dtype=torch.bfloat16, device=x.device)
+            out = torch.empty(N, OH // 2, OW // 2, OC, dtype=dt, device=x.device)
         out_code = torch.empty(N, OH // 2, OW // 2, OC, dtype=torch.uint8, device=x.device)
     else:
         out_code = None
         if out is None:
-            odt = torch.float32 if epilogue == "f32" else torch.bfloat16
+            odt = torch.float32 if epilogue == "f32" else dt
             out = torch.empty(N, OH, OW, OC, dtype=odt, device=x.device)
     assert out.stride(-1) == 1
     out_ld = out.stride(-2) if out.dim() == 4 else OC
     mask_ld = 0
     if mask is not None:
-        assert mask.dtype == torch.bfloat16 and mask.stride(3) == 1
+        assert mask.dtype == dt and mask.stride(3) == 1
         mask_ld = mask.stride(2)
     if code is not None:
         code = code.contiguous()

@@ -144,6 +144,22 @@ def test_gpu_dream_gradient_matches_cpu(native_lib, which):
 
 
 @pytest.mark.gpu
+def test_gpu_resnet_dream_fp16(native_lib):
+    """BASELINE config 5 precision: fp16 storage + f16 MFMA through ResNet-50's conv/pool kernels."""
+    cpu, gpu = ResNet50(0).build("cpu"), ResNet50(0).build("cuda", torch.float16)
+    s = DreamSettings(layers=dict(RESNET_LAYERS))
+    x = (torch.rand(2, 128, 128, 3, generator=torch.Generator().manual_seed(4)) * 2 - 1)
+    x = x.to(torch.float16).float()
+    dd = DeepDream(gpu, s)
+    assert dd.dtype == torch.float16
+    lc, gc = DeepDream(cpu, s).loss_and_grad(x)
+    lg, gg = dd.loss_and_grad(x.cuda())
+    assert torch.isfinite(gg).all() and torch.allclose(lg.cpu(), lc, rtol=3e-2)
+    for b in range(2):
+        assert _cos(gg[b].cpu(), gc[b]) > 0.97
+
+
+@pytest.mark.gpu
 def test_gpu_graph_replay_equals_eager(native_lib):
     net = InceptionV3(0).build("cuda")
     s = DreamSettings(iterations=3, octaves=2)

@@ -245,3 +245,55 @@ def test_conv_deterministic(native_lib):
     a = ops.conv2d(x, cw)
     b = ops.conv2d(x, cw)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,H,W,C,OC,stride", [(2, 16, 16, 64, 64, 1), (1, 9, 7, 128, 256, 1),
+                                               (2, 17, 13, 24, 200, 1), (2, 15, 15, 64, 128, 2)])
+def test_conv_fp16_fwd_mask_transpose(native_lib, conv_impl, N, H, W, C, OC, stride):
+    """fp16 storage + f16 MFMA (DeepDream config 5): forward, ReLU-masked dgrad and strided
+    transposed dgrad vs the fp32 reference on fp16-rounded operands."""
+    g = torch.Generator().manual_seed(5)
+    h = lambda t: t.to(torch.float16).float()  # noqa: E731
+    x = h(torch.randn(N, H, W, C, generator=g))
+    w = h(torch.randn(OC, C, 3, 3, generator=g) / np.sqrt(9 * C))
+    b = h(torch.randn(OC, generator=g) * 0.1)
+    cw = ConvWeights(w, b, "fwd")
+    cwd = cw.to_device(DEV, torch.float16)
+    ref = ops.conv2d(x, cw, stride=stride)
+    got = ops.conv2d(x.to(torch.float16).to(DEV), cwd, stride=stride)
+    assert got.dtype == torch.float16 and _rel(got, ref) < 4e-3
+    # dgrad through the ReLU: masked, transposed gather (stride > 1) or flipped kernel (stride 1)
+    gy = h(torch.randn(*ref.shape, generator=g))
+    ct = ConvWeights(w, None, "transpose")
+    if stride == 1:
+        wd = pad_channels_oihw(w.flip(2, 3).transpose(0, 1).contiguous())
+        cb = ConvWeights(wd, None, "fwd")
+        kw = dict(stride=1, relu=False, mask=None, use_bias=False)
+    else:
+        cb = ct
+        kw = dict(stride=stride, pad=1, relu=False, in_mode="transpose", out_hw=(H, W), use_bias=False)
+    for use_mask in (False, True):
+        if use_mask and conv_impl == "dma":
+            continue  # the LDS-DMA kernel has no mask prologue
+        m = ref if use_mask else None
+        kw["mask"] = m
+        r = ops.conv2d(gy, cb, **kw)
+        kw["mask"] = None if m is None else m.to(torch.float16).to(DEV)
+        o = ops.conv2d(gy.to(torch.float16).to(DEV), cb.to_device(DEV, torch.float16), **kw)
+        assert _rel(o, r) < 4e-3, (stride, use_mask)
+
+
+def test_pool_fp16(native_lib):
+    from deconv_api_amd.ops.autograd import avg_pool, max_pool
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 13, 11, 24, generator=g).to(torch.float16).float()
+    for fn in (max_pool, avg_pool):
+        xc = x.clone().requires_grad_(True)
+        yc = fn(xc, 3, 2, 1)
+        gy = torch.randn_like(yc).to(torch.float16).float()
+        (gc,) = torch.autograd.grad(yc, xc, gy)
+        xd = x.to(torch.float16).cuda().requires_grad_(True)
+        yd = fn(xd, 3, 2, 1)
+        (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.float16).cuda())
+        assert yd.dtype == torch.float16 and _rel(yd, yc) < 2e-3 and _rel(gd, gc) < 2e-3
