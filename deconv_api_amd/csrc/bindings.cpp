@@ -37,7 +37,7 @@ void check_rc(int rc, const char* what) {
 //       code_div, x_ld, mask_ld, out_ld
 void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
           c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
-          int64_t epi, int64_t impl) {
+          int64_t epi, int64_t impl, c10::optional<Tensor> res) {
   TORCH_CHECK(g.size() == 23, "conv: geometry vector must have 23 entries");
   check_cuda(x, "x");
   check_cuda(w, "w");
@@ -111,23 +111,39 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   }
   need(out, ((out_rows - 1) * a.out_ld + a.OC) * (int64_t)out.element_size(), "out");
   a.out = out.data_ptr();
+  if (res.has_value()) {  // fused residual: LDS-DMA forward conv with a 16-bit output only
+    check_cuda(*res, "res");
+    TORCH_CHECK(res->scalar_type() == dt && res->dim() == 4 && res->stride(3) == 1, "res: x's dtype, NHWC");
+    TORCH_CHECK(amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16 && !mask.has_value() && !a.accumulate &&
+                    impl != 1 && impl != 3,
+                "res: forward conv with a 16-bit epilogue on the LDS-DMA kernel only");
+    a.res_ld = res->stride(2);
+    TORCH_CHECK(res->stride(1) == a.OW * a.res_ld && res->stride(0) == (int64_t)a.OH * a.OW * a.res_ld,
+                "res: pixels must be dense");
+    need(*res, ((int64_t)(a.M - 1) * a.res_ld + a.OC) * 2, "res");
+    a.res = reinterpret_cast<const uint16_t*>(res->data_ptr());
+  }
   // Kernel choice. impl: 0 auto, 1 register-staged (conv_igemm), 2 LDS-DMA (conv_dma), 3 halo-tile.
   //  * halo-tile (3x3 s1 p1, OC tile <= 64, >= 56x56 maps): input staged once per tile, unpool fused
-  //  * LDS-DMA: FWD / TRANSPOSE without mask; an unpool input is first materialized (vector kernel)
-  //  * register-staged: everything else (ReLU-mask prologue, fused unpool gather)
+  //  * LDS-DMA: FWD / TRANSPOSE (optionally ReLU-masked); an unpool input is first materialized
+  //  * register-staged: everything else (mask with its own pixel stride, fused unpool gather)
   const bool halo_ok = (amode == dv::CONV_A_FWD || amode == dv::CONV_A_UNPOOL) && a.KH == 3 && a.KW == 3 &&
                        a.stride == 1 && a.pad_h == 1 && a.pad_w == 1 && a.C == 64 && a.H == a.OH &&
                        a.W == a.OW && !a.accumulate && !mask.has_value() && a.dtype == dv::DT_BF16 &&
                        (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad == 64);
   // persistent weight-resident halo kernel: 64-channel inputs at large maps (block1 of VGG16)
-  const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112;
+  const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112 && a.res == nullptr;
   if (impl == 3 || (impl == 0 && halo_auto)) {
     TORCH_CHECK(halo_ok, "conv: halo-tile kernel does not support this shape/mode");
     check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream()), "conv_halo");
     return;
   }
-  const bool dma_mode = (amode == dv::CONV_A_FWD || amode == dv::CONV_A_UNPOOL ||
-                         (amode == dv::CONV_A_TRANSPOSE && epi == dv::CONV_E_BF16)) && !mask.has_value();
+  // ReLU-masked A (dgrad): the DMA kernel stages the mask with x's offsets, so it needs mask_ld == x_ld
+  const bool mask_dma = mask.has_value() && a.mask_ld == a.x_ld && epi == dv::CONV_E_BF16 &&
+                        (amode == dv::CONV_A_FWD || amode == dv::CONV_A_TRANSPOSE);
+  const bool dma_mode = ((amode == dv::CONV_A_FWD || amode == dv::CONV_A_UNPOOL ||
+                          (amode == dv::CONV_A_TRANSPOSE && epi == dv::CONV_E_BF16)) && !mask.has_value()) ||
+                        mask_dma;
   TORCH_CHECK(impl != 2 || dma_mode, "conv: LDS-DMA kernel does not support this mode");
   if (dma_mode && impl != 1) {
     Tensor unpooled;
@@ -176,6 +192,38 @@ void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_
                            reinterpret_cast<uint16_t*>(out.data_ptr()), ip, (int)N, (int)H, (int)W, (int)C, (int)OH,
                            (int)OW, (int)k, (int)s, (int)pad, dt == at::kHalf ? dv::DT_F16 : dv::DT_BF16, cur_stream()),
            "pool");
+}
+
+static int dt_of(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "expected a bf16 or fp16 tensor");
+  return t.scalar_type() == at::kHalf ? dv::DT_F16 : dv::DT_BF16;
+}
+
+// DeepDream loss core: part [N, P] fp32 partial sums of x^2 over x[:, b:H-b, b:W-b, :]
+void sumsq_core(Tensor x, Tensor part, int64_t b) {
+  check_cuda(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.size(3) % 8 == 0, "sumsq: x contiguous NHWC, C % 8");
+  TORCH_CHECK(part.dim() == 2 && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.size(0) == x.size(0),
+              "sumsq: part [N, P] fp32");
+  check_rc(dv::sumsq_core_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()), part.data_ptr<float>(),
+                                 (int)part.size(1), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3),
+                                 (int)b, dt_of(x), cur_stream()),
+           "sumsq_core");
+}
+
+void sumsq_core_bwd(Tensor x, Tensor scale, Tensor gx, int64_t b) {
+  check_cuda(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.size(3) % 8 == 0, "sumsq_bwd: x contiguous NHWC, C % 8");
+  TORCH_CHECK(gx.sizes() == x.sizes() && gx.scalar_type() == x.scalar_type() && gx.is_contiguous(), "sumsq_bwd: gx");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.is_contiguous() && scale.numel() == x.size(0),
+              "sumsq_bwd: scale [N] fp32");
+  check_rc(dv::sumsq_core_bwd_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()), scale.data_ptr<float>(),
+                                     reinterpret_cast<uint16_t*>(gx.data_ptr()), (int)x.size(0), (int)x.size(1),
+                                     (int)x.size(2), (int)x.size(3), (int)b, dt_of(x), cur_stream()),
+           "sumsq_core_bwd");
 }
 
 void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
@@ -290,8 +338,13 @@ void unpool2x2(Tensor p, Tensor code, Tensor out, int64_t code_div, bool relu) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "deconv_api_amd gfx950 (MI355X) HIP kernels";
-  m.def("conv", &conv, "MFMA implicit-GEMM conv (fwd / unpool-gather / transposed; bf16/pool/f32 epilogues)");
+  m.def("conv", &conv, "MFMA implicit-GEMM conv (fwd / unpool-gather / transposed; bf16/pool/f32 epilogues)",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("out_code"), py::arg("code"),
+        py::arg("mask"), py::arg("geom"), py::arg("amode"), py::arg("epi"), py::arg("impl"),
+        py::arg("res") = py::none());
   m.def("pool", &pool, "k x k max/avg pooling forward/backward");
+  m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
+  m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);
   m.def("seed_deconv3x3", &seed_deconv3x3);

@@ -75,6 +75,13 @@ __device__ __forceinline__ uint32_t mask_pos_bf2(uint32_t v, uint32_t m) {
   return lo | hi;
 }
 
+// keep the 16-bit elements of a where the matching element of m is > 0, 2 per u32, branch-free:
+// (m & 0x7FFF) + 0x7FFF sets bit 15 iff |m| != 0 (no carry across halves); & ~m clears negatives
+__device__ __forceinline__ uint32_t mask_pos_pk(uint32_t a, uint32_t m) {
+  const uint32_t pos = (((m & 0x7FFF7FFFu) + 0x7FFF7FFFu) & ~m) & 0x80008000u;
+  return a & __umul24(pos >> 15, 0xFFFFu);
+}
+
 // Bijective XCD-aware workgroup remap (MI355X: 8 XCDs, consecutive dispatch ids go to
 // different XCDs). After the remap logically-adjacent tiles share an XCD (and its L2).
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

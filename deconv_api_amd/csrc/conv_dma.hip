@@ -57,9 +57,16 @@ __device__ __forceinline__ int row_xor(int row) {
 
 template <int DT, int FM, int FN, int EPI, bool accum>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane);
+template <int DT, int FM, int FN>
+__device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw,
+                                             int lane);
 
 // DT: 16-bit storage/MFMA dtype of x, w and a 16-bit output (DT_BF16 / DT_F16, common.h)
-template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED>
+// MASK: backward through a ReLU: A elements are kept only where mask (same layout and pixel
+// stride as x) is > 0. The mask tile is DMA'd into LDS next to the A tile with the same offsets
+// and applied to each A fragment in registers right before its MFMAs.
+template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED,
+          bool MASK = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a, int tiles_n) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16;
@@ -69,7 +76,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   constexpr int RPI = 1024 / ROWB;          // rows per DMA instruction
   constexpr int A_BYTES = BM * ROWB;
   constexpr int B_BYTES = BN * ROWB;
-  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int M_BYTES = MASK ? A_BYTES : 0;
+  constexpr int STAGE = A_BYTES + M_BYTES + B_BYTES;
   constexpr int A_I = BM / RPI / NW;        // A DMA instructions per wave per K tile
   constexpr int B_GROUPS = BN / RPI;        // RPI-row groups of the B tile
   constexpr int B_FULL = B_GROUPS / NW, B_REM = B_GROUPS % NW;
@@ -101,6 +109,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   const long long x_total = (long long)a.N * img_elems;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(xb, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
+  __amdgpu_buffer_rsrc_t mr = xr;
+  if constexpr (MASK)
+    mr = make_rsrc(a.mask + (long long)n_base * img_elems, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
 
   // lane -> (row within its DMA row group, logical 16-B chunk at LDS position lane % CPR)
   const int lrow = lane / CPR;
@@ -164,7 +175,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
 
   auto issue = [&](int kt, int buf) {
     uint8_t* As = smem + buf * STAGE;
-    uint8_t* Bs = As + A_BYTES;
+    uint8_t* Bs = As + A_BYTES + M_BYTES;
     int kh, kw, ch, tap;
     bool kval;
     if constexpr (CALIGNED) {
@@ -210,6 +221,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
       const uint32_t voff =
           ok ? (uint32_t)((((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch) * 2) : kOOB;
       dma16(xr, As + (j * NW + wave) * 1024, voff);
+      if constexpr (MASK) dma16(mr, As + A_BYTES + (j * NW + wave) * 1024, voff);
     }
     }
 #pragma unroll
@@ -225,7 +237,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
 
   // wait until this wave's DMAs of the current tile landed, leaving `pend` younger tiles in flight
   auto wait_tiles = [&](int pend) {
-    constexpr int PT_LO = A_I + B_FULL, PT_HI = A_I + B_FULL + 1;
+    constexpr int PT_LO = A_I * (MASK ? 2 : 1) + B_FULL, PT_HI = PT_LO + 1;
     const bool hi = B_REM && wave < B_REM;
     if (pend <= 0) {
       wait_vm<0>();
@@ -261,7 +273,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
     __builtin_amdgcn_s_barrier();
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const uint8_t* As = smem + cur * STAGE;
-    const uint8_t* Bs = As + A_BYTES;
+    const uint8_t* Bs = As + A_BYTES + M_BYTES;
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       typedef typename Vec8<DT>::type v8;
@@ -271,7 +283,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
         bfr[j] = *reinterpret_cast<const v8*>(Bs + (b_row0 + j * 16) * ROWB + sw[s]);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const v8 af = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + sw[s]);
+        v8 af = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + sw[s]);
+        if constexpr (MASK) {
+          uint4 av = __builtin_bit_cast(uint4, af);
+          const uint4 mv = *reinterpret_cast<const uint4*>(As + A_BYTES + (a_row0 + i * 16) * ROWB + sw[s]);
+          av.x = mask_pos_pk(av.x, mv.x);
+          av.y = mask_pos_pk(av.y, mv.y);
+          av.z = mask_pos_pk(av.z, mv.z);
+          av.w = mask_pos_pk(av.w, mv.w);
+          af = __builtin_bit_cast(v8, av);
+        }
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af, bfr[j], acc[i][j]);
       }
@@ -279,10 +300,51 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   }
 
   // ---- epilogue ----
+  if constexpr (EPI == CONV_E_BF16 && AMODE == CONV_A_FWD && !MASK) {
+    if (a.res) {
+      epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+      return;
+    }
+  }
   if (a.accumulate)
     epilogue<DT, FM, FN, EPI, true>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
   else
     epilogue<DT, FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+}
+
+// residual epilogue (ResNet block tail): out = [ReLU](acc + bias + res). Each column group's
+// residual values are all loaded before its first store, so the loads overlap each other instead
+// of each waiting behind the previous store.
+template <int DT, int FM, int FN>
+__device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw,
+                                             int lane) {
+  const int row_l = (lane >> 4) * 4;
+  const int col_l = lane & 15;
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = nw + j * 16 + col_l;
+    if (col >= a.OC) continue;
+    const float bias = a.bias ? a.bias[col] : 0.f;
+    uint16_t rv[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = min(mw + i * 16 + row_l + r, a.M - 1);
+        rv[i][r] = a.res[(long long)row * a.res_ld + col];
+      }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mw + i * 16 + row_l + r;
+        if (row >= a.M) continue;
+        float v = acc[i][j][r] + bias + to_f<DT>(rv[i][r]);
+        if (a.relu) v = fmaxf(v, 0.f);
+        out[(long long)row * a.out_ld + col] = from_f<DT>(v);
+      }
+  }
 }
 
 template <int DT, int FM, int FN, int EPI, bool accum>
@@ -337,7 +399,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
   }
 }
 
-template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI>
+template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI, bool MASK = false>
 static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   const int tiles_m = (a.M + BM - 1) / BM;
@@ -346,10 +408,10 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
   const bool aligned = (a.C % BK) == 0;
   if (aligned)
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK>), dim3((unsigned)nwg),
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   else
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK>), dim3((unsigned)nwg),
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   return (int)hipGetLastError();
 }
@@ -364,34 +426,74 @@ static int dma_variant() {
   return v;
 }
 
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, cu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+    return cu > 0 ? cu : 256;
+  }();
+  return n;
+}
+
+// Tile choice: the largest tile (best MFMA:LDS ratio) unless it leaves CUs idle. A problem with
+// fewer big tiles than the chip has CUs (deep layers at small batch, strong-scaled tiles) drops to
+// the next smaller tile, which doubles the workgroup count and fits 2 workgroups per CU in LDS.
 template <int DT, int AMODE, int EPI>
 static int dma_bn(const ConvArgs& a, hipStream_t s) {
   // measured (profiles/layers_r1_pipeline.txt): BK=32 x 4-stage rings lose to 2-stage BK=64 on the
   // 256x256 and 512x64 tiles; the 3-stage BK=64 ring wins slightly on 256x128.
   const int v = DT == DT_BF16 ? dma_variant() : 0;  // A/B variants are bf16-only
+  const long long cus = num_cus();
+  auto nwg = [&](int BM, int BN) { return (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN); };
   if (a.OCpad % 256 == 0 && a.OC > 128) {
     if constexpr (DT == DT_BF16)
       if (v == 2) return dma_cfg<DT, 2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
-    if constexpr (DT == DT_BF16)
-      if (v == 3) return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
+    if (v == 3 || (nwg(256, 256) < cus && nwg(128, 256) >= cus))
+      return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
+    if (nwg(256, 256) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
     return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 256
   }
   if (a.OCpad % 128 == 0 && a.OC > 64) {
     if constexpr (DT == DT_BF16)
       if (v == 1) return dma_cfg<DT, 4, 2, 4, 4, 64, 2, AMODE, EPI>(a, s);
+    if (nwg(256, 128) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
     return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 256 x 128
   }
   if (a.OCpad % 64 == 0 && a.OC > 16) {
     if constexpr (DT == DT_BF16)
       if (v == 2) return dma_cfg<DT, 8, 1, 4, 4, 32, 4, AMODE, EPI>(a, s);
+    if (nwg(512, 64) < cus) return dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 64
     return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s);  // 512 x 64
   }
-  if (a.OCpad % 16 == 0) return dma_cfg<DT, 8, 1, 4, 1, 64, 2, AMODE, EPI>(a, s);  // 512 x 16
+  if (a.OCpad % 16 == 0) {
+    if (nwg(512, 16) < cus) return dma_cfg<DT, 8, 1, 2, 1, 64, 2, AMODE, EPI>(a, s);  // 256 x 16
+    return dma_cfg<DT, 8, 1, 4, 1, 64, 2, AMODE, EPI>(a, s);  // 512 x 16
+  }
+  return -3;
+}
+
+// ReLU-masked dgrad: the mask tile doubles A's LDS footprint, so smaller tiles than dma_bn
+// (<= 128 KiB of LDS per workgroup at 2 stages)
+template <int DT, int AMODE>
+static int dma_mask_bn(const ConvArgs& a, hipStream_t s) {
+  if (a.OCpad % 256 == 0 && a.OC > 128) return dma_cfg<DT, 2, 4, 4, 4, 64, 2, AMODE, CONV_E_BF16, true>(a, s);  // 128x256
+  if (a.OCpad % 128 == 0 && a.OC > 64) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, CONV_E_BF16, true>(a, s);   // 128x128
+  if (a.OCpad % 64 == 0 && a.OC > 16) return dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, CONV_E_BF16, true>(a, s);    // 256x64
+  if (a.OCpad % 16 == 0) return dma_cfg<DT, 8, 1, 2, 1, 64, 2, AMODE, CONV_E_BF16, true>(a, s);                // 256x16
   return -3;
 }
 
 int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t s) {
-  if (a.C % 8 != 0 || a.Kpad % 64 != 0 || a.mask != nullptr || a.x_ld % 8 != 0) return -4;
+  if (a.C % 8 != 0 || a.Kpad % 64 != 0 || a.x_ld % 8 != 0) return -4;
+  if (a.mask != nullptr) {
+    if (a.mask_ld != a.x_ld || epi != CONV_E_BF16) return -4;
+    if (amode == CONV_A_FWD)
+      return a.dtype == DT_F16 ? dma_mask_bn<DT_F16, CONV_A_FWD>(a, s) : dma_mask_bn<DT_BF16, CONV_A_FWD>(a, s);
+    if (amode == CONV_A_TRANSPOSE)
+      return a.dtype == DT_F16 ? dma_mask_bn<DT_F16, CONV_A_TRANSPOSE>(a, s)
+                               : dma_mask_bn<DT_BF16, CONV_A_TRANSPOSE>(a, s);
+    return -1;
+  }
   if (a.dtype == DT_F16) {  // DeepDream fp16 path (BASELINE config 5): forward + dgrad
     if (amode == CONV_A_FWD && epi == CONV_E_BF16) return dma_bn<DT_F16, CONV_A_FWD, CONV_E_BF16>(a, s);
     if (amode == CONV_A_TRANSPOSE && epi == CONV_E_BF16) return dma_bn<DT_F16, CONV_A_TRANSPOSE, CONV_E_BF16>(a, s);

@@ -1,0 +1,86 @@
+// DeepDream loss kernels (engine/deepdream.py): per-image sum of squares over the activation
+// "core" (the map without a `b`-pixel border, the Keras example's act[:, 2:-2, 2:-2, :]) and its
+// input gradient. NHWC bf16/fp16, 16-B vector loads, fp32 accumulation, deterministic (block
+// partials, summed by the caller in a fixed order; no atomics).
+#include "common.h"
+#include "kernels.h"
+
+namespace dv {
+
+template <int DT>
+__global__ void __launch_bounds__(256) sumsq_core_kernel(const uint16_t* __restrict__ x, float* __restrict__ part,
+                                                         int H, int W, int C, int b) {
+  const int n = blockIdx.y;
+  const int Hc = H - 2 * b, Wc = W - 2 * b, cpp = C >> 3;
+  const long long total = (long long)Hc * Wc * cpp;
+  const uint16_t* xn = x + (long long)n * H * W * C;
+  float acc = 0.f;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int ch = (int)(t % cpp);
+    const long long pix = t / cpp;
+    const int hh = (int)(pix / Wc) + b, ww = (int)(pix % Wc) + b;
+    const uint4 v = *reinterpret_cast<const uint4*>(xn + ((long long)hh * W + ww) * C + ch * 8);
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float lo = to_f<DT>(w4[e] & 0xFFFFu), hi = to_f<DT>(w4[e] >> 16);
+      acc += lo * lo + hi * hi;
+    }
+  }
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[(long long)n * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// gx = 2 * scale[n] * x inside the core, 0 on the border
+template <int DT>
+__global__ void __launch_bounds__(256) sumsq_core_bwd_kernel(const uint16_t* __restrict__ x,
+                                                             const float* __restrict__ scale,
+                                                             uint16_t* __restrict__ gx, int N, int H, int W, int C,
+                                                             int b) {
+  const int cpp = C >> 3;
+  const long long total = (long long)N * H * W * cpp;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const long long pix = t / cpp;
+    const int ww = (int)(pix % W);
+    const int hh = (int)((pix / W) % H);
+    const int n = (int)(pix / ((long long)W * H));
+    uint4 o = {0u, 0u, 0u, 0u};
+    if (hh >= b && hh < H - b && ww >= b && ww < W - b) {
+      const float s2 = 2.f * scale[n];
+      const uint4 v = *reinterpret_cast<const uint4*>(x + t * 8);
+      o.x = pack2<DT>(s2 * to_f<DT>(v.x & 0xFFFFu), s2 * to_f<DT>(v.x >> 16));
+      o.y = pack2<DT>(s2 * to_f<DT>(v.y & 0xFFFFu), s2 * to_f<DT>(v.y >> 16));
+      o.z = pack2<DT>(s2 * to_f<DT>(v.z & 0xFFFFu), s2 * to_f<DT>(v.z >> 16));
+      o.w = pack2<DT>(s2 * to_f<DT>(v.w & 0xFFFFu), s2 * to_f<DT>(v.w >> 16));
+    }
+    *reinterpret_cast<uint4*>(gx + t * 8) = o;
+  }
+}
+
+int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, int W, int C, int b, int dtype,
+                      hipStream_t s) {
+  if (C % 8 != 0 || H <= 2 * b || W <= 2 * b || parts < 1) return -1;
+  const dim3 grid((unsigned)parts, (unsigned)N);
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(sumsq_core_kernel<DT_F16>, grid, dim3(256), 0, s, x, part, H, W, C, b);
+  else
+    hipLaunchKernelGGL(sumsq_core_kernel<DT_BF16>, grid, dim3(256), 0, s, x, part, H, W, C, b);
+  return (int)hipGetLastError();
+}
+
+int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, uint16_t* gx, int N, int H, int W, int C, int b,
+                          int dtype, hipStream_t s) {
+  if (C % 8 != 0) return -1;
+  const long long total = (long long)N * H * W * (C / 8);
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 256LL * 32);
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(sumsq_core_bwd_kernel<DT_F16>, dim3(grid), dim3(256), 0, s, x, scale, gx, N, H, W, C, b);
+  else
+    hipLaunchKernelGGL(sumsq_core_bwd_kernel<DT_BF16>, dim3(grid), dim3(256), 0, s, x, scale, gx, N, H, W, C, b);
+  return (int)hipGetLastError();
+}
+
+}  // namespace dv

@@ -41,6 +41,8 @@ struct ConvArgs {
   int M;                  // GEMM rows = N*OH*OW
   int relu, relu_in, accumulate;
   int dtype;              // 16-bit storage dtype of x/w/mask/16-bit out: 0 bf16, 1 fp16
+  const uint16_t* res;    // optional residual (LDS-DMA FWD, 16-bit out): out = [ReLU](acc + bias + res)
+  long long res_ld;
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
@@ -74,6 +76,12 @@ namespace dv {
 // dir 0 forward (in = x [N,H,W,C], out = y [N,OH,OW,C]), 1 backward (in = gy, out = gx)
 int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C,
                 int OH, int OW, int k, int s, int pad, int dtype, hipStream_t st);
+// DeepDream loss: per-(image, block) partial sums of x^2 over the map minus a b-pixel border
+// (part [N][parts]), and its gradient gx = 2*scale[n]*x in the core, 0 on the border
+int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, int W, int C, int b, int dtype,
+                      hipStream_t s);
+int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, uint16_t* gx, int N, int H, int W, int C, int b,
+                          int dtype, hipStream_t s);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s);
 }  // namespace dv

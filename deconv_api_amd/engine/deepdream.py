@@ -26,6 +26,8 @@ from typing import Dict, List, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from ..ops.autograd import sumsq_core
+
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
 
 
@@ -76,8 +78,7 @@ class DeepDream:
         total = None
         for name, coeff in self.s.layers.items():
             a = acts[name]
-            core = a[:, b:a.shape[1] - b, b:a.shape[2] - b, :].float()
-            term = coeff * (core * core).sum(dim=(1, 2, 3)) / float(a[0].numel())
+            term = coeff * sumsq_core(a, b) / float(a[0].numel())
             total = term if total is None else total + term
         return total
 
@@ -165,11 +166,15 @@ RESNET_LAYERS = {"conv3_block4_out": 0.5, "conv4_block3_out": 1.0, "conv4_block6
 
 class TiledDeepDream(DeepDream):
     """Large-image DeepDream: every gradient step rolls the image by a random offset (shared seed,
-    identical on every rank), cuts it into ``tile`` x ``tile`` tiles, computes each tile's input
-    gradient independently (tiles are assigned round-robin to ranks — the image-domain analogue of
-    context parallelism), assembles the full gradient with one all-reduce (each tile
-    has exactly one owner, so the sum is the stitch), un-rolls it, normalizes it by the global
-    per-image mean |g| and applies the same update on every rank."""
+    identical on every rank), cuts it into equal ``<= tile``-sized tiles, computes each tile's input
+    gradient independently and stitches them. (tile, image) units are dealt round-robin to the
+    ranks (the image-domain analogue of context parallelism); a rank runs ALL of its
+    units as ONE batch (tiles are equal-sized: the last row/column of tiles is shifted inwards to
+    overlap its neighbour, and each pixel's gradient is taken from exactly one owning tile), so the
+    convs see large GEMMs instead of one small launch per tile. The roll, the tile cut and the
+    stitch/un-roll are single gathers/scatters with precomputed indices. The full gradient is
+    assembled with one all-reduce (each pixel has exactly one owner, so the sum is the stitch),
+    normalized by the global per-image mean |g| and applied identically on every rank."""
 
     def __init__(self, net, settings: Optional[DreamSettings] = None, tile: int = 512, info=None, seed: int = 0,
                  dtype=None):
@@ -177,48 +182,83 @@ class TiledDeepDream(DeepDream):
         self.tile = tile
         self.info = info
         self.gen = torch.Generator().manual_seed(seed)
+        self._plans: Dict[tuple, tuple] = {}
+
+    @staticmethod
+    def _axis_tiles(L: int, tile: int):
+        """[(start, own_lo, own_hi)] of equal-size (T) windows covering [0, L); returns (T, list)."""
+        n = -(-L // tile)
+        T = -(-L // n)
+        return T, [(min(i * T, L - T), i * T, min((i + 1) * T, L)) for i in range(n)]
 
     def _tiles(self, H: int, W: int):
-        t = self.tile
-        out = []
-        for y in range(0, H, t):
-            for x in range(0, W, t):
-                out.append((y, min(y + t, H), x, min(x + t, W)))
-        return out
+        Th, ys = self._axis_tiles(H, self.tile)
+        Tw, xs = self._axis_tiles(W, self.tile)
+        return Th, Tw, [(y, x) for y in ys for x in xs]
+
+    def _my_units(self, B: int, ntiles: int, world: int, rank: int):
+        """Work units are (tile, image) pairs dealt round-robin to the ranks, so ranks stay busy
+        even when an octave has fewer tiles than ranks."""
+        return [(u // B, u % B) for u in range(rank, ntiles * B, world)]
+
+    def _plan(self, B: int, H: int, W: int, device):
+        """Static gather/scatter indices for one octave shape: (Th, Tw, unit image ids [U],
+        tile origins [U, 2], owned (local flat, unit-relative global y, x) index tensors)."""
+        key = (B, H, W)
+        if key in self._plans:
+            return self._plans[key]
+        world = self.info.world if self.info is not None else 1
+        rank = self.info.rank if self.info is not None else 0
+        Th, Tw, tiles = self._tiles(H, W)
+        units = self._my_units(B, len(tiles), world, rank)
+        img = torch.tensor([b for _, b in units], dtype=torch.long)
+        org = torch.tensor([[tiles[t][0][0], tiles[t][1][0]] for t, _ in units], dtype=torch.long).view(-1, 2)
+        loc, gy, gx, gb = [], [], [], []
+        for u, (t, b) in enumerate(units):
+            (y0, oy0, oy1), (x0, ox0, ox1) = tiles[t]
+            yy, xx = torch.meshgrid(torch.arange(oy0, oy1), torch.arange(ox0, ox1), indexing="ij")
+            loc.append(((u * Th + (yy - y0)) * Tw + (xx - x0)).reshape(-1))
+            gy.append(yy.reshape(-1))
+            gx.append(xx.reshape(-1))
+            gb.append(torch.full((yy.numel(),), b, dtype=torch.long))
+        cat = lambda v: (torch.cat(v) if v else torch.zeros(0, dtype=torch.long)).to(device)  # noqa: E731
+        plan = (Th, Tw, img.to(device), org.to(device), cat(loc), cat(gb), cat(gy), cat(gx), len(tiles))
+        self._plans[key] = plan
+        return plan
 
     def gradient_ascent(self, x: torch.Tensor) -> torch.Tensor:
         import torch.distributed as dist
-
-        from ..parallel.dist import barrier  # noqa: F401  (imported for side-effect free use)
 
         B, H, W, _ = x.shape
         x = x.clone()
         done = torch.zeros(B, dtype=torch.bool, device=x.device)
         world = self.info.world if self.info is not None else 1
-        rank = self.info.rank if self.info is not None else 0
-        tiles = self._tiles(H, W)
+        Th, Tw, img, org, loc, gb, gyo, gxo, ntiles = self._plan(B, H, W, x.device)
+        ar_h = torch.arange(Th, device=x.device)
+        ar_w = torch.arange(Tw, device=x.device)
         for _ in range(self.s.iterations):
             sy = int(torch.randint(-self.tile // 2, self.tile // 2 + 1, (1,), generator=self.gen))
             sx = int(torch.randint(-self.tile // 2, self.tile // 2 + 1, (1,), generator=self.gen))
-            rolled = torch.roll(x, shifts=(sy, sx), dims=(1, 2))
             grad = torch.zeros_like(x)
             loss = torch.zeros(B, device=x.device)
-            for ti, (y0, y1, x0, x1) in enumerate(tiles):
-                if ti % world != rank:
-                    continue
-                xt = rolled[:, y0:y1, x0:x1].contiguous()
+            if img.numel():
+                # rolled[b, y, x] = x[b, (y - sy) % H, (x - sx) % W]; tiles of the rolled image, batched
+                iy = (org[:, 0:1] + ar_h - sy) % H  # [U, Th]
+                ix = (org[:, 1:2] + ar_w - sx) % W  # [U, Tw]
+                xt = x[img[:, None, None], iy[:, :, None], ix[:, None, :]]  # [U, Th, Tw, 3]
                 xin = self._net_input(xt).requires_grad_(True)
                 acts = self.net.forward(xin, list(self.s.layers.keys()))
                 lt = self.loss(acts)
                 (g,) = torch.autograd.grad(lt.sum(), xin)
-                grad[:, y0:y1, x0:x1] = g[..., :3].float()
-                loss += lt.detach()
+                # owned pixels of each unit -> un-rolled image positions
+                gsrc = g[..., :3].reshape(-1, 3)[loc].float()
+                grad.index_put_((gb, (gyo - sy) % H, (gxo - sx) % W), gsrc)
+                loss.index_add_(0, img, lt.detach().float())
             if world > 1:
                 dist.all_reduce(grad)
                 dist.all_reduce(loss)
-            grad = torch.roll(grad, shifts=(-sy, -sx), dims=(1, 2))
             grad = grad / grad.abs().mean(dim=(1, 2, 3), keepdim=True).clamp_min(1e-7)
             if self.s.max_loss is not None:
-                done |= loss > self.s.max_loss * len(tiles)
+                done |= loss > self.s.max_loss * ntiles
             x.add_(grad * ((~done).to(grad.dtype) * self.s.step).view(-1, 1, 1, 1))
         return x

@@ -14,7 +14,7 @@ from typing import Dict, Iterable, List
 
 import torch
 
-from ..ops.autograd import ConvUnit, max_pool
+from ..ops.autograd import ConvUnit, conv_res_relu, max_pool
 
 STAGES = [(2, 3, 64, 1), (3, 4, 128, 2), (4, 6, 256, 2), (5, 3, 512, 2)]  # (stage, blocks, width, stride)
 
@@ -72,9 +72,9 @@ class ResNet50:
         for i, (name, short, (c1, c2, c3)) in enumerate(self.blocks):
             if i > last:
                 break
-            y = self.units[c3](self.units[c2](self.units[c1](x)))
             sc = self.units[short](x) if short is not None else x
-            x = torch.relu(y + sc)
+            # conv3 + shortcut add + ReLU fused into one kernel epilogue on the GPU
+            x = conv_res_relu(self.units[c2](self.units[c1](x)), sc, self.units[c3])
             if name in want:
                 out[name] = x
         return out

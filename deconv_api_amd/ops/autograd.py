@@ -11,13 +11,17 @@ On CPU the same units are plain torch functional ops (autograd), which doubles a
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
 
 from . import native
-from .conv import ConvWeights, conv2d, pad_channels_oihw
+from .conv import ConvWeights, conv2d, pad_channels_oihw, transpose_subpixel
+
+# DV_SUBPIXEL=0 falls back to the direct transposed gather for strided dgrads (A/B testing)
+SUBPIXEL = os.environ.get("DV_SUBPIXEL", "1") != "0"
 
 
 class ConvUnit:
@@ -57,6 +61,12 @@ class ConvUnit:
                 self.bwd_pad = (kh - 1 - self.pad[0], kw - 1 - self.pad[1])
             else:
                 self.bwd = ConvWeights(w8, None, "transpose").to_device(self.device, dtype)
+                # sub-pixel classes: s^2 stride-1 convs instead of one s^2-times-wasteful gather
+                self.bwd_sub = []
+                for rh, rw, ws, pd in transpose_subpixel(w8, self.stride, self.pad):
+                    cw = None if ws is None else ConvWeights(pad_channels_oihw(ws), None, "fwd").to_device(
+                        self.device, dtype)
+                    self.bwd_sub.append((rh, rw, cw, pd))
         return self
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
@@ -86,10 +96,32 @@ class _ConvFn(torch.autograd.Function):
             gy = gy.contiguous()
         if unit.stride == 1:
             gx = conv2d(gy, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, mask=mask, use_bias=False)
+        elif SUBPIXEL:
+            gx = _subpixel_dgrad(gy, mask, unit, ctx.in_hw)
         else:
             gx = conv2d(gy, unit.bwd, stride=unit.stride, pad=unit.pad, relu=False, mask=mask, in_mode="transpose",
                         out_hw=ctx.in_hw, use_bias=False)
         return gx, None
+
+
+def _subpixel_dgrad(gy, mask, unit: ConvUnit, in_hw):
+    """dx of a strided conv as s^2 stride-1 convs (ops.conv.transpose_subpixel), each written to its
+    parity class of dx."""
+    s = unit.stride
+    H, W = in_hw
+    N = gy.shape[0]
+    C = unit.fwd.cin
+    gx = torch.empty(N, H, W, C, dtype=gy.dtype, device=gy.device)
+    for rh, rw, cw, pd in unit.bwd_sub:
+        hc, wc = len(range(rh, H, s)), len(range(rw, W, s))
+        if hc == 0 or wc == 0:
+            continue
+        if cw is None:
+            gx[:, rh::s, rw::s] = 0
+            continue
+        part = conv2d(gy, cw, stride=1, pad=pd, relu=False, mask=mask, out_hw=(hc, wc), use_bias=False)
+        gx[:, rh::s, rw::s] = part[..., :C]
+    return gx
 
 
 def _pool_out(L, k, s, p):
@@ -146,3 +178,63 @@ def avg_pool(x: torch.Tensor, k: int, s: int, p: int = 0) -> torch.Tensor:
     if x.is_cuda:
         return _AvgPoolFn.apply(x, k, s, p)
     return F.avg_pool2d(x.permute(0, 3, 1, 2), k, s, p, count_include_pad=False).permute(0, 2, 3, 1)
+
+
+class _ConvResReluFn(torch.autograd.Function):
+    """y = ReLU(conv(x) + bias + sc): the ResNet block tail in one kernel (residual add and ReLU in
+    the conv epilogue). Backward: gm = gy * (y > 0) is materialized once (it is also the shortcut's
+    gradient), then the conv's dgrad runs on it without a mask."""
+
+    @staticmethod
+    def forward(ctx, x, sc, unit: ConvUnit):
+        assert not unit.relu and unit.stride == 1, "conv_res_relu: the unit must be a linear stride-1 conv"
+        y = conv2d(x, unit.fwd, stride=1, pad=unit.pad, relu=True, res=sc.contiguous())
+        ctx.unit = unit
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        unit: ConvUnit = ctx.unit
+        gm = torch.ops.aten.threshold_backward(gy.contiguous(), y, 0)
+        gx = conv2d(gm, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, use_bias=False)
+        return gx, gm, None
+
+
+def conv_res_relu(x: torch.Tensor, sc: torch.Tensor, unit: ConvUnit) -> torch.Tensor:
+    """ReLU(unit(x) + sc) for a linear (no-ReLU) stride-1 conv unit."""
+    if x.is_cuda:
+        return _ConvResReluFn.apply(x, sc, unit)
+    return torch.relu(unit(x) + sc)
+
+
+class _SumSqCoreFn(torch.autograd.Function):
+    """Per-image sum of x^2 over x[:, b:H-b, b:W-b, :] (fp32), HIP forward and backward."""
+
+    @staticmethod
+    def forward(ctx, x, b: int):
+        x = x.contiguous()
+        N = x.shape[0]
+        core = (x.shape[1] - 2 * b) * (x.shape[2] - 2 * b) * x.shape[3]
+        parts = max(1, min(64, core // (256 * 8 * 8)))
+        part = torch.empty(N, parts, dtype=torch.float32, device=x.device)
+        native.lib().sumsq_core(x, part, b)
+        ctx.b = b
+        ctx.save_for_backward(x)
+        return part.sum(dim=1)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        gx = torch.empty_like(x)
+        native.lib().sumsq_core_bwd(x, g.float().contiguous(), gx, ctx.b)
+        return gx, None
+
+
+def sumsq_core(x: torch.Tensor, b: int) -> torch.Tensor:
+    """sum(x[:, b:-b, b:-b, :]^2) per image, fp32 [N] (the DeepDream activation loss term)."""
+    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.shape[3] % 8 == 0:
+        return _SumSqCoreFn.apply(x, b)
+    core = x[:, b:x.shape[1] - b, b:x.shape[2] - b, :].float()
+    return (core * core).sum(dim=(1, 2, 3))

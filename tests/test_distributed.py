@@ -203,3 +203,45 @@ def test_shard_sizes():
     assert shard_sizes(5, 2) == [3, 3]
     assert shard_counts(5, 2) == [3, 2]
     assert sum(shard_counts(7, 4)) == 7
+
+
+def _tiled_dream(world, rank, info=None):
+    from deconv_api_amd.engine.deepdream import RESNET_LAYERS, DreamSettings, TiledDeepDream
+    from deconv_api_amd.models.resnet50 import ResNet50
+
+    torch.manual_seed(0)
+    net = ResNet50(0).build("cpu")
+    s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=1, iterations=2, max_loss=None)
+    x = torch.rand(3, 192, 192, 3, generator=torch.Generator().manual_seed(1)) * 2 - 1
+    return TiledDeepDream(net, s, tile=96, info=info, seed=5).gradient_ascent(x)
+
+
+def _worker_tiled(rank, world, port, q):
+    try:
+        info = _init(rank, world, port)
+        out = _tiled_dream(world, rank, info)
+        q.put((rank, out.numpy(), None, None))
+        from deconv_api_amd.parallel import dist as pdist
+
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), None, None))
+
+
+def test_tiled_dream_units_across_ranks():
+    """12 (tile, image) units over 3 ranks (uneven: some tiles split their images across ranks)
+    give the single-process result, identically on every rank."""
+    from deconv_api_amd.engine.deepdream import TiledDeepDream
+
+    assert TiledDeepDream._my_units(None, 3, 4, 5, 1) == [(0, 1), (2, 0), (3, 2)]
+    assert TiledDeepDream._axis_tiles(731, 512) == (366, [(0, 0, 366), (365, 366, 731)])
+    ref = _tiled_dream(1, 0).numpy()
+    outs = _run(_worker_tiled, 3)
+    for r, out, _, _ in outs:
+        assert not isinstance(out, str), out
+        assert np.array_equal(out, outs[0][1])  # every rank applies the same update
+        # vs one process: the per-image tile batches differ (3 images vs 1), so fp32 CPU conv
+        # rounding differs at the 1e-9 level and can flip a ReLU/max-pool tie; the normalized
+        # step (0.01) bounds the effect
+        d = np.abs(out - ref)
+        assert d.mean() < 1e-4 and d.max() < 2e-2, (d.mean(), d.max())

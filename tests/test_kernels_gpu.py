@@ -118,8 +118,6 @@ def test_conv_unpool_gather(native_lib):
 
 
 def test_conv_mask_and_transpose(native_lib, conv_impl):
-    if conv_impl == "dma":
-        pytest.skip("the LDS-DMA kernel has no ReLU-mask prologue (auto routes masks to conv_igemm)")
     g = torch.Generator().manual_seed(6)
     dy = torch.randn(2, 8, 9, 64, generator=g)
     mask = torch.randn(2, 8, 9, 64, generator=g)
@@ -273,8 +271,6 @@ def test_conv_fp16_fwd_mask_transpose(native_lib, conv_impl, N, H, W, C, OC, str
         cb = ct
         kw = dict(stride=stride, pad=1, relu=False, in_mode="transpose", out_hw=(H, W), use_bias=False)
     for use_mask in (False, True):
-        if use_mask and conv_impl == "dma":
-            continue  # the LDS-DMA kernel has no mask prologue
         m = ref if use_mask else None
         kw["mask"] = m
         r = ops.conv2d(gy, cb, **kw)
@@ -297,3 +293,54 @@ def test_pool_fp16(native_lib):
         yd = fn(xd, 3, 2, 1)
         (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.float16).cuda())
         assert yd.dtype == torch.float16 and _rel(yd, yc) < 2e-3 and _rel(gd, gc) < 2e-3
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C,OC,N,H", [(64, 16, 3, 20), (64, 64, 2, 33), (128, 128, 2, 17), (256, 512, 1, 14),
+                                      (512, 256, 4, 7), (16, 8, 2, 40)])
+def test_conv_masked_dgrad_shapes(native_lib, conv_impl, dt, C, OC, N, H):
+    """ReLU-masked A operand over every tile config of both kernels, with +0/-0/negative mask values
+    and rows spanning images."""
+    g = torch.Generator().manual_seed(C + OC + H)
+    r = lambda t: t.to(dt).float()  # noqa: E731
+    x = r(torch.randn(N, H, H + 3, C, generator=g))
+    m = torch.randn(N, H, H + 3, C, generator=g).clamp_min(0)
+    m[m == 0] = torch.where(torch.rand(int((m == 0).sum()), generator=g) < 0.5, 0.0, -0.0)
+    m = r(m) - r(torch.rand(N, H, H + 3, C, generator=g) < 0.05).float() * 3.0  # a few negatives
+    cw = ConvWeights(r(torch.randn(OC, C, 3, 3, generator=g) / np.sqrt(9 * C)), None, "fwd")
+    ref = ops.conv2d(x, cw, relu=False, mask=r(m), use_bias=False)
+    got = ops.conv2d(x.to(dt).to(DEV), cw.to_device(DEV, dt), relu=False, mask=m.to(dt).to(DEV), use_bias=False)
+    assert got.dtype == dt and _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C,OC,N,H", [(64, 256, 2, 19), (256, 64, 3, 8), (128, 512, 1, 12), (512, 2048, 2, 7)])
+def test_conv_residual_relu_epilogue(native_lib, dt, C, OC, N, H):
+    """Fused ResNet block tail: ReLU(conv1x1(x) + bias + res) in the LDS-DMA epilogue."""
+    g = torch.Generator().manual_seed(C * 7 + OC)
+    r = lambda t: t.to(dt).float()  # noqa: E731
+    x = r(torch.randn(N, H, H, C, generator=g))
+    res = r(torch.randn(N, H, H, OC, generator=g))
+    cw = ConvWeights(r(torch.randn(OC, C, 1, 1, generator=g) / np.sqrt(C)), r(torch.randn(OC, generator=g)), "fwd")
+    ref = ops.conv2d(x, cw, relu=True, res=res)
+    assert torch.allclose(ref, (ops.conv2d(x, cw, relu=False) + res).clamp_min(0), atol=1e-5)
+    got = ops.conv2d(x.to(dt).to(DEV), cw.to_device(DEV, dt), relu=True, res=res.to(dt).to(DEV))
+    assert got.dtype == dt and _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_sumsq_core_fwd_bwd(native_lib, dt):
+    from deconv_api_amd.ops.autograd import sumsq_core
+
+    g = torch.Generator().manual_seed(9)
+    for shape, b in [((3, 17, 23, 64), 2), ((2, 70, 70, 512), 2), ((1, 6, 6, 8), 1)]:
+        x = torch.randn(*shape, generator=g).to(dt).float()
+        xc = x.clone().requires_grad_(True)
+        lc = sumsq_core(xc, b)
+        gl = torch.rand(shape[0], generator=g)
+        (gc,) = torch.autograd.grad(lc, xc, gl)
+        xd = x.to(dt).to(DEV).requires_grad_(True)
+        ld = sumsq_core(xd, b)
+        (gd,) = torch.autograd.grad(ld, xd, gl.to(DEV))
+        assert ld.dtype == torch.float32 and torch.allclose(ld.cpu(), lc, rtol=1e-5)
+        assert gd.dtype == dt and _rel(gd, gc) < 1e-2
