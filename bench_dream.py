@@ -54,7 +54,7 @@ def main(argv=None):
         net = ResNet50(0).build(dev, dt)
         s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=a.octaves, iterations=a.steps)
     if a.tile:
-        dd = TiledDeepDream(net, s, tile=a.tile, info=info)
+        dd = TiledDeepDream(net, s, tile=a.tile, info=info, use_graphs=not a.no_graphs)
     else:
         dd = DeepDream(net, s, use_graphs=not a.no_graphs)
     g = torch.Generator(device=dev).manual_seed(7 + info.rank * (0 if a.tile else 1))
@@ -81,7 +81,7 @@ def main(argv=None):
             "value": round(imgs / per_run, 3), "unit": "images/s", "n_gpus": info.world,
             "s_per_dream_batch": round(per_run, 3), "runs": a.runs, "warmup": a.warmup,
             "higher_is_better": True, "scaling": "strong" if a.tile else "weak", "dtype": a.dtype,
-            "data": "synthetic uint8 images, seeded random-init weights", "hip_graphs": not a.no_graphs and not a.tile,
+            "data": "synthetic uint8 images, seeded random-init weights", "hip_graphs": not a.no_graphs,
             "finite": bool(torch.isfinite(out).all()),
             "config": {"model": a.model, "batch": a.batch, "image_size": a.size, "tile": a.tile,
                        "parallelism": f"{'tiles' if a.tile else 'dp'}{info.world}"},

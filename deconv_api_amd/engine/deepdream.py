@@ -177,12 +177,15 @@ class TiledDeepDream(DeepDream):
     normalized by the global per-image mean |g| and applied identically on every rank."""
 
     def __init__(self, net, settings: Optional[DreamSettings] = None, tile: int = 512, info=None, seed: int = 0,
-                 dtype=None):
+                 dtype=None, use_graphs: bool = True):
         super().__init__(net, settings, use_graphs=False, dtype=dtype)
         self.tile = tile
         self.info = info
         self.gen = torch.Generator().manual_seed(seed)
         self._plans: Dict[tuple, tuple] = {}
+        # one hipGraph per octave shape for the whole tile forward/backward/stitch
+        self.tile_graphs = use_graphs and self.device.type == "cuda"
+        self._tgraphs: Dict[tuple, tuple] = {}
 
     @staticmethod
     def _axis_tiles(L: int, tile: int):
@@ -226,39 +229,81 @@ class TiledDeepDream(DeepDream):
         self._plans[key] = plan
         return plan
 
+    def _tile_grad(self, x: torch.Tensor, shift: torch.Tensor, plan, grad: torch.Tensor, loss: torch.Tensor):
+        """grad, loss <- this rank's stitched tile gradients / summed tile losses for the image
+        rolled by ``shift`` (a device [2] tensor, so a captured graph replays any shift)."""
+        B, H, W, _ = x.shape
+        Th, Tw, img, org, loc, gb, gyo, gxo, _ = plan
+        grad.zero_()
+        loss.zero_()
+        if not img.numel():
+            return
+        sy, sx = shift[0], shift[1]
+        # rolled[b, y, x] = x[b, (y - sy) % H, (x - sx) % W]; tiles of the rolled image, batched
+        iy = (org[:, 0:1] + torch.arange(Th, device=x.device) - sy) % H  # [U, Th]
+        ix = (org[:, 1:2] + torch.arange(Tw, device=x.device) - sx) % W  # [U, Tw]
+        xt = x[img[:, None, None], iy[:, :, None], ix[:, None, :]]  # [U, Th, Tw, 3]
+        xin = self._net_input(xt).requires_grad_(True)
+        acts = self.net.forward(xin, list(self.s.layers.keys()))
+        lt = self.loss(acts)
+        (g,) = torch.autograd.grad(lt.sum(), xin)
+        # owned pixels of each unit -> un-rolled image positions
+        gsrc = g[..., :3].reshape(-1, 3)[loc].float()
+        grad.index_put_((gb, (gyo - sy) % H, (gxo - sx) % W), gsrc)
+        loss.index_add_(0, img, lt.detach().float())
+
+    def _tile_graph(self, x: torch.Tensor, plan):
+        """hipGraph of _tile_grad for one octave shape (static buffers: image, shift, grad, loss)."""
+        key = tuple(x.shape)
+        if key in self._tgraphs:
+            return self._tgraphs[key]
+        bx = x.clone()
+        shift = torch.zeros(2, dtype=torch.long, device=x.device)
+        grad = torch.zeros_like(x)
+        loss = torch.zeros(x.shape[0], device=x.device)
+        st = torch.cuda.Stream(x.device)
+        st.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.cuda.stream(st):
+            for _ in range(2):
+                self._tile_grad(bx, shift, plan, grad, loss)
+        torch.cuda.current_stream(x.device).wait_stream(st)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._tile_grad(bx, shift, plan, grad, loss)
+        self._tgraphs[key] = (g, bx, shift, grad, loss)
+        return self._tgraphs[key]
+
     def gradient_ascent(self, x: torch.Tensor) -> torch.Tensor:
         import torch.distributed as dist
 
         B, H, W, _ = x.shape
-        x = x.clone()
         done = torch.zeros(B, dtype=torch.bool, device=x.device)
         world = self.info.world if self.info is not None else 1
-        Th, Tw, img, org, loc, gb, gyo, gxo, ntiles = self._plan(B, H, W, x.device)
-        ar_h = torch.arange(Th, device=x.device)
-        ar_w = torch.arange(Tw, device=x.device)
-        for _ in range(self.s.iterations):
-            sy = int(torch.randint(-self.tile // 2, self.tile // 2 + 1, (1,), generator=self.gen))
-            sx = int(torch.randint(-self.tile // 2, self.tile // 2 + 1, (1,), generator=self.gen))
+        plan = self._plan(B, H, W, x.device)
+        ntiles = plan[-1]
+        shifts = torch.randint(-self.tile // 2, self.tile // 2 + 1, (self.s.iterations, 2), generator=self.gen)
+        if self.tile_graphs:
+            graph, bx, shift, grad, loss = self._tile_graph(x, plan)
+            bx.copy_(x)
+            x = bx
+            dshifts = shifts.to(x.device)
+        else:
+            x = x.clone()
+            shift = torch.zeros(2, dtype=torch.long, device=x.device)
             grad = torch.zeros_like(x)
             loss = torch.zeros(B, device=x.device)
-            if img.numel():
-                # rolled[b, y, x] = x[b, (y - sy) % H, (x - sx) % W]; tiles of the rolled image, batched
-                iy = (org[:, 0:1] + ar_h - sy) % H  # [U, Th]
-                ix = (org[:, 1:2] + ar_w - sx) % W  # [U, Tw]
-                xt = x[img[:, None, None], iy[:, :, None], ix[:, None, :]]  # [U, Th, Tw, 3]
-                xin = self._net_input(xt).requires_grad_(True)
-                acts = self.net.forward(xin, list(self.s.layers.keys()))
-                lt = self.loss(acts)
-                (g,) = torch.autograd.grad(lt.sum(), xin)
-                # owned pixels of each unit -> un-rolled image positions
-                gsrc = g[..., :3].reshape(-1, 3)[loc].float()
-                grad.index_put_((gb, (gyo - sy) % H, (gxo - sx) % W), gsrc)
-                loss.index_add_(0, img, lt.detach().float())
+        for it in range(self.s.iterations):
+            if self.tile_graphs:
+                shift.copy_(dshifts[it])
+                graph.replay()
+            else:
+                shift.copy_(shifts[it])
+                self._tile_grad(x, shift, plan, grad, loss)
             if world > 1:
                 dist.all_reduce(grad)
                 dist.all_reduce(loss)
-            grad = grad / grad.abs().mean(dim=(1, 2, 3), keepdim=True).clamp_min(1e-7)
+            g = grad / grad.abs().mean(dim=(1, 2, 3), keepdim=True).clamp_min(1e-7)
             if self.s.max_loss is not None:
                 done |= loss > self.s.max_loss * ntiles
-            x.add_(grad * ((~done).to(grad.dtype) * self.s.step).view(-1, 1, 1, 1))
-        return x
+            x.add_(g * ((~done).to(g.dtype) * self.s.step).view(-1, 1, 1, 1))
+        return x.clone() if self.tile_graphs else x

@@ -188,3 +188,15 @@ def test_tiled_gather_scatter_is_exact(H, W, tile, B):
     for _ in range(3):
         want += s.step * want / want.abs().mean(dim=(1, 2, 3), keepdim=True)
     assert torch.allclose(got, want, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_tiled_graph_equals_eager(native_lib):
+    """The hipGraph-captured tiled step (device-side roll shift) == the eager tiled step."""
+    net = ResNet50(0).build("cuda", torch.float16)
+    s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=2, iterations=3)
+    x = (torch.rand(2, 200, 260, 3, generator=torch.Generator().manual_seed(5)) * 2 - 1).cuda()
+    eager = TiledDeepDream(net, s, tile=128, seed=3, use_graphs=False).run(x)
+    graph = TiledDeepDream(net, s, tile=128, seed=3, use_graphs=True).run(x)
+    assert torch.isfinite(graph).all() and (graph - x).abs().max() > 1e-3
+    assert (eager - graph).abs().max() < 1e-3
