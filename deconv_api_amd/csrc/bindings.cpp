@@ -37,7 +37,7 @@ void check_rc(int rc, const char* what) {
 //       code_div, x_ld, mask_ld, out_ld
 void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
           c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
-          int64_t epi, int64_t impl, c10::optional<Tensor> res) {
+          int64_t epi, int64_t impl, c10::optional<Tensor> res, c10::optional<Tensor> emask) {
   TORCH_CHECK(g.size() == 23, "conv: geometry vector must have 23 entries");
   check_cuda(x, "x");
   check_cuda(w, "w");
@@ -114,14 +114,25 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   if (res.has_value()) {  // fused residual: LDS-DMA forward conv with a 16-bit output only
     check_cuda(*res, "res");
     TORCH_CHECK(res->scalar_type() == dt && res->dim() == 4 && res->stride(3) == 1, "res: x's dtype, NHWC");
-    TORCH_CHECK(amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16 && !mask.has_value() && !a.accumulate &&
-                    impl != 1 && impl != 3,
+    TORCH_CHECK(amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16 && !a.accumulate && impl != 1 && impl != 3 &&
+                    (!mask.has_value() || a.mask_ld == a.x_ld),
                 "res: forward conv with a 16-bit epilogue on the LDS-DMA kernel only");
     a.res_ld = res->stride(2);
     TORCH_CHECK(res->stride(1) == a.OW * a.res_ld && res->stride(0) == (int64_t)a.OH * a.OW * a.res_ld,
                 "res: pixels must be dense");
     need(*res, ((int64_t)(a.M - 1) * a.res_ld + a.OC) * 2, "res");
     a.res = reinterpret_cast<const uint16_t*>(res->data_ptr());
+    if (emask.has_value()) {
+      check_cuda(*emask, "emask");
+      TORCH_CHECK(emask->scalar_type() == dt && emask->dim() == 4 && emask->stride(3) == 1, "emask: x's dtype, NHWC");
+      a.emask_ld = emask->stride(2);
+      TORCH_CHECK(emask->stride(1) == a.OW * a.emask_ld && emask->stride(0) == (int64_t)a.OH * a.OW * a.emask_ld,
+                  "emask: pixels must be dense");
+      need(*emask, ((int64_t)(a.M - 1) * a.emask_ld + a.OC) * 2, "emask");
+      a.emask = reinterpret_cast<const uint16_t*>(emask->data_ptr());
+    }
+  } else {
+    TORCH_CHECK(!emask.has_value(), "emask requires res");
   }
   // Kernel choice. impl: 0 auto, 1 register-staged (conv_igemm), 2 LDS-DMA (conv_dma), 3 halo-tile.
   //  * halo-tile (3x3 s1 p1, OC tile <= 64, >= 56x56 maps): input staged once per tile, unpool fused
@@ -224,6 +235,22 @@ void sumsq_core_bwd(Tensor x, Tensor scale, Tensor gx, int64_t b) {
                                      reinterpret_cast<uint16_t*>(gx.data_ptr()), (int)x.size(0), (int)x.size(1),
                                      (int)x.size(2), (int)x.size(3), (int)b, dt_of(x), cur_stream()),
            "sumsq_core_bwd");
+}
+
+// geom: KH, KW, stride, pad_h, pad_w, Cr; cols [N, OH, OW, J_ld] (J = KH*KW*Cr), gx [N, H, W, 8]
+void col2im(Tensor cols, Tensor gx, std::vector<int64_t> g) {
+  check_cuda(cols, "cols");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(cols.device());
+  TORCH_CHECK(g.size() == 6, "col2im: geometry");
+  TORCH_CHECK(cols.dim() == 4 && cols.is_contiguous() && gx.dim() == 4 && gx.is_contiguous() && gx.size(3) == 8 &&
+                  gx.scalar_type() == cols.scalar_type() && gx.size(0) == cols.size(0),
+              "col2im: cols [N,OH,OW,J_ld], gx [N,H,W,8] contiguous, same dtype");
+  dv::Col2ImGeom G{(int)gx.size(0), (int)gx.size(1), (int)gx.size(2), (int)cols.size(1), (int)cols.size(2),
+                   (int)g[0], (int)g[1], (int)g[2], (int)g[3], (int)g[4], (int)g[5], (int)cols.size(3)};
+  TORCH_CHECK(G.Cr >= 1 && G.Cr <= 8 && (int64_t)G.KH * G.KW * G.Cr <= G.J_ld && G.stride >= 1, "col2im: K/Cr/J_ld");
+  check_rc(dv::col2im_launch(reinterpret_cast<const uint16_t*>(cols.data_ptr()),
+                             reinterpret_cast<uint16_t*>(gx.data_ptr()), G, dt_of(cols), cur_stream()),
+           "col2im");
 }
 
 void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
@@ -341,10 +368,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv", &conv, "MFMA implicit-GEMM conv (fwd / unpool-gather / transposed; bf16/pool/f32 epilogues)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("out_code"), py::arg("code"),
         py::arg("mask"), py::arg("geom"), py::arg("amode"), py::arg("epi"), py::arg("impl"),
-        py::arg("res") = py::none());
+        py::arg("res") = py::none(), py::arg("emask") = py::none());
   m.def("pool", &pool, "k x k max/avg pooling forward/backward");
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
+  m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);
   m.def("seed_deconv3x3", &seed_deconv3x3);

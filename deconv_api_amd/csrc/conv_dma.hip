@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   }
 
   // ---- epilogue ----
-  if constexpr (EPI == CONV_E_BF16 && AMODE == CONV_A_FWD && !MASK) {
+  if constexpr (EPI == CONV_E_BF16 && AMODE == CONV_A_FWD) {
     if (a.res) {
       epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
       return;
@@ -312,9 +312,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
     epilogue<DT, FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
 }
 
-// residual epilogue (ResNet block tail): out = [ReLU](acc + bias + res). Each column group's
-// residual values are all loaded before its first store, so the loads overlap each other instead
-// of each waiting behind the previous store.
+// residual epilogue (ResNet block tail): out = [ReLU](acc + bias + res), then optionally zeroed
+// where emask <= 0 (backward: the input gradient of a block whose input is a ReLU output, with the
+// shortcut gradient as `res`). Each column group's residual/emask values are all loaded before its
+// first store, so the loads overlap each other instead of each waiting behind the previous store.
 template <int DT, int FM, int FN>
 __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw,
                                              int lane) {
@@ -326,13 +327,14 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
     const int col = nw + j * 16 + col_l;
     if (col >= a.OC) continue;
     const float bias = a.bias ? a.bias[col] : 0.f;
-    uint16_t rv[FM][4];
+    uint16_t rv[FM][4], ev[FM][4];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = min(mw + i * 16 + row_l + r, a.M - 1);
         rv[i][r] = a.res[(long long)row * a.res_ld + col];
+        ev[i][r] = a.emask ? a.emask[(long long)row * a.emask_ld + col] : (uint16_t)0x3C00u;  // any > 0
       }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -342,6 +344,8 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
         if (row >= a.M) continue;
         float v = acc[i][j][r] + bias + to_f<DT>(rv[i][r]);
         if (a.relu) v = fmaxf(v, 0.f);
+        const uint32_t e = ev[i][r];
+        if (e == 0u || (e & 0x8000u)) v = 0.f;
         out[(long long)row * a.out_ld + col] = from_f<DT>(v);
       }
   }

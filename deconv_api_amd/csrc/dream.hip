@@ -84,3 +84,53 @@ int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, uint16_t* gx, i
 }
 
 }  // namespace dv
+
+namespace dv {
+
+// col2im for the input gradient of a strided conv with very few input channels (the RGB stem):
+// cols[n][oh][ow][(kh*KW + kw)*Cr + c] = sum_oc dy[n][oh][ow][oc] * w[oc][c][kh][kw] comes from a
+// plain GEMM (1x1 conv) that reads dy once; here each dx pixel gathers its <= ceil(KH/s)*ceil(KW/s)
+// contributions. One thread per dx pixel, fp32 sums, Cpad (8) channels written with one 16-B store.
+template <int DT>
+__global__ void __launch_bounds__(256) col2im_kernel(const uint16_t* __restrict__ cols, uint16_t* __restrict__ gx,
+                                                     Col2ImGeom g) {
+  const long long total = (long long)g.N * g.H * g.W;
+  for (long long p = blockIdx.x * 256LL + threadIdx.x; p < total; p += (long long)gridDim.x * 256) {
+    const int iw = (int)(p % g.W);
+    const int ih = (int)((p / g.W) % g.H);
+    const long long n = p / ((long long)g.W * g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int kh0 = (ih + g.pad_h) % g.stride, kw0 = (iw + g.pad_w) % g.stride;
+    for (int kh = kh0; kh < g.KH; kh += g.stride) {
+      const int oh = (ih + g.pad_h - kh) / g.stride;
+      if (oh < 0 || oh >= g.OH) continue;
+      for (int kw = kw0; kw < g.KW; kw += g.stride) {
+        const int ow = (iw + g.pad_w - kw) / g.stride;
+        if (ow < 0 || ow >= g.OW) continue;
+        const uint16_t* src = cols + ((n * g.OH + oh) * g.OW + ow) * g.J_ld + (kh * g.KW + kw) * g.Cr;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (c < g.Cr) acc[c] += to_f<DT>(src[c]);
+      }
+    }
+    uint4 o;
+    o.x = pack2<DT>(acc[0], acc[1]);
+    o.y = pack2<DT>(acc[2], acc[3]);
+    o.z = pack2<DT>(acc[4], acc[5]);
+    o.w = pack2<DT>(acc[6], acc[7]);
+    *reinterpret_cast<uint4*>(gx + p * 8) = o;
+  }
+}
+
+int col2im_launch(const uint16_t* cols, uint16_t* gx, const Col2ImGeom& g, int dtype, hipStream_t s) {
+  if (g.Cr < 1 || g.Cr > 8 || g.stride < 1) return -1;
+  const long long total = (long long)g.N * g.H * g.W;
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 256LL * 64);
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(col2im_kernel<DT_F16>, dim3(grid), dim3(256), 0, s, cols, gx, g);
+  else
+    hipLaunchKernelGGL(col2im_kernel<DT_BF16>, dim3(grid), dim3(256), 0, s, cols, gx, g);
+  return (int)hipGetLastError();
+}
+
+}  // namespace dv

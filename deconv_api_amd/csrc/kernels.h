@@ -43,6 +43,8 @@ struct ConvArgs {
   int dtype;              // 16-bit storage dtype of x/w/mask/16-bit out: 0 bf16, 1 fp16
   const uint16_t* res;    // optional residual (LDS-DMA FWD, 16-bit out): out = [ReLU](acc + bias + res)
   long long res_ld;
+  const uint16_t* emask;  // optional with res: out = 0 where emask <= 0 (same layout as out)
+  long long emask_ld;
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
@@ -82,6 +84,11 @@ int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, i
                       hipStream_t s);
 int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, uint16_t* gx, int N, int H, int W, int C, int b,
                           int dtype, hipStream_t s);
+// col2im of a strided conv's input gradient for <= 8 input channels (output padded to 8 channels)
+struct Col2ImGeom {
+  int N, H, W, OH, OW, KH, KW, stride, pad_h, pad_w, Cr, J_ld;
+};
+int col2im_launch(const uint16_t* cols, uint16_t* gx, const Col2ImGeom& g, int dtype, hipStream_t s);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s);
 }  // namespace dv

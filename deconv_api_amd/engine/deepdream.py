@@ -68,6 +68,10 @@ class DeepDream:
         self.dtype = dtype
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self._graphs: Dict[tuple, tuple] = {}
+        if hasattr(net, "grad_premasked"):
+            # the loss gradient 2*act/numel vanishes where a (ReLU) activation does, so block outputs
+            # only ever receive ReLU-masked gradients: lets the ResNet backward skip its ReLU passes
+            net.grad_premasked = True
 
     # ------------------------------------------------------------------ one step
     def _net_input(self, x: torch.Tensor) -> torch.Tensor:

@@ -14,7 +14,7 @@ from typing import Dict, Iterable, List
 
 import torch
 
-from ..ops.autograd import ConvUnit, conv_res_relu, max_pool
+from ..ops.autograd import ConvUnit, bottleneck, max_pool
 
 STAGES = [(2, 3, 64, 1), (3, 4, 128, 2), (4, 6, 256, 2), (5, 3, 512, 2)]  # (stage, blocks, width, stride)
 
@@ -24,6 +24,9 @@ class ResNet50:
         self.g = torch.Generator().manual_seed(seed)
         self.units: Dict[str, ConvUnit] = {}
         self.device = torch.device("cpu")
+        # gradient contract for the GPU backward (ops.autograd._BottleneckFn): True only when every
+        # gradient reaching a block output vanishes where the output does (set by DeepDream)
+        self.grad_premasked = False
         self._conv("conv1_conv", 3, 64, 7, 2, 3, relu=True)
         self.blocks: List[tuple] = []
         cin = 64
@@ -72,9 +75,11 @@ class ResNet50:
         for i, (name, short, (c1, c2, c3)) in enumerate(self.blocks):
             if i > last:
                 break
-            sc = self.units[short](x) if short is not None else x
-            # conv3 + shortcut add + ReLU fused into one kernel epilogue on the GPU
-            x = conv_res_relu(self.units[c2](self.units[c1](x)), sc, self.units[c3])
+            u = self.units
+            # GPU: one autograd node per block (residual add + ReLU in the conv3 epilogue, no
+            # elementwise kernels in the backward; see ops.autograd._BottleneckFn)
+            x = bottleneck(x, u[c1], u[c2], u[c3], u[short] if short is not None else None,
+                           premasked=self.grad_premasked)
             if name in want:
                 out[name] = x
         return out

@@ -22,6 +22,8 @@ from .conv import ConvWeights, conv2d, pad_channels_oihw, transpose_subpixel
 
 # DV_SUBPIXEL=0 falls back to the direct transposed gather for strided dgrads (A/B testing)
 SUBPIXEL = os.environ.get("DV_SUBPIXEL", "1") != "0"
+# DV_COL2IM=0 disables the GEMM + col2im input gradient of few-channel strided convs (A/B testing)
+COL2IM = os.environ.get("DV_COL2IM", "1") != "0"
 
 
 class ConvUnit:
@@ -61,6 +63,13 @@ class ConvUnit:
                 self.bwd_pad = (kh - 1 - self.pad[0], kw - 1 - self.pad[1])
             else:
                 self.bwd = ConvWeights(w8, None, "transpose").to_device(self.device, dtype)
+                # few input channels (RGB stem): dx = col2im(dy @ W) -- a GEMM that reads dy once
+                cr = self.w.shape[1]
+                self.col_w = None
+                if cr <= 8 and kh * kw * cr <= 256:
+                    wc = self.w.permute(2, 3, 1, 0).reshape(kh * kw * cr, self.cout, 1, 1)  # [(kh,kw,c), oc]
+                    self.col_w = ConvWeights(wc.contiguous(), None, "fwd").to_device(self.device, dtype)
+                    self.col_ld = -(-kh * kw * cr // 8) * 8
                 # sub-pixel classes: s^2 stride-1 convs instead of one s^2-times-wasteful gather
                 self.bwd_sub = []
                 for rh, rw, ws, pd in transpose_subpixel(w8, self.stride, self.pad):
@@ -96,12 +105,29 @@ class _ConvFn(torch.autograd.Function):
             gy = gy.contiguous()
         if unit.stride == 1:
             gx = conv2d(gy, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, mask=mask, use_bias=False)
+        elif unit.col_w is not None and COL2IM:
+            gx = _col2im_dgrad(gy, mask, unit, ctx.in_hw)
         elif SUBPIXEL:
             gx = _subpixel_dgrad(gy, mask, unit, ctx.in_hw)
         else:
             gx = conv2d(gy, unit.bwd, stride=unit.stride, pad=unit.pad, relu=False, mask=mask, in_mode="transpose",
                         out_hw=ctx.in_hw, use_bias=False)
         return gx, None
+
+
+def _col2im_dgrad(gy, mask, unit: ConvUnit, in_hw):
+    """dx of a strided conv with <= 8 input channels: cols = (dy*mask) @ W^T as a 1x1 conv on the
+    LDS-DMA kernel, then the col2im gather kernel."""
+    N, OH, OW, _ = gy.shape
+    H, W = in_hw
+    kh, kw = unit.w.shape[2:]
+    J = unit.col_w.cout
+    cols = torch.empty(N, OH, OW, unit.col_ld, dtype=gy.dtype, device=gy.device)
+    conv2d(gy, unit.col_w, stride=1, pad=0, relu=False, mask=mask, use_bias=False, out=cols[..., :J])
+    assert unit.fwd.cin == 8, "col2im path writes 8-channel input gradients"
+    gx = torch.empty(N, H, W, 8, dtype=gy.dtype, device=gy.device)
+    native.lib().col2im(cols, gx, [kh, kw, unit.stride, unit.pad[0], unit.pad[1], unit.w.shape[1]])
+    return gx
 
 
 def _subpixel_dgrad(gy, mask, unit: ConvUnit, in_hw):
@@ -111,13 +137,11 @@ def _subpixel_dgrad(gy, mask, unit: ConvUnit, in_hw):
     H, W = in_hw
     N = gy.shape[0]
     C = unit.fwd.cin
-    gx = torch.empty(N, H, W, C, dtype=gy.dtype, device=gy.device)
+    empty_class = any(cw is None for _, _, cw, _ in unit.bwd_sub)
+    gx = (torch.zeros if empty_class else torch.empty)(N, H, W, C, dtype=gy.dtype, device=gy.device)
     for rh, rw, cw, pd in unit.bwd_sub:
         hc, wc = len(range(rh, H, s)), len(range(rw, W, s))
-        if hc == 0 or wc == 0:
-            continue
-        if cw is None:
-            gx[:, rh::s, rw::s] = 0
+        if hc == 0 or wc == 0 or cw is None:
             continue
         part = conv2d(gy, cw, stride=1, pad=pd, relu=False, mask=mask, out_hw=(hc, wc), use_bias=False)
         gx[:, rh::s, rw::s] = part[..., :C]
@@ -238,3 +262,77 @@ def sumsq_core(x: torch.Tensor, b: int) -> torch.Tensor:
         return _SumSqCoreFn.apply(x, b)
     core = x[:, b:x.shape[1] - b, b:x.shape[2] - b, :].float()
     return (core * core).sum(dim=(1, 2, 3))
+
+
+class _BottleneckFn(torch.autograd.Function):
+    """ResNet bottleneck block y = ReLU(c3(ReLU(c2(ReLU(c1(x))))) + shortcut(x)) with a hand-written
+    backward that needs no elementwise kernels:
+
+      gm = gy (if ``premasked``) else gy * (y > 0)
+      g2 = dgrad_c3(gm);  g1 = dgrad_c2(g2, A-mask y2)
+      gs = gm (identity) | dgrad_short(gm)
+      gx = dgrad_c1(g1, A-mask y1) + gs    <- residual epilogue of the c1 dgrad,
+           zeroed where x <= 0 if ``premasked`` (x is the previous block's ReLU output)
+
+    ``premasked`` is the contract that every gradient reaching a block output is already zero
+    where that output is zero. It holds for DeepDream (the loss gradient 2*act/numel vanishes
+    where act = 0, and each block masks the gradient it hands to the previous block), and removes
+    the ReLU-backward pass of every block.
+    """
+
+    @staticmethod
+    def forward(ctx, x, units, premasked: bool):
+        c1, c2, c3, sh = units
+        y1 = conv2d(x, c1.fwd, stride=c1.stride, pad=c1.pad, relu=True)
+        y2 = conv2d(y1, c2.fwd, stride=c2.stride, pad=c2.pad, relu=True)
+        sc = x if sh is None else conv2d(x, sh.fwd, stride=sh.stride, pad=sh.pad, relu=False)
+        y = conv2d(y2, c3.fwd, stride=1, pad=c3.pad, relu=True, res=sc)
+        ctx.units = units
+        ctx.premasked = premasked
+        ctx.save_for_backward(x, y1, y2, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y1, y2, y = ctx.saved_tensors
+        c1, c2, c3, sh = ctx.units
+        in_hw = (x.shape[1], x.shape[2])
+        gy = gy.contiguous()
+        gm = gy if ctx.premasked else torch.ops.aten.threshold_backward(gy, y, 0)
+        g2 = conv2d(gm, c3.bwd, stride=1, pad=c3.bwd_pad, relu=False, use_bias=False)
+        g1 = _unit_dgrad(c2, g2, y2, (y1.shape[1], y1.shape[2]))
+        if sh is None:
+            gs = gm
+        else:
+            gs = _unit_dgrad(sh, gm, None, in_hw)
+        emask = x if ctx.premasked else None
+        if c1.stride == 1:
+            gx = conv2d(g1, c1.bwd, stride=1, pad=c1.bwd_pad, relu=False, mask=y1, use_bias=False, res=gs,
+                        emask=emask)
+        else:
+            gx = _unit_dgrad(c1, g1, y1, in_hw) + gs
+            if emask is not None:
+                gx = torch.ops.aten.threshold_backward(gx, emask, 0)
+        return gx, None, None
+
+
+def _unit_dgrad(unit: ConvUnit, gy, mask, in_hw):
+    """Input gradient of one conv unit (mask = its ReLU output, or None)."""
+    gy = gy.contiguous()
+    if unit.stride == 1:
+        return conv2d(gy, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, mask=mask, use_bias=False)
+    if unit.col_w is not None and COL2IM:
+        return _col2im_dgrad(gy, mask, unit, in_hw)
+    if SUBPIXEL:
+        return _subpixel_dgrad(gy, mask, unit, in_hw)
+    return conv2d(gy, unit.bwd, stride=unit.stride, pad=unit.pad, relu=False, mask=mask, in_mode="transpose",
+                  out_hw=in_hw, use_bias=False)
+
+
+def bottleneck(x: torch.Tensor, c1: ConvUnit, c2: ConvUnit, c3: ConvUnit, short: Optional[ConvUnit],
+               premasked: bool = False) -> torch.Tensor:
+    """ReLU(c3(c2(c1(x))) + short(x)) (c1, c2 with ReLU; c3, short linear)."""
+    if x.is_cuda:
+        return _BottleneckFn.apply(x, (c1, c2, c3, short), premasked)
+    sc = short(x) if short is not None else x
+    return torch.relu(c3(c2(c1(x))) + sc)

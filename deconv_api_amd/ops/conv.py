@@ -214,13 +214,14 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
            relu_in: bool = False, in_mode: str = "plain", code: Optional[torch.Tensor] = None,
            code_div: int = 1, mask: Optional[torch.Tensor] = None, epilogue: str = "bf16",
            out: Optional[torch.Tensor] = None, accumulate: bool = False, out_hw=None,
-           use_bias: bool = True, res: Optional[torch.Tensor] = None):
+           use_bias: bool = True, res: Optional[torch.Tensor] = None, emask: Optional[torch.Tensor] = None):
     """NHWC convolution.
 
     x: [N, H, W, C] (channel-slice views allowed: stride(3) == 1). For ``in_mode='unpool'`` x is
     the pooled map [N, H/2, W/2, C] and ``code`` its switch codes ([N/code_div, H/2, W/2, C]).
     epilogue 'pool' returns ``(pooled, code)``; otherwise the output tensor.
-    ``res``: fused residual (ResNet block tail), out = [ReLU](conv + bias + res), ReLU after the add.
+    ``res``: fused residual (ResNet block tail), out = [ReLU](conv + bias + res), ReLU after the add;
+    ``emask`` (with ``res``): the result is zeroed where emask <= 0.
     """
     if pad is None:
         pad = (cw.KH // 2, cw.KW // 2)
@@ -245,13 +246,13 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     OC = cw.cout
     if x.is_cuda:
         return _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
-                           mask, epilogue, out, accumulate, use_bias, res)
+                           mask, epilogue, out, accumulate, use_bias, res, emask)
     return _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
-                       mask, epilogue, out, accumulate, use_bias, res)
+                       mask, epilogue, out, accumulate, use_bias, res, emask)
 
 
 def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
-                epilogue, out, accumulate, use_bias, res=None):
+                epilogue, out, accumulate, use_bias, res=None, emask=None):
     dtype = x.dtype
     xf = x.float()
     if in_mode == "unpool":
@@ -278,6 +279,8 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
         y = y + res.float()
     if relu:
         y = y.clamp_min(0)
+    if emask is not None:
+        y = y * (emask.float() > 0)
     if epilogue == "pool":
         y = y.to(dtype).float()  # pool on stored-precision values, like the fused GPU epilogue
         pv, pc = maxpool_switch_ref(y)
@@ -296,7 +299,7 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
 
 
 def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
-                epilogue, out, accumulate, use_bias, res=None):
+                epilogue, out, accumulate, use_bias, res=None, emask=None):
     lib = native.lib()
     dt = x.dtype
     assert dt in (torch.bfloat16, torch.float16) and x.stride(3) == 1, \
@@ -329,7 +332,7 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
             int(relu), int(relu_in), int(accumulate), int(code_div), x_ld, mask_ld, out_ld]
     bias = cw.bias_pad if use_bias else None
     lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
-             IMPL[_policy["impl"]] if res is None else IMPL["dma"], res)  # residual: DMA kernel only
+             IMPL[_policy["impl"]] if res is None else IMPL["dma"], res, emask)  # residual: DMA kernel only
     if epilogue == "pool":
         return out, out_code
     return out

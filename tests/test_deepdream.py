@@ -200,3 +200,67 @@ def test_gpu_tiled_graph_equals_eager(native_lib):
     graph = TiledDeepDream(net, s, tile=128, seed=3, use_graphs=True).run(x)
     assert torch.isfinite(graph).all() and (graph - x).abs().max() > 1e-3
     assert (eager - graph).abs().max() < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,s,p,cin", [(7, 2, 3, 3), (3, 2, 0, 3), (3, 2, 1, 32)])
+def test_gpu_strided_conv_unit_input_grad(native_lib, k, s, p, cin):
+    """Strided conv units' input gradient (GEMM+col2im for few channels, sub-pixel classes
+    otherwise, both with the ReLU mask) vs CPU autograd."""
+    from deconv_api_amd.ops import autograd as AG
+
+    g = torch.Generator().manual_seed(k + cin)
+    w = torch.randn(64, cin, k, k, generator=g) / (k * k * cin) ** 0.5
+    b = torch.randn(64, generator=g) * 0.1
+    w = w.to(torch.float16).float()
+    x = torch.randn(2, 37, 41, cin, generator=g).to(torch.float16).float()
+    for relu in (False, True):
+        cpu = AG.ConvUnit("u", w, b, s, (p, p), relu=relu).build("cpu")
+        gpu = AG.ConvUnit("u", w, b, s, (p, p), relu=relu).build("cuda", torch.float16)
+        assert (gpu.col_w is not None) == (cin <= 8)
+        xc = x.clone().requires_grad_(True)
+        yc = cpu(xc)
+        gy = torch.randn(*yc.shape, generator=g).to(torch.float16).float()
+        (gc,) = torch.autograd.grad(yc, xc, gy)
+        x8 = torch.nn.functional.pad(x, (0, (-cin) % 8)).to(torch.float16).cuda().requires_grad_(True)
+        yd = gpu(x8)
+        (gd,) = torch.autograd.grad(yd, x8, gy.to(torch.float16).cuda())
+        gd = gd[..., :cin].float().cpu()
+        if not relu:  # exact up to fp16 rounding of the GEMM output
+            assert (gd - gc).abs().max() < 5e-3 * gc.abs().max()
+        else:  # fp16 forward rounding can flip a few ReLU-mask entries near 0
+            a, b2 = gd.flatten().double(), gc.flatten().double()
+            assert float(a @ b2 / (a.norm() * b2.norm())) > 0.999
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride,proj,premasked", [(1, False, False), (1, True, True), (2, True, False),
+                                                   (2, True, True), (1, False, True)])
+def test_gpu_bottleneck_block_grad(native_lib, stride, proj, premasked):
+    """Fused bottleneck autograd node vs CPU autograd of the unfused block (bf16)."""
+    from deconv_api_amd.ops import autograd as AG
+
+    g = torch.Generator().manual_seed(stride * 10 + proj)
+    cin, w = (64, 16) if proj else (64, 16)
+    mk = lambda n, ci, co, k, s, p, relu: AG.ConvUnit(  # noqa: E731
+        n, torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5, torch.randn(co, generator=g) * 0.1, s, (p, p),
+        relu=relu)
+    units = [mk("c1", cin, w, 1, stride, 0, True), mk("c2", w, w, 3, 1, 1, True), mk("c3", w, 64, 1, 1, 0, False),
+             mk("sh", cin, 64, 1, stride, 0, False) if (proj or stride > 1) else None]
+    x = torch.randn(2, 14, 18, cin, generator=g).clamp_min(0).to(torch.bfloat16).float()
+    cpu = [u.__class__(u.name, u.w, u.b, u.stride, u.pad, u.relu).build("cpu") if u else None for u in units]
+    gpu = [u.build("cuda") if u else None for u in units]
+    xc = x.clone().requires_grad_(True)
+    yc = AG.bottleneck(xc, *cpu)
+    gy = torch.randn(*yc.shape, generator=g)
+    if premasked:
+        gy = gy * (yc.detach() > 0)
+    (gc,) = torch.autograd.grad(yc, xc, gy)
+    if premasked:
+        gc = gc * (x > 0)  # the contract: the block hands back a gradient masked by its ReLU input
+    xd = x.to(torch.bfloat16).cuda().requires_grad_(True)
+    yd = AG.bottleneck(xd, *gpu, premasked=premasked)
+    assert (yd.float().cpu() - yc.detach()).abs().max() < 3e-2 * yc.abs().max()
+    (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.bfloat16).cuda())
+    a, b = gd.float().cpu().flatten().double(), gc.flatten().double()
+    assert float(a @ b / (a.norm() * b.norm())) > 0.99
