@@ -7,6 +7,8 @@
 
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace {
 
 using at::Tensor;
@@ -131,8 +133,21 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       need(*emask, ((int64_t)(a.M - 1) * a.emask_ld + a.OC) * 2, "emask");
       a.emask = reinterpret_cast<const uint16_t*>(emask->data_ptr());
     }
-  } else {
-    TORCH_CHECK(!emask.has_value(), "emask requires res");
+  }
+  if (emask.has_value() && a.emask == nullptr) {  // output mask without a residual
+    check_cuda(*emask, "emask");
+    TORCH_CHECK(emask->scalar_type() == dt && emask->dim() == 4 && emask->stride(3) == 1, "emask: x's dtype, NHWC");
+    TORCH_CHECK(epi == dv::CONV_E_BF16 && impl != 1 && impl != 3, "emask: 16-bit epilogue on the LDS-DMA kernel only");
+    a.emask_ld = emask->stride(2);
+    TORCH_CHECK(emask->stride(1) == a.OW * a.emask_ld && emask->stride(0) == (int64_t)a.OH * a.OW * a.emask_ld,
+                "emask: pixels must be dense");
+    need(*emask, ((int64_t)(a.M - 1) * a.emask_ld + a.OC) * 2, "emask");
+    a.emask = reinterpret_cast<const uint16_t*>(emask->data_ptr());
+  }
+  {  // LDS-staged vector epilogue: 16-bit rows (out / res / emask) 16-B aligned
+    auto al = [](const void* p, int64_t ld) { return reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 8 == 0; };
+    a.vec_epi = epi == dv::CONV_E_BF16 && al(a.out, a.out_ld) && (!a.res || al(a.res, a.res_ld)) &&
+                (!a.emask || al(a.emask, a.emask_ld)) && std::getenv("DV_NO_VEC_EPI") == nullptr;
   }
   // Kernel choice. impl: 0 auto, 1 register-staged (conv_igemm), 2 LDS-DMA (conv_dma), 3 halo-tile.
   //  * halo-tile (3x3 s1 p1, OC tile <= 64, >= 56x56 maps): input staged once per tile, unpool fused
@@ -141,9 +156,10 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   const bool halo_ok = (amode == dv::CONV_A_FWD || amode == dv::CONV_A_UNPOOL) && a.KH == 3 && a.KW == 3 &&
                        a.stride == 1 && a.pad_h == 1 && a.pad_w == 1 && a.C == 64 && a.H == a.OH &&
                        a.W == a.OW && !a.accumulate && !mask.has_value() && a.dtype == dv::DT_BF16 &&
-                       (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad == 64);
+                       (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad == 64) &&
+                       a.res == nullptr && a.emask == nullptr;
   // persistent weight-resident halo kernel: 64-channel inputs at large maps (block1 of VGG16)
-  const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112 && a.res == nullptr;
+  const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112 && a.res == nullptr && a.emask == nullptr;
   if (impl == 3 || (impl == 0 && halo_auto)) {
     TORCH_CHECK(halo_ok, "conv: halo-tile kernel does not support this shape/mode");
     check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream()), "conv_halo");
@@ -156,6 +172,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                           (amode == dv::CONV_A_TRANSPOSE && epi == dv::CONV_E_BF16)) && !mask.has_value()) ||
                         mask_dma;
   TORCH_CHECK(impl != 2 || dma_mode, "conv: LDS-DMA kernel does not support this mode");
+  TORCH_CHECK(dma_mode || (a.res == nullptr && a.emask == nullptr), "conv: res / emask need the LDS-DMA kernel");
   if (dma_mode && impl != 1) {
     Tensor unpooled;
     if (amode == dv::CONV_A_UNPOOL) {  // materialize the unpooled map, then a plain DMA conv

@@ -60,6 +60,9 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
 template <int DT, int FM, int FN>
 __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw,
                                              int lane);
+template <int DT, int NT, int BM, int BN, int FM, int FN>
+__device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
+                                             int n0, int wm, int wn, int lane, int tid);
 
 // DT: 16-bit storage/MFMA dtype of x, w and a 16-bit output (DT_BF16 / DT_F16, common.h)
 // MASK: backward through a ReLU: A elements are kept only where mask (same layout and pixel
@@ -300,8 +303,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   }
 
   // ---- epilogue ----
-  if constexpr (EPI == CONV_E_BF16 && AMODE == CONV_A_FWD) {
-    if (a.res) {
+  if constexpr (EPI == CONV_E_BF16) {
+    if (a.vec_epi) {
+      static_assert(BM * BN * 2 <= STAGES * STAGE, "C tile must fit in the operand stages");
+      __syncthreads();  // every wave is done reading the operand stages
+      epilogue_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+      return;
+    }
+    if (a.res || a.emask) {
       epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
       return;
     }
@@ -333,7 +342,7 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = min(mw + i * 16 + row_l + r, a.M - 1);
-        rv[i][r] = a.res[(long long)row * a.res_ld + col];
+        rv[i][r] = a.res ? a.res[(long long)row * a.res_ld + col] : (uint16_t)0u;
         ev[i][r] = a.emask ? a.emask[(long long)row * a.emask_ld + col] : (uint16_t)0x3C00u;  // any > 0
       }
 #pragma unroll
@@ -400,6 +409,90 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
         }
       }
     }
+  }
+}
+
+// LDS-staged 16-bit epilogue. The MFMA C layout gives each lane 4 rows x 1 column per 16x16
+// block, i.e. 2-byte scattered stores; instead the tile is written to LDS (the freed operand
+// stages, 16-B chunks XOR-swizzled by row) and read back as 8-channel chunks: every global
+// store, residual load, emask load and accumulate load is one 16-B access. Semantics as
+// epilogue/epilogue_res: v = acc + bias, [ReLU] (before a += out), + res, [ReLU] (after a res
+// add), zeroed where emask <= 0. Stores of a row's last partial chunk (OC % 8) go per element.
+template <int DT, int NT, int BM, int BN, int FM, int FN>
+__device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
+                                             int n0, int wm, int wn, int lane, int tid) {
+  constexpr int CPR = BN / 8;                       // 16-B chunks per C-tile row
+  constexpr int SWZ = (CPR < 8 ? CPR : 8) - 1;
+  const int row_l = (lane >> 4) * 4, col_l = lane & 15;
+  const bool pre_relu = a.relu && a.res == nullptr;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = wn * FN * 16 + j * 16 + col_l;
+    const int gcol = n0 + col;
+    const float bias = (a.bias && gcol < a.OCpad) ? a.bias[gcol] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * FM * 16 + i * 16 + row_l + r;
+        float v = acc[i][j][r] + bias;
+        if (pre_relu) v = fmaxf(v, 0.f);
+        *reinterpret_cast<uint16_t*>(smem + row * (BN * 2) + ((((col >> 3) ^ (row & SWZ))) << 4) + (col & 7) * 2) =
+            from_f<DT>(v);
+      }
+  }
+  __syncthreads();
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+  const bool post = a.accumulate || a.res != nullptr;
+  for (int c = tid; c < BM * CPR; c += NT) {
+    const int row = c / CPR, cc = c % CPR;
+    const int grow = m0 + row, gcol = n0 + cc * 8;
+    if (grow >= a.M || gcol >= a.OC) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((cc ^ (row & SWZ)) << 4));
+    const long long o = (long long)grow * a.out_ld + gcol;
+    if (gcol + 8 > a.OC) {  // a row's last partial chunk: element-wise (no 16-B access past OC)
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      for (int e = 0; e < a.OC - gcol; ++e) {
+        float f = to_f<DT>((vv[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+        if (a.accumulate) f += to_f<DT>(out[o + e]);
+        if (a.res) {
+          f += to_f<DT>(a.res[(long long)grow * a.res_ld + gcol + e]);
+          if (a.relu) f = fmaxf(f, 0.f);
+        }
+        if (a.emask) {
+          const uint32_t m = a.emask[(long long)grow * a.emask_ld + gcol + e];
+          if (m == 0u || (m & 0x8000u)) f = 0.f;
+        }
+        out[o + e] = from_f<DT>(f);
+      }
+      continue;
+    }
+    if (post) {
+      uint4 ad = {0u, 0u, 0u, 0u}, rs = {0u, 0u, 0u, 0u};
+      if (a.accumulate) ad = *reinterpret_cast<const uint4*>(out + o);
+      if (a.res) rs = *reinterpret_cast<const uint4*>(a.res + (long long)grow * a.res_ld + gcol);
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w}, aa[4] = {ad.x, ad.y, ad.z, ad.w}, rr[4] = {rs.x, rs.y, rs.z, rs.w};
+      uint32_t ov[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = to_f<DT>(vv[e] & 0xFFFFu) + to_f<DT>(aa[e] & 0xFFFFu) + to_f<DT>(rr[e] & 0xFFFFu);
+        float hi = to_f<DT>(vv[e] >> 16) + to_f<DT>(aa[e] >> 16) + to_f<DT>(rr[e] >> 16);
+        if (a.relu && a.res) {
+          lo = fmaxf(lo, 0.f);
+          hi = fmaxf(hi, 0.f);
+        }
+        ov[e] = pack2<DT>(lo, hi);
+      }
+      v = uint4{ov[0], ov[1], ov[2], ov[3]};
+    }
+    if (a.emask) {
+      const uint4 em = *reinterpret_cast<const uint4*>(a.emask + (long long)grow * a.emask_ld + gcol);
+      v.x = mask_pos_pk(v.x, em.x);
+      v.y = mask_pos_pk(v.y, em.y);
+      v.z = mask_pos_pk(v.z, em.z);
+      v.w = mask_pos_pk(v.w, em.w);
+    }
+    *reinterpret_cast<uint4*>(out + o) = v;
   }
 }
 

@@ -43,8 +43,9 @@ struct ConvArgs {
   int dtype;              // 16-bit storage dtype of x/w/mask/16-bit out: 0 bf16, 1 fp16
   const uint16_t* res;    // optional residual (LDS-DMA FWD, 16-bit out): out = [ReLU](acc + bias + res)
   long long res_ld;
-  const uint16_t* emask;  // optional with res: out = 0 where emask <= 0 (same layout as out)
+  const uint16_t* emask;  // optional (16-bit out): out = 0 where emask <= 0 (same layout as out)
   long long emask_ld;
+  int vec_epi;            // host-checked: 16-bit out/res/emask rows 16-B aligned -> LDS-staged epilogue
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);

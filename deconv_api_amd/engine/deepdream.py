@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from ..ops.autograd import sumsq_core
+from ..ops.autograd import premasked_grads, sumsq_core
 
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
 
@@ -68,10 +68,6 @@ class DeepDream:
         self.dtype = dtype
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self._graphs: Dict[tuple, tuple] = {}
-        if hasattr(net, "grad_premasked"):
-            # the loss gradient 2*act/numel vanishes where a (ReLU) activation does, so block outputs
-            # only ever receive ReLU-masked gradients: lets the ResNet backward skip its ReLU passes
-            net.grad_premasked = True
 
     # ------------------------------------------------------------------ one step
     def _net_input(self, x: torch.Tensor) -> torch.Tensor:
@@ -89,7 +85,8 @@ class DeepDream:
     def loss_and_grad(self, x: torch.Tensor):
         """x: fp32 [B, H, W, 3] (preprocessed). Returns (loss [B], normalized grad [B, H, W, 3])."""
         xin = self._net_input(x).requires_grad_(True)
-        acts = self.net.forward(xin, list(self.s.layers.keys()))
+        with premasked_grads():  # the loss gradient 2*act/numel vanishes where act does
+            acts = self.net.forward(xin, list(self.s.layers.keys()))
         loss = self.loss(acts)
         (g,) = torch.autograd.grad(loss.sum(), xin)
         g = g[..., :3].float()
@@ -248,7 +245,8 @@ class TiledDeepDream(DeepDream):
         ix = (org[:, 1:2] + torch.arange(Tw, device=x.device) - sx) % W  # [U, Tw]
         xt = x[img[:, None, None], iy[:, :, None], ix[:, None, :]]  # [U, Th, Tw, 3]
         xin = self._net_input(xt).requires_grad_(True)
-        acts = self.net.forward(xin, list(self.s.layers.keys()))
+        with premasked_grads():  # the loss gradient 2*act/numel vanishes where act does
+            acts = self.net.forward(xin, list(self.s.layers.keys()))
         lt = self.loss(acts)
         (g,) = torch.autograd.grad(lt.sum(), xin)
         # owned pixels of each unit -> un-rolled image positions

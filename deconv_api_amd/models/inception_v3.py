@@ -14,7 +14,7 @@ from typing import Dict, Iterable, List, Optional
 
 import torch
 
-from ..ops.autograd import ConvUnit, avg_pool, max_pool
+from ..ops.autograd import ConvUnit, avg_pool, cat_channels, max_pool
 
 MIXED = [f"mixed{i}" for i in range(11)]
 
@@ -100,7 +100,7 @@ class InceptionV3:
             elif op == "max":
                 x = max_pool(x, 3, 2, 0)
             elif isinstance(op, tuple):  # ("split", a, b): concat of two convs of the same input
-                x = torch.cat([self.units[op[1]](x), self.units[op[2]](x)], dim=3)
+                x = cat_channels([self.units[op[1]](x), self.units[op[2]](x)])
             else:
                 x = self.units[op](x)
         return x
@@ -115,7 +115,7 @@ class InceptionV3:
         for bi, (name, order, br) in enumerate(self.blocks):
             if bi > last:
                 break
-            x = torch.cat([self._branch(x, br[k]) for k in order], dim=3)
+            x = cat_channels([self._branch(x, br[k]) for k in order])
             if name in want:
                 out[name] = x
         return out

@@ -24,9 +24,6 @@ class ResNet50:
         self.g = torch.Generator().manual_seed(seed)
         self.units: Dict[str, ConvUnit] = {}
         self.device = torch.device("cpu")
-        # gradient contract for the GPU backward (ops.autograd._BottleneckFn): True only when every
-        # gradient reaching a block output vanishes where the output does (set by DeepDream)
-        self.grad_premasked = False
         self._conv("conv1_conv", 3, 64, 7, 2, 3, relu=True)
         self.blocks: List[tuple] = []
         cin = 64
@@ -78,8 +75,7 @@ class ResNet50:
             u = self.units
             # GPU: one autograd node per block (residual add + ReLU in the conv3 epilogue, no
             # elementwise kernels in the backward; see ops.autograd._BottleneckFn)
-            x = bottleneck(x, u[c1], u[c2], u[c3], u[short] if short is not None else None,
-                           premasked=self.grad_premasked)
+            x = bottleneck(x, u[c1], u[c2], u[c3], u[short] if short is not None else None)
             if name in want:
                 out[name] = x
         return out

@@ -11,6 +11,7 @@ On CPU the same units are plain torch functional ops (autograd), which doubles a
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Optional, Tuple
 
@@ -24,6 +25,47 @@ from .conv import ConvWeights, conv2d, pad_channels_oihw, transpose_subpixel
 SUBPIXEL = os.environ.get("DV_SUBPIXEL", "1") != "0"
 # DV_COL2IM=0 disables the GEMM + col2im input gradient of few-channel strided convs (A/B testing)
 COL2IM = os.environ.get("DV_COL2IM", "1") != "0"
+
+
+_PREMASKED = [False]
+
+
+@contextlib.contextmanager
+def premasked_grads():
+    """Forward passes run inside this context record the *premasked-gradient contract*: every
+    gradient that will reach a ReLU output is already zero where that output is zero. It holds
+    when all consumers of ReLU outputs are the ops of this module (each masks the gradient it
+    returns by its input's positivity, in its dgrad epilogue) and the loss gradient vanishes where
+    the activation does (DeepDream's sum of squares). ReLU units then skip their own mask pass: the
+    ReLU-masked A-operand (2x slower LDS-bound dgrad) becomes an `emask` on the producer's epilogue.
+    """
+    old = _PREMASKED[0]
+    _PREMASKED[0] = True
+    try:
+        yield
+    finally:
+        _PREMASKED[0] = old
+
+
+def _is_relu_out(t: torch.Tensor) -> bool:
+    """Tag set on tensors that are ReLU outputs (or max/avg pools / concats of them): >= 0, and
+    zero where every upstream ReLU output is zero."""
+    return bool(getattr(t, "_dv_relu", False))
+
+
+def _tag(t: torch.Tensor, relu: bool) -> torch.Tensor:
+    t._dv_relu = relu
+    return t
+
+
+def tag_relu_output(t: torch.Tensor, relu: bool = True) -> torch.Tensor:
+    """Mark a tensor built from ReLU outputs outside this module (e.g. torch.cat of branches)."""
+    return _tag(t, relu)
+
+
+def cat_channels(parts) -> torch.Tensor:
+    """torch.cat along channels (NHWC); the result is a ReLU output iff every part is."""
+    return _tag(torch.cat(parts, dim=3), all(_is_relu_out(p) for p in parts))
 
 
 class ConvUnit:
@@ -80,7 +122,7 @@ class ConvUnit:
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:
-            return _ConvFn.apply(x, self)
+            return _tag(_ConvFn.apply(x, self), self.relu)
         y = F.conv2d(x.permute(0, 3, 1, 2), self.w_dev[:, : x.shape[3]] if x.shape[3] < self.w_dev.shape[1]
                      else self.w_dev, self.b_dev, stride=self.stride, padding=self.pad).permute(0, 2, 3, 1)
         return y.relu() if self.relu else y
@@ -92,27 +134,44 @@ class _ConvFn(torch.autograd.Function):
         y = conv2d(x, unit.fwd, stride=unit.stride, pad=unit.pad, relu=unit.relu)
         ctx.unit = unit
         ctx.in_hw = (x.shape[1], x.shape[2])
-        if unit.relu:
-            ctx.save_for_backward(y)
+        ctx.premasked = _PREMASKED[0]
+        # premasked: the incoming gradient needs no ReLU mask, and the returned one is masked by
+        # x > 0 (x a ReLU output) in the dgrad epilogue
+        ctx.emask = ctx.premasked and _is_relu_out(x)
+        saved = [y if (unit.relu and not ctx.premasked) else None, x if ctx.emask else None]
+        ctx.save_for_backward(*saved)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         unit: ConvUnit = ctx.unit
-        mask = ctx.saved_tensors[0] if unit.relu else None
+        mask, x = ctx.saved_tensors
         gy = gy.contiguous() if gy.stride(-1) != 1 else gy
         if mask is not None and gy.stride() != mask.stride():
             gy = gy.contiguous()
-        if unit.stride == 1:
-            gx = conv2d(gy, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, mask=mask, use_bias=False)
-        elif unit.col_w is not None and COL2IM:
-            gx = _col2im_dgrad(gy, mask, unit, ctx.in_hw)
-        elif SUBPIXEL:
-            gx = _subpixel_dgrad(gy, mask, unit, ctx.in_hw)
-        else:
-            gx = conv2d(gy, unit.bwd, stride=unit.stride, pad=unit.pad, relu=False, mask=mask, in_mode="transpose",
-                        out_hw=ctx.in_hw, use_bias=False)
+        emask = x if (x is not None and x.is_contiguous()) else None
+        gx = _dgrad(unit, gy, mask, ctx.in_hw, emask)
+        if x is not None and emask is None:
+            gx = torch.ops.aten.threshold_backward(gx, x, 0)
         return gx, None
+
+
+def _dgrad(unit: ConvUnit, gy, mask, in_hw, emask=None):
+    """Input gradient of one conv unit: A-operand ReLU mask ``mask`` (its output, or None) and
+    output mask ``emask`` (its input, when a ReLU output; applied in the epilogue when possible)."""
+    if unit.stride == 1:
+        return conv2d(gy, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, mask=mask, use_bias=False, emask=emask)
+    gx = _dgrad_strided(unit, gy, mask, in_hw)
+    return gx if emask is None else torch.ops.aten.threshold_backward(gx, emask, 0)
+
+
+def _dgrad_strided(unit: ConvUnit, gy, mask, in_hw):
+    if unit.col_w is not None and COL2IM:
+        return _col2im_dgrad(gy, mask, unit, in_hw)
+    if SUBPIXEL:
+        return _subpixel_dgrad(gy, mask, unit, in_hw)
+    return conv2d(gy, unit.bwd, stride=unit.stride, pad=unit.pad, relu=False, mask=mask, in_mode="transpose",
+                      out_hw=in_hw, use_bias=False)
 
 
 def _col2im_dgrad(gy, mask, unit: ConvUnit, in_hw):
@@ -161,6 +220,8 @@ class _MaxPoolFn(torch.autograd.Function):
         y = torch.empty(N, OH, OW, C, dtype=x.dtype, device=x.device)
         idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=x.device)
         native.lib().pool(x, y, idx, 0, 0, [N, H, W, C, OH, OW, k, s, p])
+        # premasked: a max over ReLU outputs is 0 exactly when the chosen input is, so routing the
+        # (already masked) output gradient to the argmax keeps the input gradient masked
         ctx.save_for_backward(idx)
         ctx.geom = [N, H, W, C, OH, OW, k, s, p]
         return y
@@ -182,25 +243,30 @@ class _AvgPoolFn(torch.autograd.Function):
         y = torch.empty(N, OH, OW, C, dtype=x.dtype, device=x.device)
         native.lib().pool(x.contiguous(), y, None, 1, 0, [N, H, W, C, OH, OW, k, s, p])
         ctx.geom = [N, H, W, C, OH, OW, k, s, p]
+        # premasked: an average spreads its gradient over zero inputs too -> mask by x > 0
+        ctx.save_for_backward(x if (_PREMASKED[0] and _is_relu_out(x)) else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         g = ctx.geom
+        (x,) = ctx.saved_tensors
         gx = torch.empty(g[0], g[1], g[2], g[3], dtype=gy.dtype, device=gy.device)
         native.lib().pool(gy.contiguous(), gx, None, 1, 1, g)
+        if x is not None:
+            gx = torch.ops.aten.threshold_backward(gx, x, 0)
         return gx, None, None, None
 
 
 def max_pool(x: torch.Tensor, k: int, s: int, p: int = 0) -> torch.Tensor:
     if x.is_cuda:
-        return _MaxPoolFn.apply(x, k, s, p)
+        return _tag(_MaxPoolFn.apply(x, k, s, p), _is_relu_out(x))
     return F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1)
 
 
 def avg_pool(x: torch.Tensor, k: int, s: int, p: int = 0) -> torch.Tensor:
     if x.is_cuda:
-        return _AvgPoolFn.apply(x, k, s, p)
+        return _tag(_AvgPoolFn.apply(x, k, s, p), _is_relu_out(x))
     return F.avg_pool2d(x.permute(0, 3, 1, 2), k, s, p, count_include_pad=False).permute(0, 2, 3, 1)
 
 
@@ -266,29 +332,28 @@ def sumsq_core(x: torch.Tensor, b: int) -> torch.Tensor:
 
 class _BottleneckFn(torch.autograd.Function):
     """ResNet bottleneck block y = ReLU(c3(ReLU(c2(ReLU(c1(x))))) + shortcut(x)) with a hand-written
-    backward that needs no elementwise kernels:
+    backward that needs no elementwise kernels. Under the premasked contract (premasked_grads):
 
-      gm = gy (if ``premasked``) else gy * (y > 0)
-      g2 = dgrad_c3(gm);  g1 = dgrad_c2(g2, A-mask y2)
-      gs = gm (identity) | dgrad_short(gm)
-      gx = dgrad_c1(g1, A-mask y1) + gs    <- residual epilogue of the c1 dgrad,
-           zeroed where x <= 0 if ``premasked`` (x is the previous block's ReLU output)
+      g2 = dgrad_c3(gy)            epilogue-masked by y2 > 0
+      g1 = dgrad_c2(g2)            epilogue-masked by y1 > 0
+      gs = gy (identity) | dgrad_short(gy)
+      gx = dgrad_c1(g1) + gs       residual epilogue, masked by x > 0 when x is a ReLU output
 
-    ``premasked`` is the contract that every gradient reaching a block output is already zero
-    where that output is zero. It holds for DeepDream (the loss gradient 2*act/numel vanishes
-    where act = 0, and each block masks the gradient it hands to the previous block), and removes
-    the ReLU-backward pass of every block.
+    so no dgrad reads a ReLU mask in its A operand (the LDS-bound path) and the block hands the
+    previous block an already-masked gradient. Without the contract the masks are applied the
+    usual way (gy * (y > 0) materialized, A-operand masks for c2 / c1).
     """
 
     @staticmethod
-    def forward(ctx, x, units, premasked: bool):
+    def forward(ctx, x, units):
         c1, c2, c3, sh = units
         y1 = conv2d(x, c1.fwd, stride=c1.stride, pad=c1.pad, relu=True)
         y2 = conv2d(y1, c2.fwd, stride=c2.stride, pad=c2.pad, relu=True)
         sc = x if sh is None else conv2d(x, sh.fwd, stride=sh.stride, pad=sh.pad, relu=False)
         y = conv2d(y2, c3.fwd, stride=1, pad=c3.pad, relu=True, res=sc)
         ctx.units = units
-        ctx.premasked = premasked
+        ctx.premasked = _PREMASKED[0]
+        ctx.x_relu = _is_relu_out(x) and x.is_contiguous()
         ctx.save_for_backward(x, y1, y2, y)
         return y
 
@@ -298,41 +363,26 @@ class _BottleneckFn(torch.autograd.Function):
         c1, c2, c3, sh = ctx.units
         in_hw = (x.shape[1], x.shape[2])
         gy = gy.contiguous()
-        gm = gy if ctx.premasked else torch.ops.aten.threshold_backward(gy, y, 0)
-        g2 = conv2d(gm, c3.bwd, stride=1, pad=c3.bwd_pad, relu=False, use_bias=False)
-        g1 = _unit_dgrad(c2, g2, y2, (y1.shape[1], y1.shape[2]))
-        if sh is None:
-            gs = gm
-        else:
-            gs = _unit_dgrad(sh, gm, None, in_hw)
-        emask = x if ctx.premasked else None
+        pm = ctx.premasked
+        gm = gy if pm else torch.ops.aten.threshold_backward(gy, y, 0)
+        g2 = conv2d(gm, c3.bwd, stride=1, pad=c3.bwd_pad, relu=False, use_bias=False, emask=y2 if pm else None)
+        g1 = _dgrad(c2, g2, None if pm else y2, (y1.shape[1], y1.shape[2]), emask=y1 if pm else None)
+        gs = gm if sh is None else _dgrad(sh, gm, None, in_hw)
+        emask = x if (pm and ctx.x_relu) else None
+        a_mask = None if pm else y1
         if c1.stride == 1:
-            gx = conv2d(g1, c1.bwd, stride=1, pad=c1.bwd_pad, relu=False, mask=y1, use_bias=False, res=gs,
+            gx = conv2d(g1, c1.bwd, stride=1, pad=c1.bwd_pad, relu=False, mask=a_mask, use_bias=False, res=gs,
                         emask=emask)
         else:
-            gx = _unit_dgrad(c1, g1, y1, in_hw) + gs
+            gx = _dgrad_strided(c1, g1, a_mask, in_hw) + gs
             if emask is not None:
                 gx = torch.ops.aten.threshold_backward(gx, emask, 0)
-        return gx, None, None
+        return gx, None
 
 
-def _unit_dgrad(unit: ConvUnit, gy, mask, in_hw):
-    """Input gradient of one conv unit (mask = its ReLU output, or None)."""
-    gy = gy.contiguous()
-    if unit.stride == 1:
-        return conv2d(gy, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, mask=mask, use_bias=False)
-    if unit.col_w is not None and COL2IM:
-        return _col2im_dgrad(gy, mask, unit, in_hw)
-    if SUBPIXEL:
-        return _subpixel_dgrad(gy, mask, unit, in_hw)
-    return conv2d(gy, unit.bwd, stride=unit.stride, pad=unit.pad, relu=False, mask=mask, in_mode="transpose",
-                  out_hw=in_hw, use_bias=False)
-
-
-def bottleneck(x: torch.Tensor, c1: ConvUnit, c2: ConvUnit, c3: ConvUnit, short: Optional[ConvUnit],
-               premasked: bool = False) -> torch.Tensor:
+def bottleneck(x: torch.Tensor, c1: ConvUnit, c2: ConvUnit, c3: ConvUnit, short: Optional[ConvUnit]) -> torch.Tensor:
     """ReLU(c3(c2(c1(x))) + short(x)) (c1, c2 with ReLU; c3, short linear)."""
     if x.is_cuda:
-        return _BottleneckFn.apply(x, (c1, c2, c3, short), premasked)
+        return _tag(_BottleneckFn.apply(x, (c1, c2, c3, short)), True)
     sc = short(x) if short is not None else x
     return torch.relu(c3(c2(c1(x))) + sc)

@@ -344,3 +344,28 @@ def test_sumsq_core_fwd_bwd(native_lib, dt):
         (gd,) = torch.autograd.grad(ld, xd, gl.to(DEV))
         assert ld.dtype == torch.float32 and torch.allclose(ld.cpu(), lc, rtol=1e-5)
         assert gd.dtype == dt and _rel(gd, gc) < 1e-2
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C,OC,k,ld", [(64, 147, 1, 152), (64, 64, 3, 64), (128, 200, 3, 208), (32, 3, 3, 8)])
+def test_conv_vector_epilogue_emask_partial_chunks(native_lib, dt, C, OC, k, ld):
+    """LDS-staged epilogue: output-mask (emask) without residual, row stride != OC, OC % 8 != 0
+    (element-wise tail chunk), accumulate into an existing output."""
+    g = torch.Generator().manual_seed(OC + k)
+    r = lambda t: t.to(dt).float()  # noqa: E731
+    N, H = 2, 13
+    x = r(torch.randn(N, H, H, C, generator=g))
+    cw = ConvWeights(r(torch.randn(OC, C, k, k, generator=g) / np.sqrt(C * k * k)), r(torch.randn(OC, generator=g)),
+                     "fwd")
+    em = r(torch.randn(N, H, H, OC, generator=g))
+    base = r(torch.randn(N, H, H, ld, generator=g))
+    ref = ops.conv2d(x, cw, relu=False) * (em > 0)
+    buf = base.to(dt).to(DEV)
+    got = ops.conv2d(x.to(dt).to(DEV), cw.to_device(DEV, dt), relu=False, out=buf[..., :OC],
+                     emask=em.to(dt).to(DEV))
+    assert _rel(got, ref) < 1e-2
+    assert torch.equal(buf[..., OC:].cpu(), base[..., OC:].to(dt))  # padding columns untouched
+    acc = ops.conv2d(x, cw, relu=True) + base[..., :OC]
+    buf = base.to(dt).to(DEV)
+    got = ops.conv2d(x.to(dt).to(DEV), cw.to_device(DEV, dt), relu=True, out=buf[..., :OC], accumulate=True)
+    assert _rel(got, acc) < 1e-2

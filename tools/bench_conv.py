@@ -11,8 +11,12 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from deconv_api_amd import ops
 from deconv_api_amd.ops.conv import ConvWeights, set_policy
