@@ -332,7 +332,7 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
             int(relu), int(relu_in), int(accumulate), int(code_div), x_ld, mask_ld, out_ld]
     bias = cw.bias_pad if use_bias else None
     lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
-             IMPL[_policy["impl"]] if res is None else IMPL["dma"], res, emask)  # residual: DMA kernel only
+             IMPL[_policy["impl"]] if res is None and emask is None else IMPL["dma"], res, emask)  # DMA-only epilogues
     if epilogue == "pool":
         return out, out_code
     return out
