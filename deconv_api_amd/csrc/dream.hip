@@ -122,8 +122,86 @@ __global__ void __launch_bounds__(256) col2im_kernel(const uint16_t* __restrict_
   }
 }
 
+// LDS-tiled col2im: a workgroup owns a TH x TW tile of dx; the cols rows it needs (a
+// contiguous run of ow per oh: rows_n x cols_n x J_ld elements) are staged into LDS with 16-B
+// loads, then every dx pixel gathers its taps from LDS. The scattered 6-byte global reads of the
+// simple kernel above become coalesced streaming reads.
+constexpr int C2I_TH = 8, C2I_TW = 64;
+
+__host__ __device__ inline int c2i_lo(int i0, int pad, int k, int s) {  // first o with o*s - pad + k - 1 >= i0
+  const int t = i0 + pad - k + 1;
+  return t <= 0 ? 0 : (t + s - 1) / s;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) col2im_lds_kernel(const uint16_t* __restrict__ cols,
+                                                         uint16_t* __restrict__ gx, Col2ImGeom g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int n = blockIdx.z;
+  const int ih0 = blockIdx.y * C2I_TH, iw0 = blockIdx.x * C2I_TW;
+  const int oh_lo = c2i_lo(ih0, g.pad_h, g.KH, g.stride);
+  const int oh_hi = min(g.OH - 1, (min(ih0 + C2I_TH, g.H) - 1 + g.pad_h) / g.stride);
+  const int ow_lo = c2i_lo(iw0, g.pad_w, g.KW, g.stride);
+  const int ow_hi = min(g.OW - 1, (min(iw0 + C2I_TW, g.W) - 1 + g.pad_w) / g.stride);
+  const int rows_n = oh_hi - oh_lo + 1, cols_n = ow_hi - ow_lo + 1;
+  uint16_t* tile = reinterpret_cast<uint16_t*>(lds);
+  if (rows_n > 0 && cols_n > 0) {
+    const int seg = cols_n * g.J_ld / 8;  // 16-B chunks per oh row
+    for (int c = threadIdx.x; c < rows_n * seg; c += 256) {
+      const int r = c / seg, q = c - r * seg;
+      const uint16_t* src = cols + (((long long)n * g.OH + oh_lo + r) * g.OW + ow_lo) * g.J_ld + q * 8;
+      *reinterpret_cast<uint4*>(tile + ((long long)r * cols_n * g.J_ld) + q * 8) =
+          *reinterpret_cast<const uint4*>(src);
+    }
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < C2I_TH * C2I_TW; p += 256) {
+    const int ih = ih0 + p / C2I_TW, iw = iw0 + p % C2I_TW;
+    if (ih >= g.H || iw >= g.W) continue;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int kh0 = (ih + g.pad_h) % g.stride, kw0 = (iw + g.pad_w) % g.stride;
+    for (int kh = kh0; kh < g.KH; kh += g.stride) {
+      const int oh = (ih + g.pad_h - kh) / g.stride;
+      if (ih + g.pad_h - kh < 0 || oh >= g.OH) continue;
+      for (int kw = kw0; kw < g.KW; kw += g.stride) {
+        const int ow = (iw + g.pad_w - kw) / g.stride;
+        if (iw + g.pad_w - kw < 0 || ow >= g.OW) continue;
+        const uint16_t* src = tile + ((oh - oh_lo) * cols_n + (ow - ow_lo)) * g.J_ld + (kh * g.KW + kw) * g.Cr;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (c < g.Cr) acc[c] += to_f<DT>(src[c]);
+      }
+    }
+    uint4 o;
+    o.x = pack2<DT>(acc[0], acc[1]);
+    o.y = pack2<DT>(acc[2], acc[3]);
+    o.z = pack2<DT>(acc[4], acc[5]);
+    o.w = pack2<DT>(acc[6], acc[7]);
+    *reinterpret_cast<uint4*>(gx + (((long long)n * g.H + ih) * g.W + iw) * 8) = o;
+  }
+}
+
 int col2im_launch(const uint16_t* cols, uint16_t* gx, const Col2ImGeom& g, int dtype, hipStream_t s) {
   if (g.Cr < 1 || g.Cr > 8 || g.stride < 1) return -1;
+  {
+    const int rows_max = (C2I_TH - 1 + g.KH - 1) / g.stride + 1, cols_max = (C2I_TW - 1 + g.KW - 1) / g.stride + 1;
+    const size_t lds = (size_t)rows_max * cols_max * g.J_ld * 2;
+    if (g.J_ld % 8 == 0 && lds <= 160 * 1024 && g.N <= 65535 && reinterpret_cast<uintptr_t>(cols) % 16 == 0) {
+      const dim3 grid((unsigned)((g.W + C2I_TW - 1) / C2I_TW), (unsigned)((g.H + C2I_TH - 1) / C2I_TH), (unsigned)g.N);
+      static const bool attr_ok = [] {  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
+        return hipFuncSetAttribute((const void*)col2im_lds_kernel<DT_F16>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+               hipFuncSetAttribute((const void*)col2im_lds_kernel<DT_BF16>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+      }();
+      if (!attr_ok) return -5;
+      if (dtype == DT_F16)
+        hipLaunchKernelGGL(col2im_lds_kernel<DT_F16>, grid, dim3(256), lds, s, cols, gx, g);
+      else
+        hipLaunchKernelGGL(col2im_lds_kernel<DT_BF16>, grid, dim3(256), lds, s, cols, gx, g);
+      return (int)hipGetLastError();
+    }
+  }
   const long long total = (long long)g.N * g.H * g.W;
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 256LL * 64);
   if (dtype == DT_F16)
