@@ -69,7 +69,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
 // stride as x) is > 0. The mask tile is DMA'd into LDS next to the A tile with the same offsets
 // and applied to each A fragment in registers right before its MFMAs.
 template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED,
-          bool MASK = false>
+          bool MASK = false, bool FRAGPIPE = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a, int tiles_n) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16;
@@ -277,6 +277,31 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const uint8_t* As = smem + cur * STAGE;
     const uint8_t* Bs = As + A_BYTES + M_BYTES;
+    if constexpr (FRAGPIPE && !MASK) {
+      // all fragments of a 32-K sub-step are read up front, and the next sub-step's reads are
+      // issued before this sub-step's MFMAs (register double buffer), so LDS latency hides
+      // behind FM*FN MFMAs instead of being exposed per A fragment
+      typedef typename Vec8<DT>::type v8;
+      v8 af[2][FM], bf[2][FN];
+      auto ld = [&](int s, int b) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[b][j] = *reinterpret_cast<const v8*>(Bs + (b_row0 + j * 16) * ROWB + sw[s]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[b][i] = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + sw[s]);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int s = 0; s < BK / 32; ++s) {
+        if (s + 1 < BK / 32) ld(s + 1, (s + 1) & 1);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[s & 1][i], bf[s & 1][j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      continue;
+    }
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       typedef typename Vec8<DT>::type v8;
@@ -496,7 +521,8 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
   }
 }
 
-template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI, bool MASK = false>
+template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI, bool MASK = false,
+          bool FP = false>
 static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   const int tiles_m = (a.M + BM - 1) / BM;
@@ -505,16 +531,17 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
   const bool aligned = (a.C % BK) == 0;
   if (aligned)
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK, FP>), dim3((unsigned)nwg),
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   else
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP>), dim3((unsigned)nwg),
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   return (int)hipGetLastError();
 }
 
 // DV_DMA_VARIANT: 0 (default) 2-stage BK64 except 256x128 (3-stage); 1: all 2-stage BK64;
-// 2: BK32 x 4-stage rings for 256x256 and 512x64 (A/B testing).
+// 2: BK32 x 4-stage rings for 256x256 and 512x64; 3: 128x256 3-stage for OC%256;
+// 4: register double-buffered fragments + s_setprio around MFMA runs (A/B testing).
 static int dma_variant() {
   static int v = [] {
     const char* e = std::getenv("DV_DMA_VARIANT");
@@ -526,7 +553,7 @@ static int dma_variant() {
 static int num_cus() {
   static int n = [] {
     int dev = 0, cu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cu = 256;
     return cu > 0 ? cu : 256;
   }();
   return n;
@@ -543,22 +570,28 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
   const long long cus = num_cus();
   auto nwg = [&](int BM, int BN) { return (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN); };
   if (a.OCpad % 256 == 0 && a.OC > 128) {
-    if constexpr (DT == DT_BF16)
+    if constexpr (DT == DT_BF16) {
       if (v == 2) return dma_cfg<DT, 2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
+      if (v == 4 && nwg(256, 256) >= cus) return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI, false, true>(a, s);
+    }
     if (v == 3 || (nwg(256, 256) < cus && nwg(128, 256) >= cus))
       return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
     if (nwg(256, 256) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
     return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 256
   }
   if (a.OCpad % 128 == 0 && a.OC > 64) {
-    if constexpr (DT == DT_BF16)
+    if constexpr (DT == DT_BF16) {
       if (v == 1) return dma_cfg<DT, 4, 2, 4, 4, 64, 2, AMODE, EPI>(a, s);
+      if (v == 4 && nwg(256, 128) >= cus) return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI, false, true>(a, s);
+    }
     if (nwg(256, 128) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
     return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 256 x 128
   }
   if (a.OCpad % 64 == 0 && a.OC > 16) {
-    if constexpr (DT == DT_BF16)
+    if constexpr (DT == DT_BF16) {
       if (v == 2) return dma_cfg<DT, 8, 1, 4, 4, 32, 4, AMODE, EPI>(a, s);
+      if (v == 4 && nwg(512, 64) >= cus) return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI, false, true>(a, s);
+    }
     if (nwg(512, 64) < cus) return dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 64
     return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s);  // 512 x 64
   }
