@@ -190,7 +190,17 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     // the DMA kernel addresses A with 32-bit offsets relative to the tile's first image
     const int64_t imgs_per_tile = 512 / std::max(1, a.OH * a.OW) + 2;
     TORCH_CHECK((int64_t)a.H * a.W * a.x_ld * 2 * imgs_per_tile < 0x7FFFFFF0LL, "conv dma: image too large");
+    // split-K when the tile grid would leave most CUs idle (plain epilogues only)
+    const bool plain_epi = (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && !a.accumulate && !a.res && !a.emask;
+    const int ks = plain_epi ? dv::conv_dma_splitk(a) : 1;
+    Tensor ws;
+    if (ks > 1) {
+      ws = at::empty({(int64_t)ks * a.M * a.OCpad}, x.options().dtype(at::kFloat));
+      a.ws = ws.data_ptr<float>();
+      a.ksplit = ks;
+    }
     check_rc(dv::conv_dma_launch(a, (int)amode, (int)epi, cur_stream()), "conv_dma");
+    if (ks > 1) check_rc(dv::splitk_reduce_launch(a, (int)epi, cur_stream()), "splitk_reduce");
   } else {
     check_rc(dv::conv_igemm_launch(a, (int)amode, (int)epi, cur_stream()), "conv_igemm");
   }

@@ -265,16 +265,19 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
 #pragma unroll
   for (int s = 0; s < BK / 32; ++s) sw[s] = (((s * 4 + (lane >> 4)) ^ rx) << 4);
 
-  const int nk = a.Kpad / BK;
+  // split-K (gridDim.y > 1): this workgroup reduces K tiles [k0, k0 + nk) into a partial sum
+  const int nk_all = a.Kpad / BK;
+  const int k0 = (int)(((long long)nk_all * blockIdx.y) / gridDim.y);
+  const int nk = (int)(((long long)nk_all * (blockIdx.y + 1)) / gridDim.y) - k0;
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nk) issue(p, p);
+    if (p < nk) issue(k0 + p, p);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt % STAGES;
     const int pend = min(STAGES - 2, nk - 1 - kt);
     wait_tiles(pend);
     __builtin_amdgcn_s_barrier();
-    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    if (kt + STAGES - 1 < nk) issue(k0 + kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const uint8_t* As = smem + cur * STAGE;
     const uint8_t* Bs = As + A_BYTES + M_BYTES;
     if constexpr (FRAGPIPE && !MASK) {
@@ -328,6 +331,22 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   }
 
   // ---- epilogue ----
+  if (a.ws != nullptr) {  // split-K partial: raw fp32 sums to ws[split][row][OCpad]
+    float* ws = a.ws + (long long)blockIdx.y * a.M * a.OCpad;
+    const int row_l = (lane >> 4) * 4, col_l = lane & 15;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wn * FN * 16 + j * 16 + col_l;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * FM * 16 + i * 16 + row_l + r;
+          if (row < a.M) ws[(long long)row * a.OCpad + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
   if constexpr (EPI == CONV_E_BF16) {
     if (a.vec_epi) {
       static_assert(BM * BN * 2 <= STAGES * STAGE, "C tile must fit in the operand stages");
@@ -530,18 +549,20 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   const long long nwg = (long long)tiles_m * tiles_n;
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
   const bool aligned = (a.C % BK) == 0;
+  const dim3 grid((unsigned)nwg, (unsigned)(a.ws ? a.ksplit : 1));
   if (aligned)
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK, FP>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK, FP>), grid,
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   else
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP>), dim3((unsigned)nwg),
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP>), grid,
                        dim3(WM * WN * 64), 0, s, a, tiles_n);
   return (int)hipGetLastError();
 }
 
 // DV_DMA_VARIANT: 0 (default) 2-stage BK64 except 256x128 (3-stage); 1: all 2-stage BK64;
 // 2: BK32 x 4-stage rings for 256x256 and 512x64; 3: 128x256 3-stage for OC%256;
-// 4: register double-buffered fragments + s_setprio around MFMA runs (A/B testing).
+// 4: register double-buffered fragments + s_setprio around MFMA runs (default for 256x256; v1
+// there selects the plain fragment loop) (A/B testing).
 static int dma_variant() {
   static int v = [] {
     const char* e = std::getenv("DV_DMA_VARIANT");
@@ -572,12 +593,13 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
   if (a.OCpad % 256 == 0 && a.OC > 128) {
     if constexpr (DT == DT_BF16) {
       if (v == 2) return dma_cfg<DT, 2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
-      if (v == 4 && nwg(256, 256) >= cus) return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI, false, true>(a, s);
+      if (v == 1 && nwg(256, 256) >= cus) return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);
     }
     if (v == 3 || (nwg(256, 256) < cus && nwg(128, 256) >= cus))
       return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
     if (nwg(256, 256) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
-    return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 256
+    // 256 x 256 with register double-buffered fragments: +3% on the big VGG layers (profiles/)
+    return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI, false, true>(a, s);
   }
   if (a.OCpad % 128 == 0 && a.OC > 64) {
     if constexpr (DT == DT_BF16) {
@@ -611,6 +633,78 @@ static int dma_mask_bn(const ConvArgs& a, hipStream_t s) {
   if (a.OCpad % 64 == 0 && a.OC > 16) return dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, CONV_E_BF16, true>(a, s);    // 256x64
   if (a.OCpad % 16 == 0) return dma_cfg<DT, 8, 1, 2, 1, 64, 2, AMODE, CONV_E_BF16, true>(a, s);                // 256x16
   return -3;
+}
+
+// Tile dims the default (DV_DMA_VARIANT=0) selection above picks, for split-K planning.
+static void dma_tile_dims(const ConvArgs& a, bool mask, int& BM, int& BN) {
+  const long long cus = num_cus();
+  auto nwg = [&](int bm, int bn) { return (long long)((a.M + bm - 1) / bm) * (a.OCpad / bn); };
+  BM = 256;
+  BN = 16;
+  if (mask) {
+    if (a.OCpad % 256 == 0 && a.OC > 128) { BM = 128; BN = 256; }
+    else if (a.OCpad % 128 == 0 && a.OC > 64) { BM = 128; BN = 128; }
+    else if (a.OCpad % 64 == 0 && a.OC > 16) { BM = 256; BN = 64; }
+    return;
+  }
+  if (a.OCpad % 256 == 0 && a.OC > 128) {
+    if (nwg(256, 256) >= cus) { BM = 256; BN = 256; }
+    else if (nwg(128, 256) >= cus) { BM = 128; BN = 256; }
+    else { BM = 128; BN = 128; }
+  } else if (a.OCpad % 128 == 0 && a.OC > 64) {
+    BM = nwg(256, 128) < cus ? 128 : 256;
+    BN = 128;
+  } else if (a.OCpad % 64 == 0 && a.OC > 16) {
+    BM = nwg(512, 64) < cus ? 256 : 512;
+    BN = 64;
+  } else {
+    BM = nwg(512, 16) < cus ? 256 : 512;
+  }
+}
+
+// Split-K factor for a launch that would leave most CUs idle: small M (batch-1 serving, deep
+// layers of strong-scaled DeepDream tiles, dense layers) with a long K. 1 = no split.
+int conv_dma_splitk(const ConvArgs& a) {
+  if (std::getenv("DV_NO_SPLITK")) return 1;
+  int BM, BN;
+  dma_tile_dims(a, a.mask != nullptr, BM, BN);
+  const long long nwg = (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN);
+  const int nk = a.Kpad / 64;
+  const long long cus = num_cus();
+  if (nwg * 2 > cus || nk < 8) return 1;
+  long long k = (cus + nwg - 1) / nwg;  // about one workgroup per CU
+  k = std::min<long long>(k, nk / 4);   // >= 4 K tiles per split keeps the pipeline primed
+  k = std::min<long long>(k, 32);
+  return k < 2 ? 1 : (int)k;
+}
+
+// out = act(sum_s ws[s] + bias): the split-K epilogue (16-bit or fp32 output, row stride out_ld)
+template <int DT>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a, int epi) {
+  const long long total = (long long)a.M * a.OC;
+  const long long plane = (long long)a.M * a.OCpad;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int row = (int)(t / a.OC), col = (int)(t % a.OC);
+    const float* w = a.ws + (long long)row * a.OCpad + col;
+    float v = a.bias ? a.bias[col] : 0.f;
+    for (int k = 0; k < a.ksplit; ++k) v += w[k * plane];
+    if (a.relu) v = fmaxf(v, 0.f);
+    const long long o = (long long)row * a.out_ld + col;
+    if (epi == CONV_E_F32)
+      reinterpret_cast<float*>(a.out)[o] = v;
+    else
+      reinterpret_cast<uint16_t*>(a.out)[o] = from_f<DT>(v);
+  }
+}
+
+int splitk_reduce_launch(const ConvArgs& a, int epi, hipStream_t s) {
+  const long long total = (long long)a.M * a.OC;
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 256LL * 16);
+  if (a.dtype == DT_F16)
+    hipLaunchKernelGGL(splitk_reduce_kernel<DT_F16>, dim3(grid), dim3(256), 0, s, a, epi);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel<DT_BF16>, dim3(grid), dim3(256), 0, s, a, epi);
+  return (int)hipGetLastError();
 }
 
 int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t s) {

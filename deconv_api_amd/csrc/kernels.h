@@ -46,11 +46,16 @@ struct ConvArgs {
   const uint16_t* emask;  // optional (16-bit out): out = 0 where emask <= 0 (same layout as out)
   long long emask_ld;
   int vec_epi;            // host-checked: 16-bit out/res/emask rows 16-B aligned -> LDS-staged epilogue
+  float* ws;              // split-K: fp32 partials [ksplit][M][OCpad] (LDS-DMA kernel), else nullptr
+  int ksplit;
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
 // LDS-DMA variant (FWD / TRANSPOSE, no mask): 8-wave 128x64-per-wave tiles
 int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
+// split-K planning (1 = none) and the reduction epilogue (bias, ReLU, 16-bit / fp32 out)
+int conv_dma_splitk(const ConvArgs& a);
+int splitk_reduce_launch(const ConvArgs& a, int epi, hipStream_t stream);
 
 // ---- misc kernels (misc.hip) ----
 // per-(image, channel) sums of a NHWC bf16 tensor: sums[n][c] = sum_{hw} x[n][hw][c]

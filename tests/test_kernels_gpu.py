@@ -369,3 +369,24 @@ def test_conv_vector_epilogue_emask_partial_chunks(native_lib, dt, C, OC, k, ld)
     buf = base.to(dt).to(DEV)
     got = ops.conv2d(x.to(dt).to(DEV), cw.to_device(DEV, dt), relu=True, out=buf[..., :OC], accumulate=True)
     assert _rel(got, acc) < 1e-2
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,C,OC,epi,relu", [(1, 7, 512, 512, "bf16", True), (2, 4, 256, 1000, "f32", False),
+                                               (4, 2, 1024, 64, "bf16", False), (1, 14, 512, 16, "f32", True)])
+def test_conv_splitk_small_m(native_lib, monkeypatch, dt, N, H, C, OC, epi, relu):
+    """Small-M convs take the split-K path (fp32 partials + reduce epilogue); compare with the fp32
+    reference and with the unsplit kernel."""
+    if dt == torch.float16 and epi == "f32":
+        pytest.skip("fp16 path has 16-bit epilogues only")
+    g = torch.Generator().manual_seed(C + OC)
+    r = lambda t: t.to(dt).float()  # noqa: E731
+    x = r(torch.randn(N, H, H, C, generator=g))
+    cw = ConvWeights(r(torch.randn(OC, C, 3, 3, generator=g) / np.sqrt(9 * C)), r(torch.randn(OC, generator=g)), "fwd")
+    ref = ops.conv2d(x, cw, relu=relu, epilogue=epi)
+    dw = cw.to_device(DEV, dt)
+    got = ops.conv2d(x.to(dt).to(DEV), dw, relu=relu, epilogue=epi)
+    assert _rel(got, ref) < 1e-2
+    monkeypatch.setenv("DV_NO_SPLITK", "1")
+    whole = ops.conv2d(x.to(dt).to(DEV), dw, relu=relu, epilogue=epi)
+    assert _rel(got, whole) < 1e-2
