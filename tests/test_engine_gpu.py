@@ -66,9 +66,13 @@ def test_graphed_engine_equals_eager(native_lib):
     eager = eng.run(x, "block4_pool", k=4)
     res = gd.run(x, "block4_pool")  # bucket 4, padded with a zero image
     assert bucket_for(3) == 4 and gd.captured == [("block4_pool", 4)]
-    assert torch.equal(res.mosaic[:3], eager.mosaic) and torch.equal(res.filters[:3], eager.filters)
+    # padding the batch changes M, which may change the split-K factor of small-M layers (fp32
+    # summation order), so results agree to rounding rather than bit-for-bit
+    assert torch.equal(res.filters[:3], eager.filters)
+    assert (res.mosaic[:3].int() - eager.mosaic.int()).abs().max() <= 2
     x2 = _x8(3, 224, 5).to(torch.bfloat16).cuda()  # replay with new data
-    assert torch.equal(gd.run(x2, "block4_pool").mosaic[:3], eng.run(x2, "block4_pool", k=4).mosaic)
+    d = gd.run(x2, "block4_pool").mosaic[:3].int() - eng.run(x2, "block4_pool", k=4).mosaic.int()
+    assert d.abs().max() <= 2
 
 
 def test_service_end_to_end_gpu(native_lib):
