@@ -101,7 +101,11 @@ def test_service_end_to_end_gpu(native_lib):
 
         # (batch composition may change split-K summation order -> rounding-level differences)
         d = np.abs(parse_result_data_url(outs[0]).astype(int) - parse_result_data_url(encode_data_url(want)).astype(int))
-        assert d.mean() < 0.5 and d.max() <= 24
+        assert d.mean() < 1.0
+        # before JPEG: the service's batched mosaics == the engine's, to rounding
+        raw = svc.run_batch("block3_pool", imgs)
+        ref = eng.run(svc.preprocess(imgs), "block3_pool", k=4).mosaic.cpu().numpy()
+        assert np.abs(raw.astype(int) - ref.astype(int)).max() <= 2
         assert svc.status()["graphs"]
     finally:
         svc.close()
