@@ -72,6 +72,14 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
         if force or _newer([src, *headers], obj):
             tasks.append([hipcc, *opt, *defs, f"--offload-arch={ARCH}", "-fPIC", "-std=c++17",
                           "-Wno-unused-result", f"-I{CSRC}", "-c", str(src), "-o", str(obj)])
+    for src in sorted(CSRC.glob("*.cpp")):  # host-only C++ (no torch / HIP): the JPEG encoder
+        if src.name == "bindings.cpp":
+            continue
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _newer([src, *headers], obj):
+            tasks.append(["g++", *opt, *defs, "-fPIC", "-std=c++17", "-pthread", "-D_GLIBCXX_USE_CXX11_ABI=1",
+                          f"-I{CSRC}", "-c", str(src), "-o", str(obj)])
     bsrc = CSRC / "bindings.cpp"
     bobj = BUILD / "bindings.o"
     objs.append(bobj)
@@ -92,7 +100,7 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
             link += [f"-L{d}"]
         torch_lib = libdirs[0]
         link += [f"-Wl,-rpath,{torch_lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
-                 "-ltorch_hip", "-lamdhip64"]
+                 "-ltorch_hip", "-lamdhip64", "-pthread"]
         _run(link)
     return TARGET
 

@@ -67,10 +67,50 @@ def read_data_url(uri: str) -> np.ndarray:
     return decode_image(b64decode_lenient(split_data_url(uri)))
 
 
-def encode_jpeg(rgb: np.ndarray, quality: int = JPEG_QUALITY) -> bytes:
+def _native():
+    """The native encoder (csrc/jpeg_enc.cpp) when the extension is built, else None."""
+    global _NATIVE
+    if _NATIVE is None:
+        try:
+            from ..ops import native
+
+            _NATIVE = native.load() if native.available() else False
+        except Exception:  # noqa: BLE001 - PIL fallback
+            _NATIVE = False
+    return _NATIVE or None
+
+
+_NATIVE = None
+
+
+def encode_jpeg_pil(rgb: np.ndarray, quality: int = JPEG_QUALITY) -> bytes:
     buf = io.BytesIO()
     Image.fromarray(np.ascontiguousarray(rgb)).save(buf, format="JPEG", quality=quality, subsampling=2)
     return buf.getvalue()
+
+
+def encode_jpeg(rgb: np.ndarray, quality: int = JPEG_QUALITY) -> bytes:
+    """Baseline JPEG (YCbCr 4:2:0, IJG tables) by the native encoder, which releases the GIL and
+    scales across threads (PIL's holds it: one core's worth of encodes per process); PIL when
+    the extension is not built."""
+    lib = _native()
+    if lib is None:
+        return encode_jpeg_pil(rgb, quality)
+    import torch
+
+    return lib.jpeg_encode(torch.from_numpy(np.ascontiguousarray(rgb, dtype=np.uint8)), int(quality))
+
+
+def encode_data_urls(mosaics: np.ndarray, quality: int = JPEG_QUALITY, threads: int = 8):
+    """[B, H, W, 3] uint8 -> B response strings; native: one GIL-free call, images (or restart
+    segments of them) spread over ``threads`` native threads."""
+    lib = _native()
+    if lib is None:
+        return [encode_data_url(m, quality) for m in mosaics]
+    import torch
+
+    return lib.jpeg_data_urls(torch.from_numpy(np.ascontiguousarray(mosaics, dtype=np.uint8)), int(quality),
+                              DATA_URL_PREFIX, int(threads))
 
 
 def quote_b64(b64: str) -> str:

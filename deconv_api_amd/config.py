@@ -37,7 +37,9 @@ class Config:
     batch_timeout_ms: float = 4.0
     max_queue: int = 4096                 # backpressure: 503 beyond this many pending requests
     request_timeout_s: float = 120.0
-    codec_workers: int = 8
+    codec_workers: int = 8                # decode threads (PIL releases the GIL while decoding)
+    encode_threads: int = 16              # native JPEG encoder threads per batch (GIL released)
+    native_codec: bool = True             # native encoder for responses (PIL fallback when False/unbuilt)
     cors_origins: Tuple[str, ...] = ("*",)  # app/main.py:22-32
     host: str = "0.0.0.0"
     port: int = 80                        # Dockerfile:10,15

@@ -5,6 +5,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include "jpeg_enc.h"
 #include "kernels.h"
 
 #include <cstdlib>
@@ -280,6 +281,35 @@ void col2im(Tensor cols, Tensor gx, std::vector<int64_t> g) {
            "col2im");
 }
 
+// Response encoding (host): uint8 RGB [B, H, W, 3] (CPU) -> B data URLs, JPEG + base64 + the
+// reference's quote() escaping, on `threads` native threads with the GIL released.
+py::list jpeg_data_urls(Tensor img, int64_t quality, std::string prefix, int64_t threads) {
+  TORCH_CHECK(!img.is_cuda() && img.scalar_type() == at::kByte && img.dim() == 4 && img.size(3) == 3 &&
+                  img.is_contiguous(),
+              "jpeg_data_urls: uint8 CPU [B, H, W, 3] contiguous");
+  std::vector<std::string> out;
+  {
+    py::gil_scoped_release nogil;
+    out = dvjpeg::encode_data_urls(img.data_ptr<uint8_t>(), (int)img.size(0), (int)img.size(1), (int)img.size(2),
+                                   (int)quality, prefix, (int)threads);
+  }
+  py::list res;
+  for (auto& s : out) res.append(py::str(s));
+  return res;
+}
+
+py::bytes jpeg_encode(Tensor img, int64_t quality) {
+  TORCH_CHECK(!img.is_cuda() && img.scalar_type() == at::kByte && img.dim() == 3 && img.size(2) == 3 &&
+                  img.is_contiguous(),
+              "jpeg_encode: uint8 CPU [H, W, 3] contiguous");
+  std::string s;
+  {
+    py::gil_scoped_release nogil;
+    s = dvjpeg::encode_jpeg(img.data_ptr<uint8_t>(), (int)img.size(0), (int)img.size(1), (int)quality);
+  }
+  return py::bytes(s);
+}
+
 void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -400,6 +430,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
+  m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");
+  m.def("jpeg_encode", &jpeg_encode, "native baseline JPEG encode (GIL released)");
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);
   m.def("seed_deconv3x3", &seed_deconv3x3);

@@ -2,7 +2,8 @@
 
 The reference runs each request to completion on the event-loop thread (``async def`` with
 blocking compute, app/main.py:46), so requests serialize and the server stalls. Here:
-  * decode (PIL) and JPEG encode run on a thread pool (they release the GIL);
+  * decode (PIL, releases the GIL) runs on a thread pool; responses are JPEG-encoded by the
+    native encoder (csrc/jpeg_enc.cpp) for a whole batch at once, GIL released, on native threads;
   * requests are queued and a single GPU worker thread drains them in batches (same target layer,
     up to ``max_batch``, waiting at most ``batch_timeout_ms`` for stragglers); one batch = one
     engine call over B images x 4 filters, replayed from a hipGraph per (layer, batch bucket);
@@ -26,7 +27,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..codec import CodecPool, encode_data_url, read_data_url
+from ..codec import CodecPool, encode_data_url, encode_data_urls, read_data_url
 from ..config import Config
 from ..engine.deconvnet import DeconvNet, UnknownLayerError
 from ..models.vgg16 import VGG16
@@ -81,6 +82,9 @@ class DeconvService:
 
             self.graphs = GraphedDeconv(engine, self.cfg.image_size, self.cfg.filters, self.cfg.mode)
         self.codec = CodecPool(self.cfg.codec_workers)
+        from ..codec.image import _native
+
+        self.native_codec = bool(self.cfg.native_codec and _native() is not None)
         self.q: "queue.Queue[_Job]" = queue.Queue()
         self.done_q: "queue.Queue" = queue.Queue()
         self.batches = 0
@@ -118,14 +122,17 @@ class DeconvService:
         fut = loop.create_future()
         self.q.put(_Job(layer, img, loop, fut))
         M.QUEUE_DEPTH.set(self.q.qsize())
-        mosaic = await asyncio.wait_for(fut, timeout=self.cfg.request_timeout_s)
-        return await loop.run_in_executor(self.codec.ex, encode_data_url, mosaic, self.cfg.jpeg_quality)
+        res = await asyncio.wait_for(fut, timeout=self.cfg.request_timeout_s)
+        if isinstance(res, str):  # encoded natively, batch-wide, by the completion thread
+            return res
+        return await loop.run_in_executor(self.codec.ex, encode_data_url, res, self.cfg.jpeg_quality)
 
     def status(self) -> dict:
         st = {"device": str(self.device), "worker_alive": self._thread.is_alive() and not self.stalled,
               "stalled": self.stalled, "queue_depth": self.q.qsize(),
               "batches": self.batches, "images": self.images, "last_error": self.last_error,
               "native": ops.native.available() if self.device.type == "cuda" else None,
+              "native_codec": self.native_codec,
               "graphs": [f"{l}:{b}" for l, b in self.graphs.captured] if self.graphs else None}
         if self.device.type == "cuda":
             st["gpu"] = torch.cuda.get_device_name(self.device)
@@ -201,6 +208,10 @@ class DeconvService:
             handle, group, layer, t0 = item
             try:
                 mos = self.finish_batch(handle)
+                if self.native_codec:
+                    # one GIL-free call: the batch's JPEG + base64 + quote on native threads (a
+                    # lone request is split into restart segments across the threads)
+                    mos = encode_data_urls(mos, self.cfg.jpeg_quality, self.cfg.encode_threads)
                 for j, m in zip(group, mos):
                     _deliver(j.loop, _set_result, j.future, m)
                 dt = time.perf_counter() - t0

@@ -179,3 +179,35 @@ def test_resize_oracle_properties():
     assert (ops.resize_u8_ref(const) == 77).all()
     up = ops.resize_u8_ref(_img(100, 57))
     assert up.shape == (224, 224, 3) and up.dtype == np.uint8
+
+
+def _native_or_skip():
+    from deconv_api_amd.ops import native
+
+    if not native.available():
+        pytest.skip("native extension not built")
+    return native.lib()
+
+
+def test_native_jpeg_encoder():
+    """csrc/jpeg_enc.cpp: a standard baseline JPEG (PIL decodes it), close to PIL's q95 4:2:0
+    encode of the same image, restart-segmented scans decode identically, and the data URL is
+    exactly prefix + quote(base64(jpeg))."""
+    lib = _native_or_skip()
+    rng = np.random.default_rng(0)
+    yy, xx = np.mgrid[0:96, 0:120].astype(np.float32)
+    base = 128 + 60 * np.sin(xx / 7) * np.cos(yy / 11) + rng.normal(0, 8, (96, 120))
+    img = np.clip(np.stack([base, base[::-1], 255 - base], -1), 0, 255).astype(np.uint8)
+    for im in (img, np.ascontiguousarray(img[:37, :53])):
+        jb = lib.jpeg_encode(torch.from_numpy(im), 95)
+        assert jb[:2] == b"\xff\xd8" and jb[-2:] == b"\xff\xd9"
+        dec = np.asarray(Image.open(io.BytesIO(jb)).convert("RGB")).astype(int)
+        buf = io.BytesIO()
+        Image.fromarray(im).save(buf, "JPEG", quality=95, subsampling=2)
+        ref = np.asarray(Image.open(io.BytesIO(buf.getvalue())).convert("RGB")).astype(int)
+        assert dec.shape == im.shape and np.abs(dec - ref).mean() < 2.0
+        for threads in (1, 3, 7):
+            url = lib.jpeg_data_urls(torch.from_numpy(im[None].copy()), 95, DATA_URL_PREFIX, threads)[0]
+            assert np.array_equal(parse_result_data_url(url).astype(int), dec)  # restart segments
+    url = lib.jpeg_data_urls(torch.from_numpy(img[None].copy()), 95, DATA_URL_PREFIX, 1)[0]
+    assert url == DATA_URL_PREFIX + quote(base64.b64encode(lib.jpeg_encode(torch.from_numpy(img), 95)).decode())
