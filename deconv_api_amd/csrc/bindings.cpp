@@ -310,6 +310,17 @@ py::bytes jpeg_encode(Tensor img, int64_t quality) {
   return py::bytes(s);
 }
 
+void softmax_rows(Tensor x, Tensor y) {
+  check_cuda(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kFloat && x.is_contiguous() && y.sizes() == x.sizes() &&
+                  y.scalar_type() == at::kFloat && y.is_contiguous(),
+              "softmax_rows: fp32 [M, N] contiguous");
+  check_rc(dv::softmax_rows_launch(x.data_ptr<float>(), y.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
+                                   cur_stream()),
+           "softmax_rows");
+}
+
 void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -431,6 +442,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
   m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");
+  m.def("softmax_rows", &softmax_rows, "row softmax (classifier head)");
   m.def("jpeg_encode", &jpeg_encode, "native baseline JPEG encode (GIL released)");
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);

@@ -95,6 +95,8 @@ struct Col2ImGeom {
   int N, H, W, OH, OW, KH, KW, stride, pad_h, pad_w, Cr, J_ld;
 };
 int col2im_launch(const uint16_t* cols, uint16_t* gx, const Col2ImGeom& g, int dtype, hipStream_t s);
+// row softmax (fp32 [M][N])
+int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s);
 }  // namespace dv

@@ -443,3 +443,36 @@ int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int 
 }
 
 }  // namespace dv
+
+namespace dv {
+
+// Row softmax for the classifier (predictions, 1000 classes): one 256-thread block per row, fp32,
+// max-subtracted; the reference's DActivation softmax (app/deepdream.py:226-235).
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ x, float* __restrict__ y, int N) {
+  __shared__ float red[4];
+  const float* xr = x + (long long)blockIdx.x * N;
+  float* yr = y + (long long)blockIdx.x * N;
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < N; i += 256) m = fmaxf(m, xr[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int i = threadIdx.x; i < N; i += 256) s += __expf(xr[i] - m);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float inv = 1.f / ((red[0] + red[1]) + (red[2] + red[3]));
+  for (int i = threadIdx.x; i < N; i += 256) yr[i] = __expf(xr[i] - m) * inv;
+}
+
+int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s) {
+  if (M <= 0 || N <= 0) return -1;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)M), dim3(256), 0, s, x, y, N);
+  return (int)hipGetLastError();
+}
+
+}  // namespace dv

@@ -72,6 +72,13 @@ class DeconvNet:
 
     def _dense_up(self, x: torch.Tensor, name: str) -> torch.Tensor:
         d = self.rt.dense[name]
+        if x.is_cuda and d.up is not None:  # MFMA GEMM with fused bias (+ReLU); HIP row softmax
+            B = x.shape[0]
+            xin = x.reshape(B, 1, 1, -1).to(self.rt.dtype).contiguous()
+            if d.spec.activation == "relu":
+                return ops.conv2d(xin, d.up, relu=True, pad=0).reshape(B, -1)
+            return ops.softmax_rows(ops.conv2d(xin, d.up, relu=False, pad=0, epilogue="f32").reshape(B, -1)).to(
+                self.rt.dtype)
         y = torch.matmul(x.to(d.w.dtype), d.w).float() + d.b
         if d.spec.activation == "relu":
             y = y.clamp_min(0)
@@ -186,10 +193,16 @@ class DeconvNet:
             j = li
             while self.specs[j].kind == "dense":
                 dl = self.rt.dense[self.specs[j].name]
-                d = torch.matmul(d.to(dl.wt.dtype), dl.wt).float()
+                relu_below = self.specs[j - 1].kind == "dense"  # the lower dense layer's activation.down
+                if d.is_cuda and dl.down is not None:
+                    M = d.shape[0]
+                    d = ops.conv2d(d.reshape(M, 1, 1, -1).to(self.rt.dtype).contiguous(), dl.down, relu=relu_below,
+                                   pad=0, epilogue="f32", use_bias=False).reshape(M, -1)
+                else:
+                    d = torch.matmul(d.to(dl.wt.dtype), dl.wt).float()
+                    if relu_below:
+                        d = d.clamp_min(0)
                 j -= 1
-                if self.specs[j].kind == "dense":
-                    d = d.clamp_min(0)  # the lower dense layer's activation.down (ReLU)
             assert self.specs[j].kind == "flatten"
             fs = self.specs[j]
             d = d.reshape(B * K, fs.out_hw, fs.out_hw, fs.cin).to(self.rt.dtype if dev.type == "cuda" else torch.float32)

@@ -70,6 +70,10 @@ class DenseLayer:
     w: torch.Tensor  # [in, out]
     b: torch.Tensor  # [out] fp32
     wt: Optional[torch.Tensor] = None  # [out, in] contiguous copy for the down GEMM on device
+    # GPU: the dense layer as a 1x1 conv on the MFMA kernel ([B, 1, 1, in] NHWC rows; fused bias +
+    # ReLU epilogue, split-K for small batches): up = x . W + b, down = y . W^T
+    up: Optional[ConvWeights] = None
+    down: Optional[ConvWeights] = None
 
 
 @dataclass
@@ -175,8 +179,14 @@ class VGG16Runtime:
                 k, b = model.params[s.name]
                 wdt = dtype if device.type == "cuda" else torch.float32
                 w = k.to(device=device, dtype=wdt).contiguous()
-                self.dense[s.name] = DenseLayer(s, w, b.to(device=device, dtype=torch.float32),
-                                                k.t().contiguous().to(device=device, dtype=wdt))
+                dl = DenseLayer(s, w, b.to(device=device, dtype=torch.float32),
+                                k.t().contiguous().to(device=device, dtype=wdt))
+                if device.type == "cuda":
+                    kin, kout = k.shape  # Keras kernel [in, out]
+                    dl.up = ConvWeights(k.t().reshape(kout, kin, 1, 1).contiguous(), b.clone(), "fwd").to_device(
+                        device, dtype)
+                    dl.down = ConvWeights(k.reshape(kin, kout, 1, 1).contiguous(), None, "fwd").to_device(device, dtype)
+                self.dense[s.name] = dl
 
     def layer_index(self, name: str) -> int:
         for i, s in enumerate(self.specs):

@@ -11,6 +11,16 @@ from .conv import maxpool_switch_ref, unpool_ref
 CAFFE_MEAN = (103.939, 116.779, 123.68)
 
 
+def softmax_rows(x: torch.Tensor) -> torch.Tensor:
+    """Row softmax of fp32 [M, N] (HIP kernel on the GPU)."""
+    if x.is_cuda:
+        x = x.float().contiguous()
+        y = torch.empty_like(x)
+        native.lib().softmax_rows(x, y)
+        return y
+    return torch.softmax(x.float(), dim=-1)
+
+
 def channel_sum(x: torch.Tensor) -> torch.Tensor:
     """x: [N, H, W, C] -> fp32 [N, C] per-image channel sums (reference app/deepdream.py:369-376
     sums each filter's map; the reference additionally sums over the batch axis, see

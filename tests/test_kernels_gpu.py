@@ -390,3 +390,31 @@ def test_conv_splitk_small_m(native_lib, monkeypatch, dt, N, H, C, OC, epi, relu
     monkeypatch.setenv("DV_NO_SPLITK", "1")
     whole = ops.conv2d(x.to(dt).to(DEV), dw, relu=relu, epilogue=epi)
     assert _rel(got, whole) < 1e-2
+
+
+def test_softmax_rows(native_lib):
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(5, 1000, generator=g) * 4
+    got = ops.softmax_rows(x.to(DEV))
+    assert torch.allclose(got.cpu(), torch.softmax(x, -1), rtol=1e-5, atol=1e-7)
+
+
+def test_dense_layers_as_mfma_gemm(native_lib, small_specs):
+    """Dense up (fused bias + ReLU / softmax) and down (y . W^T, ReLU of the layer below) on the
+    MFMA kernel match the fp32 CPU engine for dense targets."""
+    from deconv_api_amd.engine.deconvnet import DeconvNet
+    from deconv_api_amd.models.vgg16 import VGG16
+
+    m = VGG16.random(0, specs=small_specs)
+    cpu = DeconvNet(m.build("cpu", torch.float32))
+    gpu = DeconvNet(m.build(DEV, torch.bfloat16))
+    x = torch.randn(3, 32, 32, 8, generator=torch.Generator().manual_seed(1)) * 50
+    x[..., 3:] = 0
+    x = x.to(torch.bfloat16).float()
+    for layer in ("fc1", "fc2", "predictions"):
+        sg, sc = gpu.forward(x.to(torch.bfloat16).to(DEV), layer), cpu.forward(x, layer)
+        assert _rel(sg.out, sc.out) < 3e-2, layer
+        idx, _ = gpu.select_filters(sg.out, 4)
+        rg, rc = gpu.backward(sg, idx).cpu(), cpu.backward(sc, idx.cpu())
+        a, b = rg.double().flatten(), rc.double().flatten()
+        assert float(a @ b / (a.norm() * b.norm() + 1e-30)) > 0.98, layer
