@@ -181,10 +181,11 @@ class VGG16Runtime:
                 w = k.to(device=device, dtype=wdt).contiguous()
                 dl = DenseLayer(s, w, b.to(device=device, dtype=torch.float32),
                                 k.t().contiguous().to(device=device, dtype=wdt))
-                if device.type == "cuda":
-                    kin, kout = k.shape  # Keras kernel [in, out]
+                kin, kout = k.shape  # Keras kernel [in, out]
+                if device.type == "cuda" and kin % 8 == 0:  # the kernel's K gather is 8-channel granular
                     dl.up = ConvWeights(k.t().reshape(kout, kin, 1, 1).contiguous(), b.clone(), "fwd").to_device(
                         device, dtype)
+                if device.type == "cuda" and kout % 8 == 0:
                     dl.down = ConvWeights(k.reshape(kin, kout, 1, 1).contiguous(), None, "fwd").to_device(device, dtype)
                 self.dense[s.name] = dl
 

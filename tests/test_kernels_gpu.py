@@ -399,13 +399,15 @@ def test_softmax_rows(native_lib):
     assert torch.allclose(got.cpu(), torch.softmax(x, -1), rtol=1e-5, atol=1e-7)
 
 
-def test_dense_layers_as_mfma_gemm(native_lib, small_specs):
+def test_dense_layers_as_mfma_gemm(native_lib):
     """Dense up (fused bias + ReLU / softmax) and down (y . W^T, ReLU of the layer below) on the
     MFMA kernel match the fp32 CPU engine for dense targets."""
     from deconv_api_amd.engine.deconvnet import DeconvNet
-    from deconv_api_amd.models.vgg16 import VGG16
+    from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
 
-    m = VGG16.random(0, specs=small_specs)
+    m = VGG16.random(0, specs=vgg16_specs(width_div=8, image_size=32, fc=64, classes=24))
+    rt = m.build(DEV, torch.bfloat16)
+    assert all(d.up is not None and d.down is not None for d in rt.dense.values())
     cpu = DeconvNet(m.build("cpu", torch.float32))
     gpu = DeconvNet(m.build(DEV, torch.bfloat16))
     x = torch.randn(3, 32, 32, 8, generator=torch.Generator().manual_seed(1)) * 50
