@@ -18,6 +18,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace dv {
 
 namespace {
@@ -200,6 +202,199 @@ __global__ void __launch_bounds__(512, 1) conv3x3_c64_persist_kernel(const ConvA
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v2: unpool + 3x3 conv 64 -> 64 (block1_conv2.down), weights resident in VGPRs.
+//
+// v1 above keeps the weights in LDS and every wave re-reads all 64 output channels' fragments per
+// tile (8x redundant LDS traffic), and stages each halo between two barriers with the MFMA pipes
+// idle (PMC: ~19% MFMA-busy, half of all wave cycles parked on s_waitcnt / s_barrier;
+// profiles/pmc_flagship_sq_pass1.txt). Here:
+//   * wave w owns output rows {2(w/2), 2(w/2)+1} x 32 px x channels [32 (w%2), +32): FM=4 x FN=2
+//     fragments; its 32 channels' weights (18 K-steps x 2 fragments = 144 VGPRs) are loaded once;
+//   * the halo is double-buffered in LDS (2 x 48 KiB, 144-B padded pixels): tile t+1 is expanded
+//     into the other buffer right after tile t's MFMAs, so one barrier separates the tiles;
+//   * the halo is fed from POOLED pixels: each 16-B pooled chunk (+ its 8 switch codes) is loaded
+//     once and written to the <= 4 unpooled positions it covers (v1 loaded it 4x);
+//   * the output tile is staged in LDS (16-B chunks XOR-swizzled by pixel) and written with 16-B
+//     stores, 128 contiguous bytes per pixel.
+namespace {
+constexpr int V2_PH = TH / 2 + 2, V2_PW = TW / 2 + 2;   // pooled halo (6 x 18)
+constexpr int V2_TASKS = V2_PH * V2_PW * 8;              // 16-B pooled chunks per tile (864)
+constexpr int V2_PER_T = (V2_TASKS + 511) / 512;         // 2
+constexpr int V2_A = IH * IW * PIXB;                     // 48960
+constexpr int V2_C = TH * TW * 128;                      // 32768: bf16 output tile staging
+}  // namespace
+
+__global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * V2_A + V2_C];
+  uint8_t* Cst = smem + 2 * V2_A;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int kq = lane >> 4, col = lane & 15;
+  const int H = a.H, W = a.W, PH = H >> 1, PW = W >> 1;
+  const int tiles_w = (W + TW - 1) / TW, tiles_h = (H + TH - 1) / TH;
+  const int ntiles = a.N * tiles_h * tiles_w;
+
+  // ---- this wave's weights -> registers: k-step s = tap*2 + half, fragment j (16 channels) ----
+  bf16x8 bw[18][2];
+#pragma unroll
+  for (int s = 0; s < 18; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int oc = wc * 32 + j * 16 + col;
+      const int k = (s >> 1) * C64 + (s & 1) * 32 + kq * 8;
+      bw[s][j] = *reinterpret_cast<const bf16x8*>(a.w + (long long)oc * a.Kpad + k);
+    }
+  float biasv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int oc = wc * 32 + j * 16 + col;
+    biasv[j] = (a.bias && oc < a.OC) ? a.bias[oc] : 0.f;
+  }
+
+  uint4 ra[V2_PER_T];
+  uint2 rc[V2_PER_T];
+  int ld_py0 = 0, ld_px0 = 0;
+  // per-tile index math is recomputed from an opaque copy of the thread id: hoisted out of the
+  // persistent loop, these loop-invariant values would be held (and spilled) across the MFMAs,
+  // whose 144 weight registers leave no room for them
+  auto opaque_tid = [tid]() {
+    int v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"(tid));
+    return v;
+  };
+  auto load_tile = [&](int t) {  // raw pooled chunks + codes of tile t (zeros outside the map)
+    const int tid = opaque_tid();
+    int b = t;
+    const int tx = b % tiles_w;
+    b /= tiles_w;
+    const int ty = b % tiles_h;
+    const int n = b / tiles_h;
+    ld_py0 = ((ty * TH - 1) >> 1);  // floor: -1 for ty == 0
+    ld_px0 = ((tx * TW - 1) >> 1);
+    const long long nc = (long long)(n / a.code_div);
+#pragma unroll
+    for (int q = 0; q < V2_PER_T; ++q) {
+      const int idx = min(tid + q * 512, V2_TASKS - 1);
+      const int pp = idx >> 3, c8 = idx & 7;
+      const int py = ld_py0 + pp / V2_PW, px = ld_px0 + pp % V2_PW;
+      const int cy = min(max(py, 0), PH - 1), cx = min(max(px, 0), PW - 1);
+      ra[q] = *reinterpret_cast<const uint4*>(a.x + (((long long)n * PH + cy) * PW + cx) * a.x_ld + c8 * 8);
+      rc[q] = *reinterpret_cast<const uint2*>(a.code + ((nc * PH + cy) * PW + cx) * C64 + c8 * 8);
+    }
+  };
+  auto store_tile = [&](uint8_t* As, int t) {  // expand pooled chunks into the unpooled halo
+    const int tid = opaque_tid();
+    int b = t;
+    const int tx = b % tiles_w;
+    b /= tiles_w;
+    const int ty = b % tiles_h;
+    const int y0 = ty * TH - 1, x0 = tx * TW - 1;  // halo origin (unpooled)
+#pragma unroll
+    for (int q = 0; q < V2_PER_T; ++q) {
+      const int idx = tid + q * 512;
+      if (idx >= V2_TASKS) continue;
+      const int pp = idx >> 3, c8 = idx & 7;
+      const int py = ld_py0 + pp / V2_PW, px = ld_px0 + pp % V2_PW;
+      const bool in = (unsigned)py < (unsigned)PH && (unsigned)px < (unsigned)PW;
+      uint4 v = in ? ra[q] : make_uint4(0, 0, 0, 0);
+      if (a.relu_in) {
+        v.x = relu_bf2(v.x);
+        v.y = relu_bf2(v.y);
+        v.z = relu_bf2(v.z);
+        v.w = relu_bf2(v.w);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int hy = 2 * py + (d >> 1) - y0, hx = 2 * px + (d & 1) - x0;
+        if ((unsigned)hy >= (unsigned)IH || (unsigned)hx >= (unsigned)IW) continue;
+        const uint32_t sel4 = (uint32_t)d * 0x01010101u;
+        const uint32_t e0 = rc[q].x ^ sel4, e1 = rc[q].y ^ sel4;
+        auto keep2 = [](uint32_t e, int b0) -> uint32_t {
+          return ((((e >> (8 * b0)) & 0xFFu) == 0u) ? 0xFFFFu : 0u) |
+                 ((((e >> (8 * (b0 + 1))) & 0xFFu) == 0u) ? 0xFFFF0000u : 0u);
+        };
+        uint4 o;
+        o.x = v.x & keep2(e0, 0);
+        o.y = v.y & keep2(e0, 2);
+        o.z = v.z & keep2(e1, 0);
+        o.w = v.w & keep2(e1, 2);
+        *reinterpret_cast<uint4*>(As + (hy * IW + hx) * PIXB + c8 * 16) = o;
+      }
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t < ntiles) {
+    load_tile(t);
+    store_tile(smem, t);
+  }
+  __syncthreads();
+  int cur = 0;
+  while (t < ntiles) {
+    const int tcur = t;
+    t += gridDim.x;
+    if (t < ntiles) load_tile(t);  // in flight during the MFMAs
+    const uint8_t* As = smem + cur * V2_A;
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // A fragment address = per-fragment base (lane-dependent) + a compile-time tap/half offset
+    const uint8_t* Ab[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Ab[i] = As + ((2 * wr + (i >> 1)) * IW + (i & 1) * 16 + col) * PIXB + kq * 16;
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      const int tap = s >> 1, kh = tap / 3, kw = tap % 3;
+      const int off = (kh * IW + kw) * PIXB + (s & 1) * 64;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ab[i] + off);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[s][j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done with the previous tile's Cst reads and this halo
+    // ---- output tile -> Cst (bias, ReLU); C row = pixel, C col = channel ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ch = wc * 32 + j * 16 + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int pix = (2 * wr + (i >> 1)) * TW + (i & 1) * 16 + kq * 4 + r;
+          float v = acc[i][j][r] + biasv[j];
+          if (a.relu) v = fmaxf(v, 0.f);
+          *reinterpret_cast<uint16_t*>(Cst + pix * 128 + ((((ch >> 3) ^ (pix & 7))) << 4) + (ch & 7) * 2) = f2bf(v);
+        }
+      }
+    if (t < ntiles) store_tile(smem + (cur ^ 1) * V2_A, t);
+    __syncthreads();
+    // ---- Cst -> global, 16 B per store ----
+    {
+      const int tid = opaque_tid();
+      int b = tcur;
+      const int tx = b % tiles_w;
+      b /= tiles_w;
+      const int ty = b % tiles_h;
+      const int n = b / tiles_h;
+#pragma unroll
+      for (int q = 0; q < (TH * TW * 8) / 512; ++q) {
+        const int c = tid + q * 512, pix = c >> 3, cc = c & 7;
+        const int oy = ty * TH + pix / TW, ox = tx * TW + pix % TW;
+        if (oy >= H || ox >= W || cc * 8 >= a.OC) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(Cst + pix * 128 + ((cc ^ (pix & 7)) << 4));
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(a.out) + (((long long)n * H + oy) * W + ox) * a.out_ld +
+                                  cc * 8) = v;
+      }
+    }
+    cur ^= 1;
+  }
+}
+
 template <int FN, int EPI, bool UNPOOL>
 static int persist_cfg(const ConvArgs& a, hipStream_t s) {
   const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
@@ -221,6 +416,21 @@ int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s) {
     return -4;
   const bool narrow = a.OC <= 16;
   if (!narrow && a.OCpad != 64) return -5;
+  // v2: unpool + 64 -> 64 with a 16-B aligned bf16 output of 64-channel rows (block1_conv2.down)
+  if (unpool && !narrow && epi == CONV_E_BF16 && a.OC == 64 && a.out_ld % 8 == 0 && a.x_ld % 8 == 0 &&
+      (a.H % 2) == 0 && (a.W % 2) == 0 && std::getenv("DV_HALO_V1") == nullptr) {
+    static const int cus = [] {
+      int dev = 0, n = 256;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      return n > 0 ? n : 256;
+    }();
+    const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+    if (ntiles <= 0 || ntiles > 0x7fffffffLL) return -2;
+    hipLaunchKernelGGL(conv3x3_unpool_c64_v2_kernel, dim3((unsigned)std::min<long long>(ntiles, cus)), dim3(512), 0, s,
+                       a);
+    return (int)hipGetLastError();
+  }
 #define DV_P(FN, E) return unpool ? persist_cfg<FN, E, true>(a, s) : persist_cfg<FN, E, false>(a, s)
   if (epi == CONV_E_F32) {
     if (narrow) DV_P(1, CONV_E_F32);

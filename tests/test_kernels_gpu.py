@@ -142,7 +142,9 @@ def test_conv_mask_and_transpose(native_lib, conv_impl):
 
 @pytest.mark.parametrize("N,H,W,C,OC,unpool,epi", [(2, 20, 40, 64, 64, False, "bf16"), (1, 18, 34, 64, 64, True, "bf16"),
                                                     (3, 16, 64, 64, 3, False, "f32"), (1, 40, 30, 64, 48, True, "bf16"),
-                                                    (2, 12, 12, 64, 16, True, "f32"), (5, 33, 17, 64, 3, False, "f32")])
+                                                    (2, 12, 12, 64, 16, True, "f32"), (5, 33, 17, 64, 3, False, "f32"),
+                                                    (3, 48, 72, 64, 64, True, "bf16"), (2, 16, 32, 64, 64, True, "bf16"),
+                                                    (4, 10, 6, 64, 64, True, "bf16")])
 def test_conv_halo_kernel(native_lib, N, H, W, C, OC, unpool, epi):
     from deconv_api_amd.ops import conv as Cm
 
@@ -165,6 +167,17 @@ def test_conv_halo_kernel(native_lib, N, H, W, C, OC, unpool, epi):
     finally:
         Cm.set_policy(**old)
     assert got.shape == ref.shape and _rel(got, ref) < 1e-2
+    if unpool and OC == 64 and epi == "bf16":  # v2 (register-resident weights) vs v1: same math
+        import os
+
+        os.environ["DV_HALO_V1"] = "1"
+        try:
+            Cm.set_policy(impl="halo")
+            v1 = ops.conv2d(x.to(torch.bfloat16).to(DEV), cw.to_device(DEV), **kw)
+        finally:
+            del os.environ["DV_HALO_V1"]
+            Cm.set_policy(**old)
+        assert _rel(got, v1) < 1e-2
 
 
 def test_conv_channel_slices(native_lib):
