@@ -395,6 +395,217 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row-streaming 3x3 conv, 64 -> OC <= 16 channels (the final block1_conv1.down: 64 -> 3, fp32).
+//
+// This layer is an HBM stream: 6.6 GB of bf16 input per 1024 signals against 0.18 TFLOP of useful
+// math. The persistent halo kernel above re-stages a 10x34 halo per 8x32 tile between two
+// barriers (1.33x input, MFMAs idle while staging) and reached 2.1 TB/s. Here one workgroup
+// (4 waves) owns a 32-px column strip of one image and walks it top to bottom:
+//   * input rows (34 px x 128 B) go straight to LDS by buffer_load...lds into a ring of
+//     R = 4 (P + 2) row slots; conv padding and the strip/image edges are out-of-range offsets
+//     that read as 0. Every input row is fetched once per strip (1.06x instead of 1.33x);
+//   * P groups of 4 rows stay in flight behind the 2 groups being consumed (counted vmcnt, one
+//     raw s_barrier per group: loads are never drained by a barrier);
+//   * wave w computes output row 4i + w: 2 fragments of 16 px x one 16-wide N fragment, the 18
+//     K-step weight fragments live in VGPRs (72 registers), A fragments are read at a per-lane
+//     pixel address with the chunk XOR (pixel & 7) applied on the source side of the DMA;
+//   * fp32 output of a full strip row (32 px x 3 ch = 384 contiguous bytes) is staged in LDS and
+//     written with 16-B stores.
+namespace {
+constexpr int ST_W = 32;                  // output px per strip
+constexpr int ST_IN = ST_W + 2;           // input px per strip row
+constexpr int ST_SLOT = ST_IN * 128;      // 34 px: 4 x 1 KiB dwordx4 DMA + one 256-B dword DMA (2 px)
+}  // namespace
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+// LDS-DMA of 16 B per lane as inline asm. With the intrinsic, the compiler's waitcnt pass treats the
+// instruction's offset VGPR as pending until the load returns and put an s_waitcnt vmcnt(0) in
+// front of the first ds_read whose destination reused that register, draining every prefetched
+// row each iteration; here the only waits are the counted vmcnt's of the kernel. M0 (LDS base of
+// the 64 x 16 B destination) is set right before the load; nothing else in these kernels uses M0.
+__device__ __forceinline__ void dma16_asm(const i32x4& rsrc, uint32_t lds_addr, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voff), "s"(rsrc)
+               : "memory");
+}
+
+__device__ __forceinline__ void dma4_asm(const i32x4& rsrc, uint32_t lds_addr, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voff), "s"(rsrc)
+               : "memory");
+}
+
+// ReLU of 2 packed 16-bit floats as one v_pk_max_i16: negative values (sign bit set) are negative
+// int16, so max(v, 0) zeroes them (and -0) and keeps every non-negative value bit-exactly
+__device__ __forceinline__ uint32_t relu_pk16(uint32_t v) {
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), (s16x2){0, 0});
+  return __builtin_bit_cast(uint32_t, r);
+}
+
+template <int P, int EPI, bool RELU_IN>
+__global__ void __launch_bounds__(256, 1) conv3x3_c64_stream_kernel(const ConvArgs a) {
+  constexpr int R = 4 * (P + 2);
+  __shared__ __attribute__((aligned(16))) uint8_t smem[R * ST_SLOT + 4 * ST_W * 3 * 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kq = lane >> 4, col = lane & 15;
+  const int H = a.H, W = a.W;
+  const int strips_w = (W + ST_W - 1) / ST_W;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / strips_w;
+  const int x0 = (bid - n * strips_w) * ST_W;  // first output px of the strip
+
+  const long long img = (long long)H * W * a.x_ld;
+  const long long rem = (long long)a.N * img - (long long)n * img;
+  const uint64_t bytes = (uint64_t)(rem * 2);
+  // buffer descriptor as 4 SGPRs {base lo, base hi (stride 0), num_records, flags}
+  i32x4 xr;
+  {
+    const uint64_t base = reinterpret_cast<uint64_t>(a.x + (long long)n * img);
+    xr.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)base);
+    xr.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(base >> 32) & 0xFFFFu));
+    xr.z = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)bytes));
+    xr.w = 0x00020000;
+  }
+
+  // weights: k-step s = tap*2 + half; B fragment lane (col = out channel, kq = 8-element K chunk)
+  bf16x8 bw[18];
+#pragma unroll
+  for (int s = 0; s < 18; ++s) {
+    const int k = (s >> 1) * C64 + (s & 1) * 32 + kq * 8;
+    bw[s] = *reinterpret_cast<const bf16x8*>(a.w + (long long)col * a.Kpad + k);
+  }
+  float bias = (a.bias && col < a.OC) ? a.bias[col] : 0.f;
+  // consume the weight loads here, so the compiler's wait for them sits before the prologue DMAs
+  // (it cannot see the asm DMAs; a vmcnt(0) after them would drain the whole prefetch)
+#pragma unroll
+  for (int s = 0; s < 18; ++s) asm volatile("" : "+v"(bw[s]));
+  asm volatile("" : "+v"(bias));
+
+  // DMA lane geometry: instruction j covers strip pixels 8j..8j+7, lane -> (pixel, chunk slot)
+  const int lp = lane >> 3, lc = lane & 7;
+  auto issue_row = [&](int r) {  // input row r (may be -1 or >= H: zeros) -> its ring slot
+    uint8_t* dst = smem + ((r + 1) % R) * ST_SLOT;
+    const bool rok = (unsigned)r < (unsigned)H;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // pixels 0..31: lane -> (pixel 8j + lane/8, 16-B chunk slot lane%8)
+      const int pix = j * 8 + lp;
+      const int x = x0 - 1 + pix;
+      const bool ok = rok && (unsigned)x < (unsigned)W;
+      const uint32_t voff = ok ? (uint32_t)((((long long)r * W + x) * a.x_ld + ((lc ^ (pix & 7)) * 8)) * 2) : 0x80000000u;
+      dma16_asm(xr, (uint32_t)(uintptr_t)(dst + j * 1024), voff);
+    }
+    {  // pixels 32, 33: 4 B per lane, lane -> (pixel 32 + lane/32, dword lane%32 of the swizzled pixel)
+      const int pix = ST_W + (lane >> 5), wd = lane & 31;
+      const int x = x0 - 1 + pix;
+      const bool ok = rok && (unsigned)x < (unsigned)W;
+      const uint32_t voff =
+          ok ? (uint32_t)((((long long)r * W + x) * a.x_ld + (((wd >> 2) ^ (pix & 7)) * 8)) * 2 + (wd & 3) * 4) : 0x80000000u;
+      dma4_asm(xr, (uint32_t)(uintptr_t)(dst + 4 * 1024), voff);
+    }
+  };
+  // group g = input rows 4g-1 .. 4g+2, row 4g-1+w loaded by wave w
+#pragma unroll
+  for (int g = 0; g <= P; ++g) issue_row(4 * g - 1 + wave);
+
+  // per-lane A-fragment chunk offsets: pixel p = fi*16 + col + kw, chunk kc = half*4 + kq
+  int xo[3][2];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) xo[kw][h] = (col + kw) * 128 + (((h * 4 + kq) ^ ((col + kw) & 7)) << 4);
+  float* stage = reinterpret_cast<float*>(smem + R * ST_SLOT) + wave * ST_W * 3;
+  const bool vec_out = EPI == CONV_E_F32 && a.OC == 3 && a.out_ld == 3 && x0 + ST_W <= W && (W & 3) == 0 &&
+                       (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
+
+  const int iters = (H + 3) / 4;
+  for (int i = 0; i < iters; ++i) {
+    if constexpr (P >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * (P - 1)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_row(4 * (i + P + 1) - 1 + wave);  // past the map: zero rows (keeps the vmcnt count uniform)
+    const int y = 4 * i + wave;
+    if (y < H) {
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      // all 36 A fragments of the row are read before the first MFMA (LDS latency overlaps the
+      // reads instead of serializing read -> MFMA pairs: one wave per SIMD has nothing to hide it)
+      uint4 af[36];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const uint8_t* rowp = smem + ((y + kh) % R) * ST_SLOT;  // input row y-1+kh
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int fi = 0; fi < 2; ++fi)
+              af[((kh * 3 + kw) * 2 + h) * 2 + fi] = *reinterpret_cast<const uint4*>(rowp + fi * 16 * 128 + xo[kw][h]);
+      }
+#pragma unroll
+      for (int s = 0; s < 18; ++s)
+#pragma unroll
+        for (int fi = 0; fi < 2; ++fi) {
+          uint4 v = af[s * 2 + fi];
+          if constexpr (RELU_IN) {
+            v.x = relu_pk16(v.x);
+            v.y = relu_pk16(v.y);
+            v.z = relu_pk16(v.z);
+            v.w = relu_pk16(v.w);
+          }
+          acc[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, v), bw[s], acc[fi], 0, 0, 0);
+        }
+      // C fragment: lane holds px fi*16 + kq*4 + r of output channel col
+      const long long obase = ((long long)n * H + y) * W + x0;
+      if (vec_out) {
+        if (col < 3) {
+#pragma unroll
+          for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float v = acc[fi][r] + bias;
+              if (a.relu) v = fmaxf(v, 0.f);
+              stage[(fi * 16 + kq * 4 + r) * 3 + col] = v;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < ST_W * 3 / 4)
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.out) + obase * 3 + lane * 4) =
+              *reinterpret_cast<const float4*>(stage + lane * 4);
+        __builtin_amdgcn_wave_barrier();
+      } else if (col < a.OC) {
+#pragma unroll
+        for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ox = x0 + fi * 16 + kq * 4 + r;
+            if (ox >= W) continue;
+            float v = acc[fi][r] + bias;
+            if (a.relu) v = fmaxf(v, 0.f);
+            const long long o = (obase + (ox - x0)) * a.out_ld + col;
+            if constexpr (EPI == CONV_E_F32)
+              reinterpret_cast<float*>(a.out)[o] = v;
+            else
+              reinterpret_cast<uint16_t*>(a.out)[o] = f2bf(v);
+          }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup retires
+}
+
+static int stream_variant() {
+  static int v = [] {
+    const char* e = std::getenv("DV_STREAM_P");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
 template <int FN, int EPI, bool UNPOOL>
 static int persist_cfg(const ConvArgs& a, hipStream_t s) {
   const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
@@ -430,6 +641,30 @@ int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s) {
     hipLaunchKernelGGL(conv3x3_unpool_c64_v2_kernel, dim3((unsigned)std::min<long long>(ntiles, cus)), dim3(512), 0, s,
                        a);
     return (int)hipGetLastError();
+  }
+  if (!unpool && narrow && std::getenv("DV_HALO_V1") == nullptr) {  // row-streaming strips
+    const long long nwg = (long long)a.N * ((a.W + ST_W - 1) / ST_W);
+    if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
+    const int P = stream_variant();
+#define DV_S2(PP, E)                                                                                               \
+  do {                                                                                                             \
+    if (a.relu_in)                                                                                                 \
+      hipLaunchKernelGGL((conv3x3_c64_stream_kernel<PP, E, true>), dim3((unsigned)nwg), dim3(256), 0, s, a);       \
+    else                                                                                                           \
+      hipLaunchKernelGGL((conv3x3_c64_stream_kernel<PP, E, false>), dim3((unsigned)nwg), dim3(256), 0, s, a);      \
+  } while (0)
+#define DV_S(PP)                                                 \
+  do {                                                           \
+    if (epi == CONV_E_F32) DV_S2(PP, CONV_E_F32);                \
+    else DV_S2(PP, CONV_E_BF16);                                 \
+    return (int)hipGetLastError();                               \
+  } while (0)
+    if (P == 1) DV_S(1);
+    if (P == 3) DV_S(3);
+    if (P == 4) DV_S(4);
+    DV_S(2);
+#undef DV_S
+#undef DV_S2
   }
 #define DV_P(FN, E) return unpool ? persist_cfg<FN, E, true>(a, s) : persist_cfg<FN, E, false>(a, s)
   if (epi == CONV_E_F32) {

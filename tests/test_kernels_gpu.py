@@ -144,7 +144,9 @@ def test_conv_mask_and_transpose(native_lib, conv_impl):
                                                     (3, 16, 64, 64, 3, False, "f32"), (1, 40, 30, 64, 48, True, "bf16"),
                                                     (2, 12, 12, 64, 16, True, "f32"), (5, 33, 17, 64, 3, False, "f32"),
                                                     (3, 48, 72, 64, 64, True, "bf16"), (2, 16, 32, 64, 64, True, "bf16"),
-                                                    (4, 10, 6, 64, 64, True, "bf16")])
+                                                    (4, 10, 6, 64, 64, True, "bf16"), (2, 224, 224, 64, 3, False, "f32"),
+                                                    (2, 9, 64, 64, 3, False, "bf16"), (1, 7, 100, 64, 16, False, "f32"),
+                                                    (1, 3, 36, 64, 5, False, "f32")])
 def test_conv_halo_kernel(native_lib, N, H, W, C, OC, unpool, epi):
     from deconv_api_amd.ops import conv as Cm
 
