@@ -161,6 +161,16 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                        a.res == nullptr && a.emask == nullptr;
   // persistent weight-resident halo kernel: 64-channel inputs at large maps (block1 of VGG16)
   const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112 && a.res == nullptr && a.emask == nullptr;
+  // conv 64 -> 64 + fused 2x2 max-pool at large maps (VGG16 block1_conv2 forward): weight-resident
+  // halo kernel with LDS-DMA staging and the pool in registers
+  if (epi == dv::CONV_E_POOL && amode == dv::CONV_A_FWD && (impl == 0 || impl == 3) && a.H * a.W >= 112 * 112 &&
+      !mask.has_value() && std::getenv("DV_NO_POOL_V3") == nullptr) {
+    const int rc = dv::conv3x3_pool_v3_launch(a, cur_stream());
+    if (rc >= 0) {
+      check_rc(rc, "conv_pool_v3");
+      return;
+    }
+  }
   if (impl == 3 || (impl == 0 && halo_auto)) {
     TORCH_CHECK(halo_ok, "conv: halo-tile kernel does not support this shape/mode");
     check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream()), "conv_halo");

@@ -598,6 +598,180 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_stream_kernel(const ConvAr
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup retires
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// v3: forward 3x3 conv 64 -> 64 + bias + ReLU + fused 2x2 max-pool with switch codes
+// (block1_conv2 forward: 224x224x64 -> pooled 112x112x64 + uint8 codes).
+//
+// The implicit-GEMM kernel runs this layer at ~0.5 PF/s (512x64 tiles re-fetch every input pixel
+// per tap). Here (one 512-thread workgroup per CU, persistent over 8x32 output tiles):
+//   * wave w owns output rows {2(w/2), 2(w/2)+1} x 32 px x channels [32 (w%2), +32); its weights
+//     (18 K-steps x 2 fragments) stay in VGPRs, as in v2;
+//   * the 10 x 34 x 64 halo of the NEXT tile is LDS-DMA'd row by row (4 x 1 KiB + 256 B per row,
+//     chunk XOR (pixel & 7) applied on the source side) into the other half of a double buffer
+//     while this tile's MFMAs run: no register staging, no VALU on the input;
+//   * each lane's accumulators already hold whole 2x2 pool windows (rows i>>1, columns r, r+1), so
+//     max + first-max switch code are computed in registers; pooled bf16 values and codes are
+//     staged in LDS and written with 16-B stores (the full-resolution activation is never stored).
+namespace {
+constexpr int V3_BUF = IH * ST_SLOT;                 // 10 rows x 4352 B
+constexpr int V3_PV = (TH / 2) * (TW / 2) * 128;     // pooled bf16 staging (64 px x 64 ch)
+constexpr int V3_PC = (TH / 2) * (TW / 2) * 64;      // pooled code staging
+}  // namespace
+
+__global__ void __launch_bounds__(256, 1) conv3x3_c64_pool_v3_kernel(const ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * V3_BUF + V3_PV + V3_PC];
+  __shared__ float bias_s[64];
+  uint8_t* Pv = smem + 2 * V3_BUF;
+  uint8_t* Pc = Pv + V3_PV;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave;  // output rows 2 wr, 2 wr + 1; all 64 channels
+  const int kq = lane >> 4, col = lane & 15;
+  const int H = a.H, W = a.W, PH = H >> 1, PW = W >> 1;
+  const int tiles_w = (W + TW - 1) / TW, tiles_h = (H + TH - 1) / TH;
+  const int ntiles = a.N * tiles_h * tiles_w;
+
+  bf16x8 bw[18][4];
+#pragma unroll
+  for (int s = 0; s < 18; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oc = j * 16 + col;
+      const int k = (s >> 1) * C64 + (s & 1) * 32 + kq * 8;
+      bw[s][j] = *reinterpret_cast<const bf16x8*>(a.w + (long long)oc * a.Kpad + k);
+    }
+  if (tid < 64) bias_s[tid] = a.bias ? a.bias[tid] : 0.f;  // read back in the epilogue (frees VGPRs)
+#pragma unroll
+  for (int s = 0; s < 18; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(bw[s][j]));  // weight loads done before any DMA
+
+  // lane-dependent DMA address terms are recomputed from an opaque lane id in every call: hoisted
+  // out of the persistent loop they would be held across the MFMAs (weights fill the VGPRs)
+  auto issue_tile = [&](int t, uint8_t* buf) {  // 10 halo rows of tile t -> buf (50 DMA pieces)
+    int ln;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    const int lp = ln >> 3, lc = ln & 7;
+    int b = t;
+    const int tx = b % tiles_w;
+    b /= tiles_w;
+    const int ty = b % tiles_h;
+    const int n = __builtin_amdgcn_readfirstlane(b / tiles_h);
+    const int y0 = ty * TH - 1, x0 = tx * TW - 1;
+    const long long img = (long long)H * W * a.x_ld;
+    const uint64_t base = reinterpret_cast<uint64_t>(a.x + (long long)n * img);
+    i32x4 xr;
+    xr.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)base);
+    xr.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(base >> 32) & 0xFFFFu));
+    xr.z = __builtin_amdgcn_readfirstlane((int)(img * 2 > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)(img * 2)));
+    xr.w = 0x00020000;
+    for (int q = wave; q < IH * 5; q += 4) {  // wave-uniform piece list
+      const int hr = q / 5, piece = q - hr * 5;
+      const int y = y0 + hr;
+      const bool rok = (unsigned)y < (unsigned)H;
+      uint8_t* dst = buf + hr * ST_SLOT + piece * 1024;
+      if (piece < 4) {
+        const int pix = piece * 8 + lp;
+        const int x = x0 + pix;
+        const bool ok = rok && (unsigned)x < (unsigned)W;
+        const uint32_t voff = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + ((lc ^ (pix & 7)) * 8)) * 2) : 0x80000000u;
+        dma16_asm(xr, (uint32_t)(uintptr_t)dst, voff);
+      } else {
+        const int pix = TW + (ln >> 5), wd = ln & 31;
+        const int x = x0 + pix;
+        const bool ok = rok && (unsigned)x < (unsigned)W;
+        const uint32_t voff = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + (((wd >> 2) ^ (pix & 7)) * 8)) * 2 +
+                                              (wd & 3) * 4)
+                                 : 0x80000000u;
+        dma4_asm(xr, (uint32_t)(uintptr_t)dst, voff);
+      }
+    }
+  };
+
+
+  int t = blockIdx.x;
+  if (t < ntiles) issue_tile(t, smem);
+  int cur = 0;
+  while (t < ntiles) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int tcur = t;
+    t += gridDim.x;
+    if (t < ntiles) issue_tile(t, smem + (cur ^ 1) * V3_BUF);
+    const uint8_t* buf = smem + cur * V3_BUF;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      const int tap = s >> 1, kh = tap / 3, kw = tap % 3, h = s & 1;
+      const int p = col + kw;  // A-fragment pixel within the halo row (+ 16 for i & 1)
+      const int xo = p * 128 + (((h * 4 + kq) ^ (p & 7)) << 4);
+      uint4 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const uint4*>(buf + (2 * wr + (i >> 1) + kh) * ST_SLOT + (i & 1) * 2048 + xo);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]), bw[s][j], acc[i][j], 0,
+                                                              0, 0);
+    }
+    // ---- 2x2 max-pool in registers: window (rows i>>1 = 0/1) x (columns r = 2q, 2q+1) ----
+#pragma unroll
+    for (int hx = 0; hx < 2; ++hx)      // 16-px half of the row (fragment i & 1)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = j * 16 + col;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          float best = -INFINITY;
+          int code = 0;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            float v = acc[hx + 2 * (d >> 1)][j][2 * q + (d & 1)] + bias_s[ch];
+            if (a.relu) v = fmaxf(v, 0.f);
+            v = bf2f(f2bf(v));
+            if (v > best) {
+              best = v;
+              code = d;
+            }
+          }
+          const int pix = wr * 16 + hx * 8 + kq * 2 + q;  // pooled pixel within the 4 x 16 tile
+          *reinterpret_cast<uint16_t*>(Pv + pix * 128 + ((((ch >> 3) ^ (pix & 7))) << 4) + (ch & 7) * 2) = f2bf(best);
+          Pc[pix * 64 + ch] = (uint8_t)code;
+        }
+      }
+    __syncthreads();
+    {
+      int b = tcur;
+      const int tx = b % tiles_w;
+      b /= tiles_w;
+      const int ty = b % tiles_h;
+      const int n = b / tiles_h;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {  // 64 px x 8 chunks = two 16-B chunks per thread
+        const int c = tid + q * 256, pix = c >> 3, cc = c & 7;
+        const int py = ty * (TH / 2) + (pix >> 4), px = tx * (TW / 2) + (pix & 15);
+        if (py < PH && px < PW) {
+          const long long prow = ((long long)n * PH + py) * PW + px;
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(a.out) + prow * a.out_ld + cc * 8) =
+              *reinterpret_cast<const uint4*>(Pv + pix * 128 + ((cc ^ (pix & 7)) << 4));
+          if (cc < 4)
+            *reinterpret_cast<uint4*>(a.out_code + prow * 64 + cc * 16) =
+                *reinterpret_cast<const uint4*>(Pc + pix * 64 + cc * 16);
+        }
+      }
+    }
+    cur ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 static int stream_variant() {
   static int v = [] {
     const char* e = std::getenv("DV_STREAM_P");
@@ -618,6 +792,24 @@ static int persist_cfg(const ConvArgs& a, hipStream_t s) {
   }();
   const long long grid = std::min<long long>(ntiles, (long long)cus);
   hipLaunchKernelGGL((conv3x3_c64_persist_kernel<FN, EPI, UNPOOL>), dim3((unsigned)grid), dim3(512), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int conv3x3_pool_v3_launch(const ConvArgs& a, hipStream_t s) {
+  if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.C != C64 || a.OC != 64 ||
+      a.OCpad != 64 || a.H != a.OH || a.W != a.OW || (a.H & 1) || (a.W & 1) || a.accumulate || a.mask ||
+      a.Kpad < KW9 || a.x_ld % 8 || a.out_ld % 8 || a.dtype != DT_BF16 || a.res || a.emask ||
+      (reinterpret_cast<uintptr_t>(a.out) & 15) || (reinterpret_cast<uintptr_t>(a.out_code) & 15))
+    return -4;
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+  if (ntiles <= 0 || ntiles > 0x7fffffffLL) return -2;
+  hipLaunchKernelGGL(conv3x3_c64_pool_v3_kernel, dim3((unsigned)std::min<long long>(ntiles, cus)), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 

@@ -99,4 +99,6 @@ int col2im_launch(const uint16_t* cols, uint16_t* gx, const Col2ImGeom& g, int d
 int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s);
+// 3x3 conv 64 -> 64 + bias + ReLU + fused 2x2 max-pool/switch (bf16); < 0 if the shape is unsupported
+int conv3x3_pool_v3_launch(const ConvArgs& a, hipStream_t s);
 }  // namespace dv

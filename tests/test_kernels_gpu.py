@@ -104,6 +104,32 @@ def test_conv_pool_epilogue(native_lib):
     assert agree.float().mean() > 0.999
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 112, 120), (1, 118, 112), (1, 224, 224)])
+def test_conv_pool_v3(native_lib, N, H, W):
+    """64 -> 64 conv + fused pool at >= 112^2 maps (weight-resident halo kernel) vs the fp32 reference
+    and vs the implicit-GEMM pool epilogue (DV_NO_POOL_V3)."""
+    import os
+
+    g = torch.Generator().manual_seed(41)
+    x = torch.relu(torch.randn(N, H, W, 64, generator=g))
+    cw = _cw(64, 64)
+    (rp, rc), (gp, gc) = _cmp_conv(x, cw, epilogue="pool")
+    assert gp.shape == (N, H // 2, W // 2, 64) and gc.shape == gp.shape
+    assert _rel(gp, rp) < 1e-2
+    full = ops.conv2d(_bf(x), cw).float()
+    win = full.view(N, H // 2, 2, W // 2, 2, 64).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4, 64)
+    top2 = win.topk(2, dim=3).values
+    clear = (top2[:, :, :, 0] - top2[:, :, :, 1]) > 0.02 * top2[:, :, :, 0].abs().clamp_min(1e-3)
+    assert (gc.cpu() == rc)[clear].float().mean() > 0.999
+    os.environ["DV_NO_POOL_V3"] = "1"
+    try:
+        ip, ic = ops.conv2d(x.to(torch.bfloat16).to(DEV), cw.to_device(DEV), epilogue="pool")
+    finally:
+        del os.environ["DV_NO_POOL_V3"]
+    assert _rel(gp, ip) < 1e-2
+    assert (gc == ic).float().mean() > 0.995
+
+
 def test_conv_unpool_gather(native_lib):
     g = torch.Generator().manual_seed(5)
     K = 2
