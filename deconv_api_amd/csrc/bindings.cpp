@@ -40,7 +40,8 @@ void check_rc(int rc, const char* what) {
 //       code_div, x_ld, mask_ld, out_ld
 void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
           c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
-          int64_t epi, int64_t impl, c10::optional<Tensor> res, c10::optional<Tensor> emask) {
+          int64_t epi, int64_t impl, c10::optional<Tensor> res, c10::optional<Tensor> emask,
+          c10::optional<Tensor> stats, int64_t stats_div) {
   TORCH_CHECK(g.size() == 23, "conv: geometry vector must have 23 entries");
   check_cuda(x, "x");
   check_cuda(w, "w");
@@ -150,6 +151,24 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     a.vec_epi = epi == dv::CONV_E_BF16 && al(a.out, a.out_ld) && (!a.res || al(a.res, a.res_ld)) &&
                 (!a.emask || al(a.emask, a.emask_ld)) && std::getenv("DV_NO_VEC_EPI") == nullptr;
   }
+  bool stats_done = false;
+  if (stats.has_value()) {  // per-(image) {sum, sum^2} of the fp32 output for the single-pass deprocess
+    check_cuda(*stats, "stats");
+    TORCH_CHECK(epi == dv::CONV_E_F32 && stats->scalar_type() == at::kDouble && stats->is_contiguous() &&
+                    stats_div >= 1 && a.N % stats_div == 0 && stats->numel() == 2 * (a.N / stats_div) &&
+                    a.out_ld == a.OC,
+                "conv stats: fp64 [N/stats_div, 2], fp32 dense output");
+    check_rc((int)hipMemsetAsync(stats->data_ptr(), 0, stats->numel() * 8, cur_stream()), "stats memset");
+    a.stats = stats->data_ptr<double>();
+    a.stats_div = (int)stats_div;
+  }
+  // statistics the chosen kernel did not produce: one extra pass over the fp32 output
+  auto finish_stats = [&]() {
+    if (stats.has_value() && !stats_done)
+      check_rc(dv::recon_stats_launch(reinterpret_cast<const float*>(a.out), a.stats,
+                                      (long long)a.stats_div * a.OH * a.OW * a.OC, a.N / a.stats_div, cur_stream()),
+               "recon_stats");
+  };
   // Kernel choice. impl: 0 auto, 1 register-staged (conv_igemm), 2 LDS-DMA (conv_dma), 3 halo-tile.
   //  * halo-tile (3x3 s1 p1, OC tile <= 64, >= 56x56 maps): input staged once per tile, unpool fused
   //  * LDS-DMA: FWD / TRANSPOSE (optionally ReLU-masked); an unpool input is first materialized
@@ -168,12 +187,15 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     const int rc = dv::conv3x3_pool_v3_launch(a, cur_stream());
     if (rc >= 0) {
       check_rc(rc, "conv_pool_v3");
+      finish_stats();
       return;
     }
   }
   if (impl == 3 || (impl == 0 && halo_auto)) {
     TORCH_CHECK(halo_ok, "conv: halo-tile kernel does not support this shape/mode");
-    check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream()), "conv_halo");
+    check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream(), &stats_done),
+             "conv_halo");
+    finish_stats();
     return;
   }
   // ReLU-masked A (dgrad): the DMA kernel stages the mask with x's offsets, so it needs mask_ld == x_ld
@@ -215,6 +237,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   } else {
     check_rc(dv::conv_igemm_launch(a, (int)amode, (int)epi, cur_stream()), "conv_igemm");
   }
+  finish_stats();
 }
 
 // kind 0 max / 1 avg; dir 0 fwd (in=x, out=y) / 1 bwd (in=gy, out=gx); geom = N,H,W,C,OH,OW,k,s,pad
@@ -375,7 +398,7 @@ void seed_deconv3x3(Tensor S, Tensor f, Tensor wt, Tensor out) {
            "seed_deconv3x3");
 }
 
-void deprocess_mosaic(Tensor recon, Tensor out, int64_t tiles, bool reverse) {
+void deprocess_mosaic(Tensor recon, Tensor out, int64_t tiles, bool reverse, c10::optional<Tensor> stats) {
   check_cuda(recon, "recon");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(recon.device());
   TORCH_CHECK(recon.dim() == 4 && recon.size(3) == 3 && recon.scalar_type() == at::kFloat && recon.is_contiguous(),
@@ -386,9 +409,27 @@ void deprocess_mosaic(Tensor recon, Tensor out, int64_t tiles, bool reverse) {
   const int64_t rows = (tiles + 1) / 2;
   TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.numel() == B * rows * H * 2 * W * 3,
               "deprocess: out [B, rows*H, 2*W, 3] u8");
-  check_rc(dv::deprocess_mosaic_launch(recon.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)B, (int)H, (int)W,
-                                       (int)tiles, reverse ? 1 : 0, cur_stream()),
-           "deprocess_mosaic");
+  if (W % 4 != 0 || std::getenv("DV_DEPROCESS_V1")) {  // one block per image, two-pass statistics
+    check_rc(dv::deprocess_mosaic_launch(recon.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)B, (int)H, (int)W,
+                                         (int)tiles, reverse ? 1 : 0, cur_stream()),
+             "deprocess_mosaic");
+    return;
+  }
+  Tensor st;
+  if (stats.has_value()) {  // {sum, sum^2} per image, from the final conv's epilogue
+    TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->is_contiguous() && stats->numel() == 2 * B &&
+                    stats->device() == recon.device(),
+                "deprocess: stats fp64 [B, 2]");
+    st = *stats;
+  } else {
+    st = at::zeros({B, 2}, recon.options().dtype(at::kDouble));
+    check_rc(dv::recon_stats_launch(recon.data_ptr<float>(), st.data_ptr<double>(), tiles * H * W * 3, (int)B,
+                                    cur_stream()),
+             "recon_stats");
+  }
+  check_rc(dv::deprocess_apply_launch(recon.data_ptr<float>(), st.data_ptr<double>(), out.data_ptr<uint8_t>(), (int)B,
+                                      (int)H, (int)W, (int)tiles, reverse ? 1 : 0, cur_stream()),
+           "deprocess_apply");
 }
 
 void resize_preprocess(Tensor img, Tensor out, int64_t mode) {
@@ -446,7 +487,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv", &conv, "MFMA implicit-GEMM conv (fwd / unpool-gather / transposed; bf16/pool/f32 epilogues)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("out_code"), py::arg("code"),
         py::arg("mask"), py::arg("geom"), py::arg("amode"), py::arg("epi"), py::arg("impl"),
-        py::arg("res") = py::none(), py::arg("emask") = py::none());
+        py::arg("res") = py::none(), py::arg("emask") = py::none(), py::arg("stats") = py::none(),
+        py::arg("stats_div") = 1);
   m.def("pool", &pool, "k x k max/avg pooling forward/backward");
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
@@ -457,7 +499,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);
   m.def("seed_deconv3x3", &seed_deconv3x3);
-  m.def("deprocess_mosaic", &deprocess_mosaic);
+  m.def("deprocess_mosaic", &deprocess_mosaic, py::arg("recon"), py::arg("out"), py::arg("tiles"), py::arg("reverse"),
+        py::arg("stats") = py::none());
   m.def("resize_preprocess", &resize_preprocess);
   m.def("maxpool2x2", &maxpool2x2);
   m.def("unpool2x2", &unpool2x2);

@@ -522,6 +522,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_stream_kernel(const ConvAr
   const bool vec_out = EPI == CONV_E_F32 && a.OC == 3 && a.out_ld == 3 && x0 + ST_W <= W && (W & 3) == 0 &&
                        (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
 
+  double st1 = 0.0, st2 = 0.0;  // this lane's share of sum(out), sum(out^2) (a.stats)
   const int iters = (H + 3) / 4;
   for (int i = 0; i < iters; ++i) {
     if constexpr (P >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * (P - 1)) : "memory");
@@ -568,6 +569,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_stream_kernel(const ConvAr
             for (int r = 0; r < 4; ++r) {
               float v = acc[fi][r] + bias;
               if (a.relu) v = fmaxf(v, 0.f);
+              st1 += v;
+              st2 += (double)v * v;
               stage[(fi * 16 + kq * 4 + r) * 3 + col] = v;
             }
         }
@@ -586,6 +589,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_stream_kernel(const ConvAr
             if (ox >= W) continue;
             float v = acc[fi][r] + bias;
             if (a.relu) v = fmaxf(v, 0.f);
+            st1 += v;
+            st2 += (double)v * v;
             const long long o = (obase + (ox - x0)) * a.out_ld + col;
             if constexpr (EPI == CONV_E_F32)
               reinterpret_cast<float*>(a.out)[o] = v;
@@ -593,6 +598,15 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_stream_kernel(const ConvAr
               reinterpret_cast<uint16_t*>(a.out)[o] = f2bf(v);
           }
       }
+    }
+  }
+  if (a.stats) {  // per-image statistics for the single-pass deprocess (one atomic pair per wave)
+    st1 = wave_sum_d(st1);
+    st2 = wave_sum_d(st2);
+    if (lane == 0) {
+      double* d = a.stats + 2 * (n / a.stats_div);
+      atomicAdd(d, st1);
+      atomicAdd(d + 1, st2);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup retires
@@ -774,8 +788,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_pool_v3_kernel(const ConvA
 
 static int stream_variant() {
   static int v = [] {
-    const char* e = std::getenv("DV_STREAM_P");
-    return e ? std::atoi(e) : 2;
+    const char* e = std::getenv("DV_STREAM_P");  // measured: P=1 (3 WG/CU) 1.57 ms, P=2 1.60, P=3 1.94
+    return e ? std::atoi(e) : 1;
   }();
   return v;
 }
@@ -813,7 +827,7 @@ int conv3x3_pool_v3_launch(const ConvArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s) {
+int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, bool* stats_done) {
   if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.C != C64 || a.H != a.OH ||
       a.W != a.OW || a.accumulate || a.mask || a.Kpad < KW9)
     return -4;
@@ -838,6 +852,7 @@ int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s) {
     const long long nwg = (long long)a.N * ((a.W + ST_W - 1) / ST_W);
     if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
     const int P = stream_variant();
+    if (stats_done) *stats_done = a.stats != nullptr;
 #define DV_S2(PP, E)                                                                                               \
   do {                                                                                                             \
     if (a.relu_in)                                                                                                 \

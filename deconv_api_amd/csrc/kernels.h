@@ -48,6 +48,8 @@ struct ConvArgs {
   int vec_epi;            // host-checked: 16-bit out/res/emask rows 16-B aligned -> LDS-staged epilogue
   float* ws;              // split-K: fp32 partials [ksplit][M][OCpad] (LDS-DMA kernel), else nullptr
   int ksplit;
+  double* stats;          // optional (row-streaming kernel): stats[n / stats_div] += {sum out, sum out^2}
+  int stats_div;
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
@@ -68,6 +70,11 @@ int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint
 // fp32 recon [B*4][224][224][3] -> u8 mosaic [B][448][448][3] (channel-reversed), Keras deprocess
 int deprocess_mosaic_launch(const float* recon, uint8_t* out, int B, int H, int W, int tiles,
                             int reverse_channels, hipStream_t s);
+// per-group {sum, sum of squares} (fp64, atomically ADDED to stats[g][2]) of fp32 data [groups][per_group]
+int recon_stats_launch(const float* x, double* stats, long long per_group, int groups, hipStream_t s);
+// deprocess with precomputed per-image stats (single pass, 4 px per thread); W % 4 == 0
+int deprocess_apply_launch(const float* recon, const double* stats, uint8_t* out, int B, int H, int W, int tiles,
+                           int reverse_channels, hipStream_t s);
 // uint8 [B][Hs][Ws][3] RGB -> bf16 NHWC [B][OH][OW][Cpad]: cv2 INTER_LINEAR resize + caffe mean subtract
 int resize_preprocess_launch(const uint8_t* img, int B, int Hs, int Ws, uint16_t* out, int OH, int OW,
                              int Cpad, int mode, hipStream_t s);
@@ -98,7 +105,7 @@ int col2im_launch(const uint16_t* cols, uint16_t* gx, const Col2ImGeom& g, int d
 // row softmax (fp32 [M][N])
 int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
-int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s);
+int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, bool* stats_done = nullptr);
 // 3x3 conv 64 -> 64 + bias + ReLU + fused 2x2 max-pool/switch (bf16); < 0 if the shape is unsupported
 int conv3x3_pool_v3_launch(const ConvArgs& a, hipStream_t s);
 }  // namespace dv

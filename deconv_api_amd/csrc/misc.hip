@@ -3,6 +3,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace dv {
 
 // ---------------------------------------------------------------------------------------
@@ -240,6 +242,119 @@ int deprocess_mosaic_launch(const float* recon, uint8_t* out, int B, int H, int 
                             hipStream_t s) {
   if (B <= 0 || tiles <= 0 || tiles > 4) return -1;
   hipLaunchKernelGGL(deprocess_mosaic_kernel, dim3(B), dim3(1024), 0, s, recon, out, H, W, tiles, reverse);
+  return (int)hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Single-pass deprocess (same arithmetic as deprocess_mosaic_kernel) from per-image statistics
+// {sum, sum of squares} in fp64: a grid of 4-pixel quads instead of one block per image with three
+// passes. The statistics come from the final conv-down's epilogue (conv3x3_c64_stream_kernel) or
+// from recon_stats_kernel. Population variance = E[x^2] - mean^2 in fp64.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) recon_stats_kernel(const float* __restrict__ x, double* __restrict__ stats,
+                                                          long long per_group, int blocks_per_group) {
+  const int g = blockIdx.x / blocks_per_group, part = blockIdx.x % blocks_per_group;
+  const float4* src = reinterpret_cast<const float4*>(x + (long long)g * per_group);
+  const long long n4 = per_group >> 2;
+  double s1 = 0.0, s2 = 0.0;
+  for (long long i = (long long)part * 256 + threadIdx.x; i < n4; i += (long long)blocks_per_group * 256) {
+    const float4 v = src[i];
+    s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+    s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+  if (part == 0 && threadIdx.x < (per_group & 3)) {  // tail elements
+    const float v = x[(long long)g * per_group + (n4 << 2) + threadIdx.x];
+    s1 += v;
+    s2 += (double)v * v;
+  }
+  __shared__ double sh[16];
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh[wid] = s1;
+    sh[8 + wid] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0;
+    for (int w = 0; w < 4; ++w) {
+      a += sh[w];
+      b += sh[8 + w];
+    }
+    atomicAdd(stats + 2 * g, a);
+    atomicAdd(stats + 2 * g + 1, b);
+  }
+}
+
+int recon_stats_launch(const float* x, double* stats, long long per_group, int groups, hipStream_t s) {
+  if (groups <= 0 || per_group <= 0) return -1;
+  const int bpg = (int)std::min<long long>(64, (per_group / 4 + 1023) / 1024);
+  hipLaunchKernelGGL(recon_stats_kernel, dim3(groups * std::max(bpg, 1)), dim3(256), 0, s, x, stats, per_group,
+                     std::max(bpg, 1));
+  return (int)hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) deprocess_apply_kernel(const float* __restrict__ recon,
+                                                              const double* __restrict__ stats,
+                                                              uint8_t* __restrict__ out, int B, int H, int W,
+                                                              int tiles, int reverse) {
+  const int qpr = W >> 2;  // 4-pixel quads per row
+  const long long total = (long long)B * tiles * H * qpr;
+  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < total; q += (long long)gridDim.x * 256) {
+    const int xq = (int)(q % qpr);
+    long long r = q / qpr;
+    const int y = (int)(r % H);
+    r /= H;
+    const int t = (int)(r % tiles);
+    const int b = (int)(r / tiles);
+    const double cnt = (double)tiles * H * W * 3;
+    const double mean_d = stats[2 * b] / cnt;
+    const double var = fmax(stats[2 * b + 1] / cnt - mean_d * mean_d, 0.0);
+    const float mean = (float)mean_d;
+    const float denom = (float)sqrt(var) + 1e-7f;
+    const float4* src = reinterpret_cast<const float4*>(recon + ((((long long)b * tiles + t) * H + y) * W + xq * 4) * 3);
+    float v[12];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float4 f = src[k];
+      v[4 * k] = f.x;
+      v[4 * k + 1] = f.y;
+      v[4 * k + 2] = f.z;
+      v[4 * k + 3] = f.w;
+    }
+    uint8_t o[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+      float x = v[e];
+      x = x - mean;
+      x = x / denom;
+      x = x * 0.1f;
+      x = x + 0.5f;
+      x = fminf(fmaxf(x, 0.f), 1.f);
+      x = x * 255.f;
+      x = fminf(fmaxf(x, 0.f), 255.f);
+      const int px = e / 3, c = e % 3;
+      o[px * 3 + (reverse ? 2 - c : c)] = (uint8_t)x;
+    }
+    const int cols = 2, OW = W * cols;
+    const long long oy = (long long)b * ((tiles + cols - 1) / cols) * H + (t / cols) * H + y;
+    const long long ox = (long long)(t % cols) * W + xq * 4;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(out + (oy * OW + ox) * 3);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      dst[k] = (uint32_t)o[4 * k] | ((uint32_t)o[4 * k + 1] << 8) | ((uint32_t)o[4 * k + 2] << 16) |
+               ((uint32_t)o[4 * k + 3] << 24);
+  }
+}
+
+int deprocess_apply_launch(const float* recon, const double* stats, uint8_t* out, int B, int H, int W, int tiles,
+                           int reverse, hipStream_t s) {
+  if (B <= 0 || tiles <= 0 || tiles > 4 || (W & 3)) return -1;
+  const long long total = (long long)B * tiles * H * (W / 4);
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 256LL * 32);
+  hipLaunchKernelGGL(deprocess_apply_kernel, dim3(grid), dim3(256), 0, s, recon, stats, out, B, H, W, tiles, reverse);
   return (int)hipGetLastError();
 }
 

@@ -148,9 +148,11 @@ class DeconvNet:
         return S.reshape(B * K, H, W).contiguous()
 
     def backward(self, st: ForwardState, idx: torch.Tensor, mode: str = "all",
-                 batch_topk: str = "per_image", layer: Optional[str] = None) -> torch.Tensor:
+                 batch_topk: str = "per_image", layer: Optional[str] = None,
+                 stats: Optional[torch.Tensor] = None) -> torch.Tensor:
         """B*K deconv chains from ``layer`` (default: the forward target) to the input.
-        Returns fp32 reconstructions [B, K, 224, 224, 3]."""
+        Returns fp32 reconstructions [B, K, 224, 224, 3]. ``stats`` (GPU, fp64 [B, 2]) receives each
+        image's {sum, sum of squares} over its K reconstructions from the final conv's epilogue."""
         if mode not in VALID_MODES:
             raise ValueError(f"Illegal visualize mode {mode!r}; use 'all' or 'max'")
         layer = layer or st.target
@@ -220,6 +222,8 @@ class DeconvNet:
             cl = self.rt.convs[s.name]
             last = j == 1
             kw = dict(relu=True, relu_in=True, epilogue="f32" if last else "bf16", use_bias=False)
+            if last and stats is not None:
+                kw.update(stats=stats, stats_div=K)
             if pending_code is not None:
                 d = ops.conv2d(d, cl.dec, in_mode="unpool", code=pending_code, code_div=K, **kw)
                 pending_code = None
@@ -229,7 +233,10 @@ class DeconvNet:
                 recon = d
             j -= 1
         if recon is None:  # target was block1_conv1: the seed step already produced the image
-            recon = d[..., :3].float()
+            recon = d[..., :3].float().contiguous()
+            if stats is not None:  # no fp32 conv epilogue on this path: sums over each image's K maps
+                r = recon.reshape(B, -1).double()
+                stats.copy_(torch.stack([r.sum(1), (r * r).sum(1)], 1))
         return recon.reshape(B, K, *recon.shape[1:])
 
     # ------------------------------------------------------------------ one call
@@ -241,13 +248,17 @@ class DeconvNet:
             st = self.forward(x, layer)
         with tracing.range_("dv.select"):
             idx, val = self.select_filters(st.out, k, batch_topk)
+        stats = None
+        if mosaic and k == 4 and x.is_cuda and layer != "block1_conv1":  # deprocess stats from the last conv
+            stats = torch.empty(x.shape[0], 2, dtype=torch.float64, device=x.device)
         with tracing.range_("dv.backward"):
-            recon = self.backward(st, idx, mode, batch_topk)
+            recon = self.backward(st, idx, mode, batch_topk, stats=stats)
         res = DeconvResult(recon, idx, val)
         if mosaic and k == 4:
             B = recon.shape[0]
             with tracing.range_("dv.deprocess"):
-                res.mosaic = ops.deprocess_mosaic(recon.reshape(B * 4, *recon.shape[2:]).contiguous(), 4, True)
+                res.mosaic = ops.deprocess_mosaic(recon.reshape(B * 4, *recon.shape[2:]).contiguous(), 4, True,
+                                                  stats=stats)
         return res
 
 

@@ -214,7 +214,8 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
            relu_in: bool = False, in_mode: str = "plain", code: Optional[torch.Tensor] = None,
            code_div: int = 1, mask: Optional[torch.Tensor] = None, epilogue: str = "bf16",
            out: Optional[torch.Tensor] = None, accumulate: bool = False, out_hw=None,
-           use_bias: bool = True, res: Optional[torch.Tensor] = None, emask: Optional[torch.Tensor] = None):
+           use_bias: bool = True, res: Optional[torch.Tensor] = None, emask: Optional[torch.Tensor] = None,
+           stats: Optional[torch.Tensor] = None, stats_div: int = 1):
     """NHWC convolution.
 
     x: [N, H, W, C] (channel-slice views allowed: stride(3) == 1). For ``in_mode='unpool'`` x is
@@ -222,6 +223,8 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     epilogue 'pool' returns ``(pooled, code)``; otherwise the output tensor.
     ``res``: fused residual (ResNet block tail), out = [ReLU](conv + bias + res), ReLU after the add;
     ``emask`` (with ``res``): the result is zeroed where emask <= 0.
+    ``stats`` (GPU, fp32 epilogue): fp64 [N / stats_div, 2] receives {sum, sum of squares} of each
+    group of ``stats_div`` output images (the single-pass mosaic deprocess consumes it).
     """
     if pad is None:
         pad = (cw.KH // 2, cw.KW // 2)
@@ -246,7 +249,8 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     OC = cw.cout
     if x.is_cuda:
         return _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
-                           mask, epilogue, out, accumulate, use_bias, res, emask)
+                           mask, epilogue, out, accumulate, use_bias, res, emask, stats, stats_div)
+    assert stats is None, "conv2d: stats are produced by the GPU kernels only"
     return _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
                        mask, epilogue, out, accumulate, use_bias, res, emask)
 
@@ -299,7 +303,7 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
 
 
 def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
-                epilogue, out, accumulate, use_bias, res=None, emask=None):
+                epilogue, out, accumulate, use_bias, res=None, emask=None, stats=None, stats_div=1):
     lib = native.lib()
     dt = x.dtype
     assert dt in (torch.bfloat16, torch.float16) and x.stride(3) == 1, \
@@ -332,7 +336,8 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
             int(relu), int(relu_in), int(accumulate), int(code_div), x_ld, mask_ld, out_ld]
     bias = cw.bias_pad if use_bias else None
     lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
-             IMPL[_policy["impl"]] if res is None and emask is None else IMPL["dma"], res, emask)  # DMA-only epilogues
+             IMPL[_policy["impl"]] if res is None and emask is None else IMPL["dma"], res, emask,  # DMA-only epilogues
+             stats, stats_div)
     if epilogue == "pool":
         return out, out_code
     return out

@@ -3,6 +3,8 @@ standalone pool/unpool. HIP kernels for device tensors (csrc/misc.hip), PyTorch 
 from __future__ import annotations
 
 import numpy as np
+from typing import Optional
+
 import torch
 
 from . import native
@@ -86,9 +88,12 @@ def seed_deconv3x3(S: torch.Tensor, f: torch.Tensor, wt: torch.Tensor) -> torch.
     return out.to(wt.dtype)
 
 
-def deprocess_mosaic(recon: torch.Tensor, tiles: int = 4, reverse_channels: bool = True) -> torch.Tensor:
+def deprocess_mosaic(recon: torch.Tensor, tiles: int = 4, reverse_channels: bool = True,
+                     stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """recon fp32 [B*tiles, H, W, 3] -> u8 mosaic [B, 2H, 2W, 3].
 
+    ``stats`` (GPU): fp64 [B, 2] per-mosaic {sum, sum of squares} already produced by the final
+    conv (``conv2d(..., stats=...)``); without it the GPU path computes them in a separate pass.
     Mosaic [[t0, t1], [t2, t3]] (app/main.py:67-69), then Keras ``deprocess_image`` on the whole
     mosaic (app/deepdream.py:483-498), then channel reversal for an RGB encoder (OpenCV writes
     channel 0 as blue, app/main.py:73)."""
@@ -97,7 +102,7 @@ def deprocess_mosaic(recon: torch.Tensor, tiles: int = 4, reverse_channels: bool
     rows = (tiles + 1) // 2
     if recon.is_cuda:
         out = torch.empty(B, rows * H, 2 * W, 3, dtype=torch.uint8, device=recon.device)
-        native.lib().deprocess_mosaic(recon.float().contiguous(), out, tiles, reverse_channels)
+        native.lib().deprocess_mosaic(recon.float().contiguous(), out, tiles, reverse_channels, stats)
         return out
     r = recon.float().view(B, tiles, H, W, 3)
     out = torch.zeros(B, rows * H, 2 * W, 3, dtype=torch.uint8)

@@ -254,6 +254,34 @@ def test_deprocess_mosaic(native_lib):
     got = ops.deprocess_mosaic(r.to(DEV)).cpu()
     d = (got.int() - ref.int()).abs()
     assert got.shape == (2, 448, 448, 3) and d.max() <= 1 and (d > 0).float().mean() < 1e-3
+    # precomputed per-image statistics (as the final conv's epilogue supplies them) give the same mosaic
+    rd = r.to(DEV).reshape(2, -1).double()
+    st = torch.stack([rd.sum(1), (rd * rd).sum(1)], 1).contiguous()
+    got2 = ops.deprocess_mosaic(r.to(DEV), stats=st).cpu()
+    assert (got2.int() - got.int()).abs().max() <= 1
+
+
+@pytest.mark.parametrize("N,H,W,stats_div", [(8, 32, 64, 4), (4, 9, 40, 2), (8, 224, 224, 4)])
+def test_conv_stream_stats(native_lib, N, H, W, stats_div):
+    """The final 64 -> 3 conv-down's epilogue statistics (per group of stats_div images) equal the
+    fp64 sums of its own fp32 output, on the row-streaming kernel and on the generic fallback pass."""
+    from deconv_api_amd.ops import conv as Cm
+
+    g = torch.Generator().manual_seed(12)
+    x = torch.relu(torch.randn(N, H, W, 64, generator=g)).to(torch.bfloat16).to(DEV)
+    cw = _cw(3, 64, bias=False).to_device(DEV)
+    old = Cm.get_policy()
+    for impl in ("auto", "dma"):
+        Cm.set_policy(impl=impl)
+        try:
+            st = torch.full((N // stats_div, 2), 7.0, dtype=torch.float64, device=DEV)
+            y = ops.conv2d(x, cw, relu=True, relu_in=True, epilogue="f32", use_bias=False, stats=st,
+                           stats_div=stats_div)
+        finally:
+            Cm.set_policy(**old)
+        yd = y.reshape(N // stats_div, -1).double()
+        ref = torch.stack([yd.sum(1), (yd * yd).sum(1)], 1)
+        assert torch.allclose(st, ref, rtol=1e-9, atol=1e-6), impl
 
 
 def test_resize_preprocess_exact(native_lib):
