@@ -328,8 +328,11 @@ Plan make_plan(int H, int W, int quality, int segments) {
 // Entropy-coded data of MCU rows [seg*rows_per_seg, ...) (byte-stuffed, padded to a byte):
 // colour conversion of just those pixel rows, DCT, quantization and Huffman coding. DC
 // predictors start at 0, as they do after a restart marker. Compiled twice (AVX2/FMA and
-// baseline x86-64) and dispatched at load time.
+// baseline x86-64) and dispatched at load time (an ifunc; sanitizer builds, whose runtime is not up
+// when ifunc resolvers run, use the baseline version only: -DDVJPEG_NO_CLONES).
+#ifndef DVJPEG_NO_CLONES
 __attribute__((target_clones("arch=haswell", "default")))
+#endif
 void encode_segment(const Plan& p, const uint8_t* rgb, int seg, std::string& out) {
   const int H = p.H, W = p.W;
   const int r0 = seg * p.rows_per_seg, r1 = std::min(p.mcuy, r0 + p.rows_per_seg);
