@@ -191,6 +191,16 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       return;
     }
   }
+  // first layer (8-channel padded RGB image -> 64 channels): row-streaming, output-write bound
+  if (epi == dv::CONV_E_BF16 && amode == dv::CONV_A_FWD && (impl == 0 || impl == 3) && a.C == 8 &&
+      a.H * a.W >= 56 * 56 && !mask.has_value() && std::getenv("DV_NO_C8_STREAM") == nullptr) {
+    const int rc = dv::conv3x3_c8_stream_launch(a, cur_stream());
+    if (rc >= 0) {
+      check_rc(rc, "conv_c8_stream");
+      finish_stats();
+      return;
+    }
+  }
   if (impl == 3 || (impl == 0 && halo_auto)) {
     TORCH_CHECK(halo_ok, "conv: halo-tile kernel does not support this shape/mode");
     check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream(), &stats_done),

@@ -786,6 +786,145 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_pool_v3_kernel(const ConvA
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Row-streaming first layer: 3x3 conv of an 8-channel (RGB padded) image -> OC <= 64 channels,
+// bias + ReLU, bf16 out (VGG16 block1_conv1 forward). K = 9 taps x 8 channels = 72 (3 MFMA K-steps
+// of 32, taps 9..11 have zero weights). The layer is output-write bound (64 bf16 channels per pixel
+// from 3 real input channels): the input strip rows (34 px x 16 B) stream through a small LDS ring
+// (one 1 KiB LDS-DMA per row), and the MFMA is issued TRANSPOSED (A = weights, B = pixels) so each
+// lane's accumulator holds 4 consecutive channels of one pixel: the epilogue packs them into one
+// 8-B store per lane and MFMA tile, 16 pixels x 32 contiguous bytes per store instruction.
+namespace {
+constexpr int S8_W = 32;        // output px per strip
+constexpr int S8_SLOT = 1024;   // 64 px x 16 B per row slot (34 used)
+}  // namespace
+
+// FULL (H % 4 == 0, W % 32 == 0, OC == 64): every wave issues exactly 1 DMA + 8 stores per iteration,
+// so the wait counts the younger stores instead of draining them (vmcnt counts loads, stores and
+// LDS-DMA in issue order); otherwise the wait conservatively drains the previous stores too.
+template <int P, bool FULL>
+__global__ void __launch_bounds__(256) conv3x3_c8_stream_kernel(const ConvArgs a) {
+  constexpr int R = 4 * (P + 2);
+  __shared__ __attribute__((aligned(16))) uint8_t smem[R * S8_SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kq = lane >> 4, col = lane & 15;
+  const int H = a.H, W = a.W;
+  const int strips_w = (W + S8_W - 1) / S8_W;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / strips_w;
+  const int x0 = (bid - n * strips_w) * S8_W;
+
+  const long long img = (long long)H * W * a.x_ld;
+  i32x4 xr;
+  {
+    const uint64_t base = reinterpret_cast<uint64_t>(a.x + (long long)n * img);
+    xr.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)base);
+    xr.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(base >> 32) & 0xFFFFu));
+    xr.z = __builtin_amdgcn_readfirstlane((int)(img * 2 > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)(img * 2)));
+    xr.w = 0x00020000;
+  }
+  // A = weights: fragment (K-step s, 16-channel block j): lane -> channel j*16 + col, K chunk kq
+  bf16x8 wa[3][4];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      wa[s][j] = *reinterpret_cast<const bf16x8*>(a.w + (long long)(j * 16 + col) * a.Kpad + s * 32 + kq * 8);
+  float bias[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int oc = j * 16 + kq * 4 + r;
+      bias[j][r] = (a.bias && oc < a.OC) ? a.bias[oc] : 0.f;
+    }
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(wa[s][j]));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(bias[j][0]), "+v"(bias[j][1]), "+v"(bias[j][2]), "+v"(bias[j][3]));
+
+  auto issue_row = [&](int r) {  // input row r -> slot; lane = strip pixel (x0 - 1 + lane), 16 B
+    const int x = x0 - 1 + lane;
+    const bool ok = lane < S8_W + 2 && (unsigned)x < (unsigned)W && (unsigned)r < (unsigned)H;
+    const uint32_t voff = ok ? (uint32_t)((((long long)r * W + x) * a.x_ld) * 2) : 0x80000000u;
+    dma16_asm(xr, (uint32_t)(uintptr_t)(smem + ((r + 1) % R) * S8_SLOT), voff);
+  };
+#pragma unroll
+  for (int g = 0; g <= P; ++g) issue_row(4 * g - 1 + wave);
+
+  // B operand of K-step s: tap t = 4 s + kq (zero for t >= 9) at strip pixel fi*16 + col + kw
+  const int iters = (H + 3) / 4;
+  for (int i = 0; i < iters; ++i) {
+    if constexpr (FULL) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + 9 * (P - 1)) : "memory");
+    else if constexpr (P >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P - 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_row(4 * (i + P + 1) - 1 + wave);
+    const int y = 4 * i + wave;
+    if (FULL || y < H) {
+      f32x4 acc[2][4];
+#pragma unroll
+      for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[fi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int t = 4 * s + kq;
+        const int kh = t / 3, kw = t - 3 * (t / 3);
+        const bool tv = t < 9;
+#pragma unroll
+        for (int fi = 0; fi < 2; ++fi) {
+          uint4 bv = make_uint4(0, 0, 0, 0);
+          if (tv) bv = *reinterpret_cast<const uint4*>(smem + ((y + kh) % R) * S8_SLOT + (fi * 16 + col + kw) * 16);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[fi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][j], __builtin_bit_cast(bf16x8, bv), acc[fi][j],
+                                                                 0, 0, 0);
+        }
+      }
+      // C[channel][px]: lane (px = fi*16 + col, kq) holds channels j*16 + kq*4 + r, r = 0..3
+#pragma unroll
+      for (int fi = 0; fi < 2; ++fi) {
+        const int ox = x0 + fi * 16 + col;
+        if (!FULL && ox >= W) continue;
+        uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + (((long long)n * H + y) * W + ox) * a.out_ld;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int oc = j * 16 + kq * 4;
+          if (!FULL && oc >= a.OC) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = acc[fi][j][r] + bias[j][r];
+            if (a.relu) v[r] = fmaxf(v[r], 0.f);
+          }
+          *reinterpret_cast<uint2*>(orow + oc) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s) {
+  if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.C != 8 || a.x_ld != 8 || a.relu_in ||
+      a.OC > 64 || a.OCpad != 64 || a.OC % 4 != 0 || a.H != a.OH || a.W != a.OW || a.accumulate || a.mask ||
+      a.Kpad < 96 || a.out_ld % 4 != 0 || a.dtype != DT_BF16 || a.res || a.emask ||
+      (reinterpret_cast<uintptr_t>(a.out) & 7))
+    return -4;
+  const long long nwg = (long long)a.N * ((a.W + S8_W - 1) / S8_W);
+  if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
+  if (a.H % 4 == 0 && a.W % S8_W == 0 && a.OC == 64)
+    hipLaunchKernelGGL((conv3x3_c8_stream_kernel<4, true>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv3x3_c8_stream_kernel<4, false>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
 static int stream_variant() {
   static int v = [] {
     const char* e = std::getenv("DV_STREAM_P");  // measured: P=1 (3 WG/CU) 1.57 ms, P=2 1.60, P=3 1.94

@@ -108,4 +108,6 @@ int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s);
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, bool* stats_done = nullptr);
 // 3x3 conv 64 -> 64 + bias + ReLU + fused 2x2 max-pool/switch (bf16); < 0 if the shape is unsupported
 int conv3x3_pool_v3_launch(const ConvArgs& a, hipStream_t s);
+// first layer: 3x3 conv of an 8-channel image -> <= 64 channels, bias + ReLU, bf16 (< 0: unsupported)
+int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s);
 }  // namespace dv

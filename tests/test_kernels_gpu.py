@@ -130,6 +130,26 @@ def test_conv_pool_v3(native_lib, N, H, W):
     assert (gc == ic).float().mean() > 0.995
 
 
+@pytest.mark.parametrize("N,H,W,OC", [(2, 224, 224, 64), (3, 60, 70, 64), (1, 57, 33, 48)])
+def test_conv_first_layer_stream(native_lib, N, H, W, OC):
+    """8-channel (padded RGB) -> OC first-layer conv on the row-streaming kernel vs the fp32 reference
+    and vs the implicit-GEMM kernel (DV_NO_C8_STREAM)."""
+    import os
+
+    g = torch.Generator().manual_seed(43)
+    x = torch.randn(N, H, W, 8, generator=g) * 50
+    x[..., 3:] = 0
+    cw = _cw(OC, 8)
+    ref, got = _cmp_conv(x, cw, relu=True)
+    assert got.shape == ref.shape and _rel(got, ref) < 1e-2
+    os.environ["DV_NO_C8_STREAM"] = "1"
+    try:
+        alt = ops.conv2d(x.to(torch.bfloat16).to(DEV), cw.to_device(DEV), relu=True)
+    finally:
+        del os.environ["DV_NO_C8_STREAM"]
+    assert _rel(got, alt) < 1e-2
+
+
 def test_conv_unpool_gather(native_lib):
     g = torch.Generator().manual_seed(5)
     K = 2

@@ -22,6 +22,7 @@ CASES = {
     "b2c1down": (1024, 112, 112, 128, 64, False, "bf16"),
     "b4c2down": (1024, 28, 28, 512, 512, False, "bf16"),
     "b1c2fwd": (256, 224, 224, 64, 64, False, "pool"),
+    "b1c1fwd": (256, 224, 224, 8, 64, False, "bf16"),
 }
 
 
@@ -46,7 +47,7 @@ def main():
     else:
         x = torch.randn(N, H, W, C, device=dev, generator=g).to(torch.bfloat16)
         kw = {}
-    run = lambda: ops.conv2d(x, cw, relu=True, relu_in=True, epilogue=epi, use_bias=False, **kw)  # noqa: E731
+    run = lambda: ops.conv2d(x, cw, relu=True, relu_in="down" in a.case, epilogue=epi, use_bias=False, **kw)  # noqa: E731
     run()
     torch.cuda.synchronize()
     t = time.perf_counter()
