@@ -230,6 +230,21 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       a.code = nullptr;
       amode = dv::CONV_A_FWD;
     }
+    Tensor relu_x, dense_mask;
+    if (a.relu_in) {  // the DMA kernel stages A verbatim: ReLU a dense copy first (the deconvnet passes
+                      // relu_in = false for inputs that already are ReLU outputs and never takes this pass)
+      const std::vector<int64_t> sz{a.N, a.H, a.W, a.C};
+      const std::vector<int64_t> st{(int64_t)a.H * a.W * a.x_ld, (int64_t)a.W * a.x_ld, (int64_t)a.x_ld, 1};
+      relu_x = at::relu(x.as_strided(sz, st));
+      a.x = reinterpret_cast<const uint16_t*>(relu_x.data_ptr());
+      if (mask.has_value()) {  // the mask is staged with x's offsets: same dense layout
+        dense_mask = mask->as_strided(sz, st).contiguous();
+        a.mask = reinterpret_cast<const uint16_t*>(dense_mask.data_ptr());
+        a.mask_ld = a.C;
+      }
+      a.x_ld = a.C;
+      a.relu_in = 0;
+    }
     // the DMA kernel addresses A with 32-bit offsets relative to the tile's first image
     const int64_t imgs_per_tile = 512 / std::max(1, a.OH * a.OW) + 2;
     TORCH_CHECK((int64_t)a.H * a.W * a.x_ld * 2 * imgs_per_tile < 0x7FFFFFF0LL, "conv dma: image too large");

@@ -62,16 +62,22 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
                                              int lane);
 template <int DT, int NT, int BM, int BN, int FM, int FN>
 __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
-                                             int n0, int wm, int wn, int lane, int tid);
+                                             int n0, int wm, int wn, int lane, int tid, bool writer = true);
 
 // DT: 16-bit storage/MFMA dtype of x, w and a 16-bit output (DT_BF16 / DT_F16, common.h)
 // MASK: backward through a ReLU: A elements are kept only where mask (same layout and pixel
 // stride as x) is > 0. The mask tile is DMA'd into LDS next to the A tile with the same offsets
 // and applied to each A fragment in registers right before its MFMAs.
+// KS2: in-workgroup K split. Two groups of WM x WN waves share the C tile; group g computes the
+// 32-deep sub-step g of every BK=64 tile, and group 1's partial sums are added into group 0's
+// through LDS before the epilogue. Each wave then owns a (16*FM) x (16*FN) = 128 x 64 tile where
+// a plain 8-wave layout would own 64 x 64: 12 instead of 16 fragment reads per 32 MFMAs, for the
+// 128- and 64-output-channel layers whose 256 x 128 / 512 x 64 tiles are LDS-read bound.
 template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED,
-          bool MASK = false, bool FRAGPIPE = false>
-__global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a, int tiles_n) {
-  constexpr int NW = WM * WN;
+          bool MASK = false, bool FRAGPIPE = false, bool KS2 = false>
+__global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(const ConvArgs a, int tiles_n) {
+  constexpr int NW = WM * WN * (KS2 ? 2 : 1);
+  static_assert(!KS2 || (BK == 64 && !MASK), "KS2: BK=64 (one 32-deep sub-step per group), no mask");
   constexpr int BM = WM * FM * 16;
   constexpr int BN = WN * FN * 16;
   constexpr int ROWB = BK * 2;              // LDS bytes per row
@@ -91,7 +97,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
+  const int kg = KS2 ? wave / (WM * WN) : 0;  // K group (KS2)
+  const int wl = KS2 ? wave - kg * (WM * WN) : wave;
+  const int wm = wl / WN, wn = wl % WN;
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_n = wgid % tiles_n;
   const int tile_m = wgid / tiles_n;
@@ -280,6 +288,22 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
     if (kt + STAGES - 1 < nk) issue(k0 + kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const uint8_t* As = smem + cur * STAGE;
     const uint8_t* Bs = As + A_BYTES + M_BYTES;
+    if constexpr (KS2) {
+      typedef typename Vec8<DT>::type v8;
+      const int swk = ((kg * 4 + (lane >> 4)) ^ rx) << 4;
+      v8 af[FM], bf[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const v8*>(Bs + (b_row0 + j * 16) * ROWB + swk);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + swk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bf[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      continue;
+    }
     if constexpr (FRAGPIPE && !MASK) {
       // all fragments of a 32-K sub-step are read up front, and the next sub-step's reads are
       // issued before this sub-step's MFMAs (register double buffer), so LDS latency hides
@@ -330,8 +354,29 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
     }
   }
 
+  if constexpr (KS2) {  // group 1's partial sums -> group 0 (lane-linear 16-B slots, conflict-free)
+    static_assert(WM * WN * FM * FN * 64 * 16 <= STAGES * STAGE, "KS2 reduction must fit in the stages");
+    f32x4* red = reinterpret_cast<f32x4*>(smem) + (wl * FM * FN) * 64 + lane;
+    __syncthreads();  // every wave is done reading the operand stages
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) red[(i * FN + j) * 64] = acc[i][j];
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += red[(i * FN + j) * 64];
+    }
+    __syncthreads();  // the epilogue may reuse the stages
+  }
+
   // ---- epilogue ----
   if (a.ws != nullptr) {  // split-K partial: raw fp32 sums to ws[split][row][OCpad]
+    if (kg != 0) return;
     float* ws = a.ws + (long long)blockIdx.y * a.M * a.OCpad;
     const int row_l = (lane >> 4) * 4, col_l = lane & 15;
 #pragma unroll
@@ -350,10 +395,13 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a
   if constexpr (EPI == CONV_E_BF16) {
     if (a.vec_epi) {
       static_assert(BM * BN * 2 <= STAGES * STAGE, "C tile must fit in the operand stages");
-      __syncthreads();  // every wave is done reading the operand stages
-      epilogue_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+      if constexpr (!KS2) __syncthreads();  // every wave is done reading the operand stages
+      epilogue_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid, kg == 0);
       return;
     }
+  }
+  if (kg != 0) return;
+  if constexpr (EPI == CONV_E_BF16) {
     if (a.res || a.emask) {
       epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
       return;
@@ -464,13 +512,14 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
 // add), zeroed where emask <= 0. Stores of a row's last partial chunk (OC % 8) go per element.
 template <int DT, int NT, int BM, int BN, int FM, int FN>
 __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
-                                             int n0, int wm, int wn, int lane, int tid) {
+                                             int n0, int wm, int wn, int lane, int tid, bool writer) {
   constexpr int CPR = BN / 8;                       // 16-B chunks per C-tile row
   constexpr int SWZ = (CPR < 8 ? CPR : 8) - 1;
   const int row_l = (lane >> 4) * 4, col_l = lane & 15;
   const bool pre_relu = a.relu && a.res == nullptr;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
+    if (!writer) break;
     const int col = wn * FN * 16 + j * 16 + col_l;
     const int gcol = n0 + col;
     const float bias = (a.bias && gcol < a.OCpad) ? a.bias[gcol] : 0.f;
@@ -541,9 +590,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
 }
 
 template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI, bool MASK = false,
-          bool FP = false>
+          bool FP = false, bool KS2 = false>
 static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  constexpr int NT = WM * WN * (KS2 ? 128 : 64);
   const int tiles_m = (a.M + BM - 1) / BM;
   const int tiles_n = a.OCpad / BN;
   const long long nwg = (long long)tiles_m * tiles_n;
@@ -551,11 +601,11 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   const bool aligned = (a.C % BK) == 0;
   const dim3 grid((unsigned)nwg, (unsigned)(a.ws ? a.ksplit : 1));
   if (aligned)
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK, FP>), grid,
-                       dim3(WM * WN * 64), 0, s, a, tiles_n);
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK, FP, KS2>), grid,
+                       dim3(NT), 0, s, a, tiles_n);
   else
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP>), grid,
-                       dim3(WM * WN * 64), 0, s, a, tiles_n);
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP, KS2>), grid,
+                       dim3(NT), 0, s, a, tiles_n);
   return (int)hipGetLastError();
 }
 
@@ -567,6 +617,18 @@ static int dma_variant() {
   static int v = [] {
     const char* e = std::getenv("DV_DMA_VARIANT");
     return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+// DV_KS2=1 enables the in-workgroup K split (KS2) on the 256 x 128 and 512 x 64 tiles (A/B only).
+// Measured slower on every VGG16 layer it applies to (profiles/layers_r1_ks2_{off,on}.txt, e.g.
+// block2_conv2.down 0.72 -> 0.68 PF/s): these tiles are bound by the A-operand DMA stream (~9 TB/s
+// L2 -> LDS for both tile shapes), not by LDS fragment reads, so it stays off.
+static bool ks2_on() {
+  static bool v = [] {
+    const char* e = std::getenv("DV_KS2");
+    return e ? std::atoi(e) != 0 : false;
   }();
   return v;
 }
@@ -607,6 +669,7 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
       if (v == 4 && nwg(256, 128) >= cus) return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI, false, true>(a, s);
     }
     if (nwg(256, 128) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
+    if (ks2_on()) return dma_cfg<DT, 2, 2, 8, 4, 64, 3, AMODE, EPI, false, false, true>(a, s);  // 256 x 128, KS2
     return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 256 x 128
   }
   if (a.OCpad % 64 == 0 && a.OC > 16) {
@@ -615,6 +678,7 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
       if (v == 4 && nwg(512, 64) >= cus) return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI, false, true>(a, s);
     }
     if (nwg(512, 64) < cus) return dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 64
+    if (ks2_on()) return dma_cfg<DT, 4, 1, 8, 4, 64, 2, AMODE, EPI, false, false, true>(a, s);  // 512 x 64, KS2
     return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s);  // 512 x 64
   }
   if (a.OCpad % 16 == 0) {

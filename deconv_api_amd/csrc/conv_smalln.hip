@@ -803,6 +803,22 @@ constexpr int S8_SLOT = 1024;   // 64 px x 16 B per row slot (34 used)
 // FULL (H % 4 == 0, W % 32 == 0, OC == 64): every wave issues exactly 1 DMA + 8 stores per iteration,
 // so the wait counts the younger stores instead of draining them (vmcnt counts loads, stores and
 // LDS-DMA in issue order); otherwise the wait conservatively drains the previous stores too.
+// Iteration i needs row group i+1. Younger than it: the prologue's groups i+2..P and iterations
+// 0..i-1 (1 DMA + 8 stores each) while i < P, i.e. P-1+8i; in the steady state (i >= P) the stores of
+// iteration i-P and iterations i-P+1..i-1, i.e. 9P-1. The first P iterations need their own
+// (smaller) immediates: waiting with the steady-state count there does not wait at all.
+template <int P, int I = 0>
+__device__ __forceinline__ void c8_full_wait(int i) {
+  if constexpr (I >= P) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(9 * P - 1) : "memory");
+  } else {
+    if (i == I)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P - 1 + 8 * I) : "memory");
+    else
+      c8_full_wait<P, I + 1>(i);
+  }
+}
+
 template <int P, bool FULL>
 __global__ void __launch_bounds__(256) conv3x3_c8_stream_kernel(const ConvArgs a) {
   constexpr int R = 4 * (P + 2);
@@ -859,7 +875,7 @@ __global__ void __launch_bounds__(256) conv3x3_c8_stream_kernel(const ConvArgs a
   // B operand of K-step s: tap t = 4 s + kq (zero for t >= 9) at strip pixel fi*16 + col + kw
   const int iters = (H + 3) / 4;
   for (int i = 0; i < iters; ++i) {
-    if constexpr (FULL) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + 9 * (P - 1)) : "memory");
+    if constexpr (FULL) c8_full_wait<P>(i);
     else if constexpr (P >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P - 1) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();

@@ -221,11 +221,14 @@ class DeconvNet:
             assert s.kind == "conv", s
             cl = self.rt.convs[s.name]
             last = j == 1
-            kw = dict(relu=True, relu_in=True, epilogue="f32" if last else "bf16", use_bias=False)
+            kw = dict(relu=True, epilogue="f32" if last else "bf16", use_bias=False)
             if last and stats is not None:
                 kw.update(stats=stats, stats_div=K)
+            # down = ReLU(convT(ReLU(signal))) (app/deepdream.py:110,260). The input ReLU only acts on
+            # an unpooled signal (the unpool consumes it for free): every other input is already a
+            # ReLU output (seed stencil, conv-down epilogues), so relu_in would be a no-op pass
             if pending_code is not None:
-                d = ops.conv2d(d, cl.dec, in_mode="unpool", code=pending_code, code_div=K, **kw)
+                d = ops.conv2d(d, cl.dec, in_mode="unpool", code=pending_code, code_div=K, relu_in=True, **kw)
                 pending_code = None
             else:
                 d = ops.conv2d(d, cl.dec, **kw)

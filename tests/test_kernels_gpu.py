@@ -150,6 +150,49 @@ def test_conv_first_layer_stream(native_lib, N, H, W, OC):
     assert _rel(got, alt) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C,OC", [(6, 112, 112, 128, 128), (11, 112, 112, 128, 64), (5, 115, 121, 64, 128)])
+def test_conv_large_m_ks2_tiles(native_lib, conv_impl, N, H, W, C, OC):
+    """Large-M launches of the 128- and 64-output-channel layers take the in-workgroup K-split
+    (KS2) 256x128 / 512x64 tiles (>= one tile per CU): bf16 vector epilogue, unaligned row
+    stride (per-element epilogue), f32 epilogue, fused pool+switch and the transposed dgrad."""
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(N, H, W, C, generator=g)
+    cw = _cw(OC, C)
+    ref, got = _cmp_conv(x, cw, relu=True)
+    assert got.shape == ref.shape and _rel(got, ref) < 1e-2
+    ref, got = _cmp_conv(x, cw, relu=False, epilogue="f32")
+    assert _rel(got, ref) < 1e-3
+    if H % 2 == 0 and W % 2 == 0:
+        (rp, _), (gp, _) = _cmp_conv(x, cw, epilogue="pool")
+        assert _rel(gp, rp) < 1e-2
+    ct = _cw(C, OC, kind="transpose", bias=False)  # input gradient of a forward conv OC -> C
+    kw = dict(relu=True, in_mode="transpose", stride=1, pad=(1, 1), out_hw=(H, W), use_bias=False)
+    ref = ops.conv2d(_bf(x), ct, **kw)
+    got = ops.conv2d(x.to(torch.bfloat16).to(DEV), ct.to_device(DEV), **kw)
+    assert got.shape == ref.shape and _rel(got, ref) < 1e-2
+
+
+def test_conv_relu_in_every_kernel(native_lib, conv_impl):
+    """relu_in (ReLU on the input) on signed inputs: the LDS-DMA kernel stages A verbatim, so the
+    binding ReLUs a dense copy; plain, channel-slice view, transposed and masked inputs."""
+    g = torch.Generator().manual_seed(23)
+    full = torch.randn(2, 12, 14, 192, generator=g)
+    cw = _cw(128, 128)
+    fd = full.to(torch.bfloat16).to(DEV)
+    for lo in (0, 32):
+        xd = fd[..., lo:lo + 128]  # channel-slice view (x_ld = 192)
+        ref = ops.conv2d(_bf(full[..., lo:lo + 128]), cw, relu=True, relu_in=True)
+        got = ops.conv2d(xd, cw.to_device(DEV), relu=True, relu_in=True)
+        assert _rel(got, ref) < 1e-2
+    x = full[..., :128].contiguous()
+    mask = torch.randn(2, 12, 14, 128, generator=g)
+    ct = _cw(128, 64, kind="transpose", bias=False)
+    kw = dict(relu=False, relu_in=True, in_mode="transpose", stride=1, pad=(1, 1), out_hw=(12, 14), use_bias=False)
+    ref = ops.conv2d(_bf(x), ct, mask=_bf(mask), **kw)
+    got = ops.conv2d(x.to(torch.bfloat16).to(DEV), ct.to_device(DEV), mask=mask.to(torch.bfloat16).to(DEV), **kw)
+    assert _rel(got, ref) < 1e-2
+
+
 def test_conv_unpool_gather(native_lib):
     g = torch.Generator().manual_seed(5)
     K = 2

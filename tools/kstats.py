@@ -24,6 +24,7 @@ def main(argv=None):
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--last-frac", type=float, default=1.0,
                     help="only dispatches in the last fraction of the trace's GPU time span")
+    ap.add_argument("--gaps", action="store_true", help="also report idle gaps between dispatches")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels").fetchall()
@@ -47,6 +48,36 @@ def main(argv=None):
     print(f"{'total_ms':>9} {'%':>5} {'calls':>7} {'avg_us':>8}  kernel")
     for name, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
         print(f"{us / 1e3:9.2f} {100 * us / busy:5.1f} {n:7d} {us / n:8.1f}  {name}")
+    if a.gaps:
+        gaps(rows, cut, a.top)
+
+
+def gaps(rows, cut, top):
+    """Idle time between consecutive dispatches (GPU timeline, single queue assumed): a histogram
+    and the kernels that the largest idle totals FOLLOW (host syncs / launch-bound stretches)."""
+    ev = sorted((s, e, short(n)) for n, s, e, _, _ in rows if s >= cut)
+    hist = defaultdict(lambda: [0, 0.0])
+    after = defaultdict(lambda: [0, 0.0])
+    edges = (2, 5, 10, 20, 50, 100, 1000, float("inf"))
+    end = ev[0][1] if ev else 0
+    prev = ev[0][2] if ev else ""
+    for s, e, n in ev[1:]:
+        g = (s - end) / 1e3  # us
+        if g > 0:
+            b = next(x for x in edges if g <= x)
+            hist[b][0] += 1
+            hist[b][1] += g
+            after[prev][0] += 1
+            after[prev][1] += g
+        if e >= end:
+            end, prev = e, n
+    print("idle gaps (us bucket <=: count, total ms)")
+    for b in edges:
+        if b in hist:
+            print(f"  <= {b:>6}: {hist[b][0]:7d} {hist[b][1] / 1e3:9.2f}")
+    print(f"{'idle_ms':>9} {'gaps':>7} {'avg_us':>8}  preceding kernel")
+    for name, (n, us) in sorted(after.items(), key=lambda kv: -kv[1][1])[:top]:
+        print(f"{us / 1e3:9.2f} {n:7d} {us / n:8.1f}  {name}")
 
 
 if __name__ == "__main__":
