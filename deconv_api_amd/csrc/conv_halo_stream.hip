@@ -1,0 +1,248 @@
+// Halo-stream 3x3 conv for gfx950 (MI355X): 3x3 / stride 1 / pad 1, C % 32 == 0, 64 or 128 output
+// channels, 16-bit in/out, fp32 accumulation. Targets the 112x112 layers of VGG16 whose implicit-GEMM
+// launches are bound by the A-operand LDS-DMA stream (block2 forward and conv-downs at B*K = 1024):
+// the implicit GEMM re-fetches every input pixel once per tap (9x) from L2, this kernel once.
+//
+// Work decomposition: one 512-thread workgroup per 16 x 32 output tile (512 pixels) x all output
+// channels. K runs as (32-channel chunk c, tap t): the (16+2) x (32+2) input halo of chunk c is staged
+// ONCE into LDS and serves all 9 taps (each tap reads a shifted window of it); the weights of one
+// (chunk, tap) step (OC x 32 channels) stream through a 3-slot LDS ring. Both are staged by LDS-DMA
+// (`buffer_load_dwordx4 ... lds`), with conv zero padding / the image border from the buffer range
+// check (an out-of-range offset reads 0).
+//
+// MFMA `v_mfma_f32_32x32x16_*` transposed: A = weights (32 output channels x 16 K), B = pixels (16 K x
+// 32 pixels of one tile row), so C holds 4 consecutive output channels of one pixel per register
+// quad and the epilogue packs them into one 8-B store per lane (lanes h = 0/1 cover 16 contiguous B).
+//
+// LDS layouts: a halo pixel and a weight row both hold 32 channels (64 B) in an 80-B slot (5 bank
+// slots of 16 B): the 32 rows a fragment read touches start at 5j mod 16 = a permutation of the 16 slots
+// for every ds_read_b128 lane group ({0-3,12-15,20-27} etc.) and any base -> conflict-free for every
+// tap shift. The DMA destination stays lane-linear (1 KiB per wave instruction); the per-lane SOURCE
+// maps slot s -> (pixel s/5, chunk s%5), chunk 4 is the pad (reads out of range -> 0).
+//
+// Pipeline per step k = 9c + t (one barrier per step): wait until this wave's DMA of B(k) landed
+// (counted vmcnt: every wave issues the same number of DMAs per step, dummy out-of-range ones pad the
+// count), barrier, issue [halo(c+1) if t == 0] + B(k+2), then 2 x (FN + 2) fragment reads and 4 FN MFMAs.
+#include "common.h"
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace dv {
+
+namespace {
+
+constexpr int HS_TH = 16, HS_TW = 32;                 // output tile
+constexpr int HS_HH = HS_TH + 2, HS_HW = HS_TW + 2;   // 18 x 34 halo
+constexpr int HS_PS = 80;                              // bytes per halo pixel / weight row slot
+constexpr int HS_HSLOTS = HS_HH * HS_HW * 5;           // 3060 16-B slots
+constexpr int HS_HI = (HS_HSLOTS + 511) / 512;         // halo DMA instructions per wave (6)
+constexpr int HS_HBUF = HS_HI * 8 * 1024;              // 49152 B per halo buffer (incl. overrun of the last)
+constexpr uint32_t HS_OOB = 0x80000000u;
+
+typedef int hs_i32x4 __attribute__((ext_vector_type(4)));
+
+// LDS-DMA of 16 B per lane as inline asm (as conv_smalln.hip's dma16_asm): with the intrinsic the
+// compiler's waitcnt pass drains the prefetch (vmcnt(0)) before ds_reads that reuse the offset VGPR;
+// here the only waits are the kernel's counted ones. M0 = LDS base of the 64 x 16 B destination.
+__device__ __forceinline__ void hs_dma16(const hs_i32x4& rsrc, const uint8_t* lds_dst, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_dst)), "v"(voff), "s"(rsrc)
+               : "memory");
+}
+
+__device__ __forceinline__ hs_i32x4 hs_rsrc(const void* base, long long bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  hs_i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(b >> 32) & 0xFFFFu));
+  r.z = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)bytes));
+  r.w = 0x00020000;
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void hs_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+template <int DT>
+__device__ __forceinline__ f32x16 hs_mfma(const typename Vec8<DT>::type& a, const typename Vec8<DT>::type& b,
+                                          const f32x16& c) {
+  if constexpr (DT == DT_BF16) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+}  // namespace
+
+// OCT: output channels per workgroup (= OCpad, 64 or 128)
+template <int DT, int OCT>
+__global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+  constexpr int FN = OCT / 32;                    // 32-channel A blocks per wave
+  constexpr int BI = (OCT * 5 + 511) / 512;       // weight DMA instructions per wave and step (2 / 1)
+  constexpr int BSLOT = BI * 8 * 1024;            // ring slot bytes (incl. the dummy instructions' bytes)
+  constexpr int STEPS_PER_CHUNK = 9;
+  typedef typename Vec8<DT>::type v8;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * HS_HBUF + 3 * BSLOT];
+  uint8_t* halo = smem;
+  uint8_t* ring = smem + 2 * HS_HBUF;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, px = lane & 31;
+  const int H = a.H, W = a.W, C = a.C;
+  const int per_img = tiles_x * tiles_y;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / per_img;
+  const int tr = bid - n * per_img;
+  const int ty0 = (tr / tiles_x) * HS_TH, tx0 = (tr % tiles_x) * HS_TW;
+
+  const long long img = (long long)H * W * a.x_ld;
+  const hs_i32x4 xr = hs_rsrc(a.x + (long long)n * img, img * 2);
+  const hs_i32x4 wr = hs_rsrc(a.w, (long long)a.OCpad * a.Kpad * 2);
+
+  // per-lane DMA source offsets (chunk 0 / tap 0); slot s of instruction m -> (row s/5, 16-B chunk s%5)
+  uint32_t hoff[HS_HI];
+#pragma unroll
+  for (int u = 0; u < HS_HI; ++u) {
+    const int s = (u * 8 + wave) * 64 + lane;
+    const int p = s / 5, q = s - 5 * (s / 5);
+    const int hy = p / HS_HW, hx = p - HS_HW * (p / HS_HW);
+    const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+    const bool ok = q < 4 && p < HS_HH * HS_HW && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    hoff[u] = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + q * 8) * 2) : HS_OOB;
+  }
+  uint32_t woff[BI];
+#pragma unroll
+  for (int u = 0; u < BI; ++u) {
+    const int s = (u * 8 + wave) * 64 + lane;
+    const int r = s / 5, q = s - 5 * (s / 5);
+    woff[u] = (q < 4 && r < OCT) ? (uint32_t)(((long long)r * a.Kpad + q * 8) * 2) : HS_OOB;
+  }
+  const int nch = C / 32;
+  const int nsteps = nch * STEPS_PER_CHUNK;
+  auto issue_halo = [&](int c, int buf) {  // c >= nch: dummy (out-of-range) loads keep the count uniform
+    const uint32_t add = c < nch ? (uint32_t)(c * 64) : HS_OOB;  // chunk c: channels 32c.. (64 B)
+#pragma unroll
+    for (int u = 0; u < HS_HI; ++u)
+      hs_dma16(xr, halo + buf * HS_HBUF + (u * 8 + wave) * 1024,
+               hoff[u] == HS_OOB || add == HS_OOB ? HS_OOB : hoff[u] + add);
+  };
+  auto issue_w = [&](int k) {  // weights of step k = 9c + t: K columns t*C + 32c .. +32
+    const int c = k / STEPS_PER_CHUNK, t = k - STEPS_PER_CHUNK * (k / STEPS_PER_CHUNK);
+    const uint32_t add = k < nsteps ? (uint32_t)((t * C + c * 32) * 2) : HS_OOB;
+    uint8_t* dst = ring + (k % 3) * BSLOT;
+#pragma unroll
+    for (int u = 0; u < BI; ++u)
+      hs_dma16(wr, dst + (u * 8 + wave) * 1024, woff[u] == HS_OOB || add == HS_OOB ? HS_OOB : woff[u] + add);
+  };
+
+  f32x16 acc[2][FN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // fragment read bases: weights row 32j + px, pixel (tile row 2*wave + i, column px), chunk 2s + h
+  const int wrow = px * HS_PS + h * 16;
+  const int prow = ((2 * wave) * HS_HW + px) * HS_PS + h * 16;
+
+  issue_halo(0, 0);
+  issue_w(0);
+  issue_w(1);
+  for (int c = 0; c < nch; ++c) {
+    const uint8_t* hb = halo + (c & 1) * HS_HBUF + prow;
+#pragma unroll
+    for (int t = 0; t < STEPS_PER_CHUNK; ++t) {
+      const int k = c * STEPS_PER_CHUNK + t;
+      // younger than B(k): everything step k-1 issued (the prologue's B(1) for k = 0)
+      if (t == 1) hs_wait<HS_HI + BI>();
+      else hs_wait<BI>();
+      __builtin_amdgcn_s_barrier();
+      if (t == 0) issue_halo(c + 1, (c + 1) & 1);
+      issue_w(k + 2);
+      const uint8_t* wb = ring + (k % 3) * BSLOT + wrow;
+      const int kh = t / 3, kw = t % 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        v8 wf[FN], pf[2];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) wf[j] = *reinterpret_cast<const v8*>(wb + j * 32 * HS_PS + s * 32);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          pf[i] = *reinterpret_cast<const v8*>(hb + ((i + kh) * HS_HW + kw) * HS_PS + s * 32);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = hs_mfma<DT>(wf[j], pf[i], acc[i][j]);
+      }
+    }
+  }
+  hs_wait<0>();  // the dummy DMAs of the last steps land before the workgroup retires
+
+  // epilogue: lane = pixel (tile row 2*wave + i, column px); register r of block j = output channel
+  // 32j + 8(r >> 2) + 4h + (r & 3): 4 consecutive channels -> one 8-B store
+  const int ox = tx0 + px;
+  if (ox >= W) return;
+  // the lane's bias values (the same for both pixel rows), all loads in flight together
+  float4 bv[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      bv[j][g] = a.bias ? *reinterpret_cast<const float4*>(a.bias + 32 * j + 8 * g + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float lo = a.relu ? 0.f : -INFINITY;
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oy = ty0 + 2 * wave + i;
+    if (oy >= H) continue;
+    uint16_t* orow = out + (((long long)n * H + oy) * W + ox) * a.out_ld;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int oc = 32 * j + 8 * g + 4 * h;
+        const float v0 = fmaxf(acc[i][j][4 * g + 0] + bv[j][g].x, lo);
+        const float v1 = fmaxf(acc[i][j][4 * g + 1] + bv[j][g].y, lo);
+        const float v2 = fmaxf(acc[i][j][4 * g + 2] + bv[j][g].z, lo);
+        const float v3 = fmaxf(acc[i][j][4 * g + 3] + bv[j][g].w, lo);
+        if (oc + 4 <= a.OC) {
+          *reinterpret_cast<uint2*>(orow + oc) = make_uint2(pack2<DT>(v0, v1), pack2<DT>(v2, v3));
+        } else if (oc < a.OC) {  // OC % 4 tail (never for VGG16)
+          const float v[4] = {v0, v1, v2, v3};
+          for (int r = 0; r < a.OC - oc; ++r) orow[oc + r] = from_f<DT>(v[r]);
+        }
+      }
+  }
+}
+
+int conv3x3_hs_launch(const ConvArgs& a, hipStream_t s) {
+  if (std::getenv("DV_NO_HS") != nullptr) return -4;
+  if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH || a.W != a.OW ||
+      a.C % 32 != 0 || a.x_ld % 8 != 0 || (a.OCpad != 64 && a.OCpad != 128) || a.relu_in || a.accumulate ||
+      a.mask || a.code || a.res || a.emask || a.ws || a.stats || a.out_ld % 4 != 0 ||
+      (reinterpret_cast<uintptr_t>(a.out) & 7) || (reinterpret_cast<uintptr_t>(a.x) & 15) ||
+      (reinterpret_cast<uintptr_t>(a.bias) & 15) ||
+      (long long)a.Kpad < 9LL * a.C || (long long)a.H * a.W * a.x_ld * 2 > 0x7FFFFFF0LL)
+    return -4;
+  const int tx = (a.W + HS_TW - 1) / HS_TW, ty = (a.H + HS_TH - 1) / HS_TH;
+  const long long nwg = (long long)a.N * tx * ty;
+  if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
+  const dim3 grid((unsigned)nwg), block(512);
+  if (a.dtype == DT_F16) {
+    if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs_kernel<DT_F16, 128>), grid, block, 0, s, a, tx, ty);
+    else hipLaunchKernelGGL((conv3x3_hs_kernel<DT_F16, 64>), grid, block, 0, s, a, tx, ty);
+  } else {
+    if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs_kernel<DT_BF16, 128>), grid, block, 0, s, a, tx, ty);
+    else hipLaunchKernelGGL((conv3x3_hs_kernel<DT_BF16, 64>), grid, block, 0, s, a, tx, ty);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace dv

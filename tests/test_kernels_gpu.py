@@ -172,6 +172,30 @@ def test_conv_large_m_ks2_tiles(native_lib, conv_impl, N, H, W, C, OC):
     assert got.shape == ref.shape and _rel(got, ref) < 1e-2
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,W,C,OC,bias,relu", [(2, 112, 112, 128, 128, False, True), (2, 112, 112, 128, 64, False, True),
+                                                   (1, 112, 112, 64, 128, True, True), (1, 70, 100, 96, 128, True, False),
+                                                   (3, 64, 77, 32, 64, True, True), (1, 65, 64, 256, 120, True, True)])
+def test_conv_halo_stream(native_lib, dt, N, H, W, C, OC, bias, relu):
+    """Halo-stream kernel (3x3 s1 p1, C % 32 == 0, OCpad 64/128, >= 64x64 maps; auto policy) vs the
+    fp32 reference and vs the implicit-GEMM path (DV_NO_HS): ragged tiles, OC < OCpad, no-bias, fp16."""
+    import os
+
+    g = torch.Generator().manual_seed(29)
+    x = torch.randn(N, H, W, C, generator=g)
+    cw = _cw(OC, C, bias=bias)
+    xd = x.to(dt).to(DEV)
+    ref = ops.conv2d(x.to(dt).float(), cw, relu=relu, use_bias=bias)
+    got = ops.conv2d(xd, cw.to_device(DEV, dt), relu=relu, use_bias=bias)
+    assert got.shape == ref.shape and got.dtype == dt and _rel(got, ref) < 1e-2
+    os.environ["DV_NO_HS"] = "1"
+    try:
+        alt = ops.conv2d(xd, cw.to_device(DEV, dt), relu=relu, use_bias=bias)
+    finally:
+        del os.environ["DV_NO_HS"]
+    assert _rel(got, alt) < 1e-2
+
+
 def test_conv_relu_in_every_kernel(native_lib, conv_impl):
     """relu_in (ReLU on the input) on signed inputs: the LDS-DMA kernel stages A verbatim, so the
     binding ReLUs a dense copy; plain, channel-slice view, transposed and masked inputs."""
