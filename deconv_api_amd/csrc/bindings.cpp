@@ -247,9 +247,9 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     }
     // 3x3 s1 p1 convs with 64/128 output channels at large maps: halo-stream kernel (every input
     // pixel fetched once per 32-channel chunk instead of once per tap)
-    if (impl == 0 && amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16 && !mask.has_value() && !a.res &&
-        !a.emask && !a.accumulate && (int64_t)a.H * a.W >= 64 * 64 && a.W >= 64) {
-      const int rc = dv::conv3x3_hs_launch(a, cur_stream());
+    if (impl == 0 && amode == dv::CONV_A_FWD && (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_POOL) &&
+        !mask.has_value() && !a.res && !a.emask && !a.accumulate && (int64_t)a.H * a.W >= 64 * 64 && a.W >= 64) {
+      const int rc = dv::conv3x3_hs_launch(a, (int)epi, cur_stream());
       if (rc >= 0) {
         check_rc(rc, "conv_halo_stream");
         finish_stats();

@@ -22,7 +22,9 @@
 //
 // Pipeline per step k = 9c + t (one barrier per step): wait until this wave's DMA of B(k) landed
 // (counted vmcnt: every wave issues the same number of DMAs per step, dummy out-of-range ones pad the
-// count), barrier, issue [halo(c+1) if t == 0] + B(k+2), then 2 x (FN + 2) fragment reads and 4 FN MFMAs.
+// count), barrier, issue [halo(c+1) if t == 0] + B(k+RING-1) (4-5 steps of weight prefetch: one step is
+// only ~0.25-0.5 us of MFMA work, less than an L2 round trip), then 2 x (FN + 2) fragment reads and
+// 4 FN MFMAs.
 #include "common.h"
 #include "kernels.h"
 
@@ -47,6 +49,13 @@ typedef int hs_i32x4 __attribute__((ext_vector_type(4)));
 // here the only waits are the kernel's counted ones. M0 = LDS base of the 64 x 16 B destination.
 __device__ __forceinline__ void hs_dma16(const hs_i32x4& rsrc, const uint8_t* lds_dst, uint32_t voff) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_dst)), "v"(voff), "s"(rsrc)
+               : "memory");
+}
+
+__device__ __forceinline__ void hs_dma4(const hs_i32x4& rsrc, const uint8_t* lds_dst, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
                :
                : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_dst)), "v"(voff), "s"(rsrc)
                : "memory");
@@ -78,15 +87,18 @@ __device__ __forceinline__ f32x16 hs_mfma(const typename Vec8<DT>::type& a, cons
 
 }  // namespace
 
-// OCT: output channels per workgroup (= OCpad, 64 or 128)
-template <int DT, int OCT>
+// OCT: output channels per workgroup (= OCpad, 64 or 128); POOL: fused 2x2 max-pool + switch epilogue
+template <int DT, int OCT, bool POOL, int RING>
 __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
-  constexpr int FN = OCT / 32;                    // 32-channel A blocks per wave
-  constexpr int BI = (OCT * 5 + 511) / 512;       // weight DMA instructions per wave and step (2 / 1)
-  constexpr int BSLOT = BI * 8 * 1024;            // ring slot bytes (incl. the dummy instructions' bytes)
+  constexpr int FN = OCT / 32;  // 32-channel A blocks per wave
+  // weights of one step: OCT rows x 80 B. OCT = 128: 10 KiB = one 1-KiB dwordx4 DMA + one 256-B dword
+  // DMA per wave (exact); OCT = 64: 5 KiB in one dwordx4 DMA per wave, 3 of them out-of-range dummies
+  constexpr int BI = OCT == 128 ? 2 : 1;          // weight DMA instructions per wave and step
+  constexpr int BSLOT = OCT == 128 ? 10240 : 8192;
+  constexpr int LA = RING - 1;                    // B(k + RING - 1) is issued at step k
   constexpr int STEPS_PER_CHUNK = 9;
   typedef typename Vec8<DT>::type v8;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * HS_HBUF + 3 * BSLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * HS_HBUF + RING * BSLOT];
   uint8_t* halo = smem;
   uint8_t* ring = smem + 2 * HS_HBUF;
 
@@ -116,11 +128,15 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
     hoff[u] = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + q * 8) * 2) : HS_OOB;
   }
   uint32_t woff[BI];
-#pragma unroll
-  for (int u = 0; u < BI; ++u) {
-    const int s = (u * 8 + wave) * 64 + lane;
+  {
+    const int s = wave * 64 + lane;  // dwordx4 part: 16-B slot s of the ring slot
     const int r = s / 5, q = s - 5 * (s / 5);
-    woff[u] = (q < 4 && r < OCT) ? (uint32_t)(((long long)r * a.Kpad + q * 8) * 2) : HS_OOB;
+    woff[0] = (q < 4 && r < OCT) ? (uint32_t)(((long long)r * a.Kpad + q * 8) * 2) : HS_OOB;
+    if constexpr (BI == 2) {  // dword part: bytes 8192 + 256 wave + 4 lane
+      const int s2 = 512 + wave * 16 + (lane >> 2), d = lane & 3;
+      const int r2 = s2 / 5, q2 = s2 - 5 * (s2 / 5);
+      woff[BI - 1] = q2 < 4 ? (uint32_t)(((long long)r2 * a.Kpad + q2 * 8) * 2 + d * 4) : HS_OOB;
+    }
   }
   const int nch = C / 32;
   const int nsteps = nch * STEPS_PER_CHUNK;
@@ -134,10 +150,10 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
   auto issue_w = [&](int k) {  // weights of step k = 9c + t: K columns t*C + 32c .. +32
     const int c = k / STEPS_PER_CHUNK, t = k - STEPS_PER_CHUNK * (k / STEPS_PER_CHUNK);
     const uint32_t add = k < nsteps ? (uint32_t)((t * C + c * 32) * 2) : HS_OOB;
-    uint8_t* dst = ring + (k % 3) * BSLOT;
-#pragma unroll
-    for (int u = 0; u < BI; ++u)
-      hs_dma16(wr, dst + (u * 8 + wave) * 1024, woff[u] == HS_OOB || add == HS_OOB ? HS_OOB : woff[u] + add);
+    uint8_t* dst = ring + (k % RING) * BSLOT;
+    hs_dma16(wr, dst + wave * 1024, woff[0] == HS_OOB || add == HS_OOB ? HS_OOB : woff[0] + add);
+    if constexpr (BI == 2)
+      hs_dma4(wr, dst + 8192 + wave * 256, woff[1] == HS_OOB || add == HS_OOB ? HS_OOB : woff[1] + add);
   };
 
   f32x16 acc[2][FN];
@@ -153,20 +169,21 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
   const int prow = ((2 * wave) * HS_HW + px) * HS_PS + h * 16;
 
   issue_halo(0, 0);
-  issue_w(0);
-  issue_w(1);
+#pragma unroll
+  for (int p = 0; p < LA; ++p) issue_w(p);
   for (int c = 0; c < nch; ++c) {
     const uint8_t* hb = halo + (c & 1) * HS_HBUF + prow;
 #pragma unroll
     for (int t = 0; t < STEPS_PER_CHUNK; ++t) {
       const int k = c * STEPS_PER_CHUNK + t;
-      // younger than B(k): everything step k-1 issued (the prologue's B(1) for k = 0)
-      if (t == 1) hs_wait<HS_HI + BI>();
-      else hs_wait<BI>();
+      // younger than B(k): the B's of steps k-LA+1 .. k-1 (or of the prologue), plus halo(c) when
+      // step 9c lies in that window (1 <= t <= LA-1)
+      if (t >= 1 && t <= LA - 1) hs_wait<(LA - 1) * BI + HS_HI>();
+      else hs_wait<(LA - 1) * BI>();
       __builtin_amdgcn_s_barrier();
       if (t == 0) issue_halo(c + 1, (c + 1) & 1);
-      issue_w(k + 2);
-      const uint8_t* wb = ring + (k % 3) * BSLOT + wrow;
+      issue_w(k + LA);
+      const uint8_t* wb = ring + (k % RING) * BSLOT + wrow;
       const int kh = t / 3, kw = t % 3;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -198,6 +215,55 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
       bv[j][g] = a.bias ? *reinterpret_cast<const float4*>(a.bias + 32 * j + 8 * g + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
   const float lo = a.relu ? 0.f : -INFINITY;
   uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+  if constexpr (POOL) {
+    // fused 2x2/s2 max-pool + first-max (row-major) switch code: the lane holds both window rows
+    // (i = 0, 1) of its column; the odd column comes from lane ^ 1 (DPP quad_perm [1,0,3,2]).
+    // Values are compared at storage precision (like the CPU reference and the DMA kernel's epilogue).
+    const int PH = H >> 1, PW = W >> 1;
+    const long long prow = ((long long)n * PH + (ty0 >> 1) + wave) * PW + (ox >> 1);
+    const bool st = (px & 1) == 0 && ty0 + 2 * wave < H;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int oc = 32 * j + 8 * g + 4 * h;
+        const float b4[4] = {bv[j][g].x, bv[j][g].y, bv[j][g].z, bv[j][g].w};
+        float best[4];
+        uint32_t codes = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float w4[4];  // window order (dy, dx) = (0,0), (0,1), (1,0), (1,1)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const float v = to_f<DT>(from_f<DT>(fmaxf(acc[i][j][4 * g + r] + b4[r], lo)));
+            const float pv = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+            w4[2 * i] = v;
+            w4[2 * i + 1] = pv;
+          }
+          float m = w4[0];
+          uint32_t c = 0;
+#pragma unroll
+          for (int q = 1; q < 4; ++q)
+            if (w4[q] > m) {
+              m = w4[q];
+              c = q;
+            }
+          best[r] = m;
+          codes |= c << (8 * r);
+        }
+        if (st && oc + 4 <= a.OC) {
+          *reinterpret_cast<uint2*>(out + prow * a.out_ld + oc) =
+              make_uint2(pack2<DT>(best[0], best[1]), pack2<DT>(best[2], best[3]));
+          *reinterpret_cast<uint32_t*>(a.out_code + prow * a.OC + oc) = codes;
+        } else if (st && oc < a.OC) {
+          for (int r = 0; r < a.OC - oc; ++r) {
+            out[prow * a.out_ld + oc + r] = from_f<DT>(best[r]);
+            a.out_code[prow * a.OC + oc + r] = (uint8_t)(codes >> (8 * r));
+          }
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int oy = ty0 + 2 * wave + i;
@@ -222,7 +288,27 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
   }
 }
 
-int conv3x3_hs_launch(const ConvArgs& a, hipStream_t s) {
+// weight ring depth (slots; B(k + ring - 1) is prefetched at step k). DV_HS_RING = 3 / 4 / 5 (A/B)
+static int hs_ring() {
+  static int v = [] {
+    const char* e = std::getenv("DV_HS_RING");
+    const int r = e ? std::atoi(e) : 3;
+    return r == 4 || r == 5 ? r : 3;
+  }();
+  return v;
+}
+
+#define HS_LAUNCH(DT_, OCT_, POOL_)                                                                    \
+  do {                                                                                                 \
+    if (ring == 5)                                                                                     \
+      hipLaunchKernelGGL((conv3x3_hs_kernel<DT_, OCT_, POOL_, 5>), grid, block, 0, s, a, tx, ty);      \
+    else if (ring == 4)                                                                                \
+      hipLaunchKernelGGL((conv3x3_hs_kernel<DT_, OCT_, POOL_, 4>), grid, block, 0, s, a, tx, ty);      \
+    else                                                                                               \
+      hipLaunchKernelGGL((conv3x3_hs_kernel<DT_, OCT_, POOL_, 3>), grid, block, 0, s, a, tx, ty);      \
+  } while (0)
+
+int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
   if (std::getenv("DV_NO_HS") != nullptr) return -4;
   if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH || a.W != a.OW ||
       a.C % 32 != 0 || a.x_ld % 8 != 0 || (a.OCpad != 64 && a.OCpad != 128) || a.relu_in || a.accumulate ||
@@ -231,16 +317,25 @@ int conv3x3_hs_launch(const ConvArgs& a, hipStream_t s) {
       (reinterpret_cast<uintptr_t>(a.bias) & 15) ||
       (long long)a.Kpad < 9LL * a.C || (long long)a.H * a.W * a.x_ld * 2 > 0x7FFFFFF0LL)
     return -4;
+  const bool pool = epi == CONV_E_POOL;
+  if (!pool && epi != CONV_E_BF16) return -4;
+  if (pool && (a.H % 2 || a.W % 2 || a.out_code == nullptr || a.OC % 4 || a.dtype != DT_BF16 ||
+               (reinterpret_cast<uintptr_t>(a.out_code) & 3)))
+    return -4;
   const int tx = (a.W + HS_TW - 1) / HS_TW, ty = (a.H + HS_TH - 1) / HS_TH;
   const long long nwg = (long long)a.N * tx * ty;
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
   const dim3 grid((unsigned)nwg), block(512);
-  if (a.dtype == DT_F16) {
-    if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs_kernel<DT_F16, 128>), grid, block, 0, s, a, tx, ty);
-    else hipLaunchKernelGGL((conv3x3_hs_kernel<DT_F16, 64>), grid, block, 0, s, a, tx, ty);
+  const int ring = hs_ring();
+  if (pool) {
+    if (a.OCpad == 128) HS_LAUNCH(DT_BF16, 128, true);
+    else HS_LAUNCH(DT_BF16, 64, true);
+  } else if (a.dtype == DT_F16) {
+    if (a.OCpad == 128) HS_LAUNCH(DT_F16, 128, false);
+    else HS_LAUNCH(DT_F16, 64, false);
   } else {
-    if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs_kernel<DT_BF16, 128>), grid, block, 0, s, a, tx, ty);
-    else hipLaunchKernelGGL((conv3x3_hs_kernel<DT_BF16, 64>), grid, block, 0, s, a, tx, ty);
+    if (a.OCpad == 128) HS_LAUNCH(DT_BF16, 128, false);
+    else HS_LAUNCH(DT_BF16, 64, false);
   }
   return (int)hipGetLastError();
 }

@@ -110,6 +110,7 @@ int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, b
 int conv3x3_pool_v3_launch(const ConvArgs& a, hipStream_t s);
 // first layer: 3x3 conv of an 8-channel image -> <= 64 channels, bias + ReLU, bf16 (< 0: unsupported)
 int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s);
-// halo-stream 3x3 s1 p1 conv, C % 32 == 0 -> OCpad 64 / 128, 16-bit out (< 0: unsupported)
-int conv3x3_hs_launch(const ConvArgs& a, hipStream_t s);
+// halo-stream 3x3 s1 p1 conv, C % 32 == 0 -> OCpad 64 / 128, 16-bit out or fused 2x2 max-pool +
+// switch (epi CONV_E_BF16 / CONV_E_POOL; < 0: unsupported)
+int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s);
 }  // namespace dv

@@ -196,6 +196,22 @@ def test_conv_halo_stream(native_lib, dt, N, H, W, C, OC, bias, relu):
     assert _rel(got, alt) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C,OC", [(2, 112, 112, 128, 128), (1, 64, 96, 64, 128), (1, 80, 70, 96, 64)])
+def test_conv_halo_stream_pool(native_lib, N, H, W, C, OC):
+    """Fused 2x2 max-pool + switch epilogue of the halo-stream kernel (DPP pair exchange) vs the fp32
+    reference: pooled values, and switch codes wherever the window max is not a near-tie."""
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(N, H, W, C, generator=g)
+    cw = _cw(OC, C)
+    (rp, rc), (gp, gc) = _cmp_conv(x, cw, epilogue="pool")
+    assert gp.shape == (N, H // 2, W // 2, OC) and _rel(gp, rp) < 1e-2
+    full = ops.conv2d(_bf(x), cw).float()
+    win = full.view(N, H // 2, 2, W // 2, 2, OC).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4, OC)
+    top2 = win.topk(2, dim=3).values
+    clear = (top2[:, :, :, 0] - top2[:, :, :, 1]) > 0.02 * top2[:, :, :, 0].abs().clamp_min(1e-3)
+    assert (gc.cpu() == rc)[clear].float().mean() > 0.999
+
+
 def test_conv_relu_in_every_kernel(native_lib, conv_impl):
     """relu_in (ReLU on the input) on signed inputs: the LDS-DMA kernel stages A verbatim, so the
     binding ReLUs a dense copy; plain, channel-slice view, transposed and masked inputs."""
