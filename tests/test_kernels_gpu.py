@@ -196,6 +196,20 @@ def test_conv_halo_stream(native_lib, dt, N, H, W, C, OC, bias, relu):
     assert _rel(got, alt) < 1e-2
 
 
+def test_conv_halo_stream_slices(native_lib):
+    """Halo-stream kernel on a channel-slice input view (x_ld > C) writing into a channel-slice
+    output view (out_ld > OC, concat layout) of a larger buffer: no byte outside the slices changes."""
+    g = torch.Generator().manual_seed(37)
+    big = torch.randn(2, 72, 80, 160, generator=g).to(torch.bfloat16).to(DEV)
+    cw = _cw(128, 96)
+    x = big[..., 32:128]
+    ref = ops.conv2d(big[..., 32:128].float().cpu(), cw, relu=True)
+    buf = torch.full((2, 72, 80, 192), 7.0, dtype=torch.bfloat16, device=DEV)
+    got = ops.conv2d(x, cw.to_device(DEV), relu=True, out=buf[..., 40:168])
+    assert _rel(got, ref) < 1e-2
+    assert (buf[..., :40] == 7).all() and (buf[..., 168:] == 7).all()
+
+
 @pytest.mark.parametrize("N,H,W,C,OC", [(2, 112, 112, 128, 128), (1, 64, 96, 64, 128), (1, 80, 70, 96, 64)])
 def test_conv_halo_stream_pool(native_lib, N, H, W, C, OC):
     """Fused 2x2 max-pool + switch epilogue of the halo-stream kernel (DPP pair exchange) vs the fp32
