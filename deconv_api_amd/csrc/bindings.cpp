@@ -41,7 +41,7 @@ void check_rc(int rc, const char* what) {
 void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
           c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
           int64_t epi, int64_t impl, c10::optional<Tensor> res, c10::optional<Tensor> emask,
-          c10::optional<Tensor> stats, int64_t stats_div) {
+          c10::optional<Tensor> stats, int64_t stats_div, c10::optional<Tensor> ucode, int64_t ucode_div) {
   TORCH_CHECK(g.size() == 23, "conv: geometry vector must have 23 entries");
   check_cuda(x, "x");
   check_cuda(w, "w");
@@ -98,7 +98,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     a.bias = bias->data_ptr<float>();
   }
   // output extent
-  int64_t out_rows = a.M;
+  int64_t out_rows = ucode.has_value() ? 4 * (int64_t)a.M : a.M;
   if (epi == dv::CONV_E_POOL) {
     TORCH_CHECK(a.OH % 2 == 0 && a.OW % 2 == 0, "conv pool: OH, OW must be even");
     out_rows = a.M / 4;
@@ -151,6 +151,18 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     a.vec_epi = epi == dv::CONV_E_BF16 && al(a.out, a.out_ld) && (!a.res || al(a.res, a.res_ld)) &&
                 (!a.emask || al(a.emask, a.emask_ld)) && std::getenv("DV_NO_VEC_EPI") == nullptr;
   }
+  if (ucode.has_value()) {  // max-unpooled output (the consumer of this conv reads the full-res map)
+    check_cuda(*ucode, "ucode");
+    TORCH_CHECK(ucode->scalar_type() == at::kByte && ucode_div >= 1 && a.N % ucode_div == 0,
+                "ucode: uint8 switch codes, N % ucode_div == 0");
+    TORCH_CHECK(epi == dv::CONV_E_BF16 && a.vec_epi && !a.res && !a.emask && !a.accumulate && a.OC % 8 == 0 &&
+                    impl != 1 && impl != 3 && !stats.has_value(),
+                "ucode: 16-bit LDS-staged epilogue of the LDS-DMA kernel (16-B aligned rows, OC % 8 == 0)");
+    need(*ucode, (int64_t)(a.N / ucode_div) * a.OH * a.OW * a.OC, "ucode");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(ucode->data_ptr()) % 8 == 0, "ucode must be 8-byte aligned");
+    a.ucode = reinterpret_cast<const uint8_t*>(ucode->data_ptr());
+    a.ucode_div = (int)ucode_div;
+  }
   bool stats_done = false;
   if (stats.has_value()) {  // per-(image) {sum, sum^2} of the fp32 output for the single-pass deprocess
     check_cuda(*stats, "stats");
@@ -177,7 +189,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                        a.stride == 1 && a.pad_h == 1 && a.pad_w == 1 && a.C == 64 && a.H == a.OH &&
                        a.W == a.OW && !a.accumulate && !mask.has_value() && a.dtype == dv::DT_BF16 &&
                        (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad == 64) &&
-                       a.res == nullptr && a.emask == nullptr;
+                       a.res == nullptr && a.emask == nullptr && a.ucode == nullptr;
   // persistent weight-resident halo kernel: 64-channel inputs at large maps (block1 of VGG16)
   const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112 && a.res == nullptr && a.emask == nullptr;
   // conv 64 -> 64 + fused 2x2 max-pool at large maps (VGG16 block1_conv2 forward): weight-resident
@@ -192,7 +204,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     }
   }
   // first layer (8-channel padded RGB image -> 64 channels): row-streaming, output-write bound
-  if (epi == dv::CONV_E_BF16 && amode == dv::CONV_A_FWD && (impl == 0 || impl == 3) && a.C == 8 &&
+  if (epi == dv::CONV_E_BF16 && amode == dv::CONV_A_FWD && (impl == 0 || impl == 3) && a.C == 8 && !a.ucode &&
       a.H * a.W >= 56 * 56 && !mask.has_value() && std::getenv("DV_NO_C8_STREAM") == nullptr) {
     const int rc = dv::conv3x3_c8_stream_launch(a, cur_stream());
     if (rc >= 0) {
@@ -215,7 +227,8 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                           (amode == dv::CONV_A_TRANSPOSE && epi == dv::CONV_E_BF16)) && !mask.has_value()) ||
                         mask_dma;
   TORCH_CHECK(impl != 2 || dma_mode, "conv: LDS-DMA kernel does not support this mode");
-  TORCH_CHECK(dma_mode || (a.res == nullptr && a.emask == nullptr), "conv: res / emask need the LDS-DMA kernel");
+  TORCH_CHECK(dma_mode || (a.res == nullptr && a.emask == nullptr && a.ucode == nullptr),
+              "conv: res / emask / ucode need the LDS-DMA kernel");
   if (dma_mode && impl != 1) {
     Tensor unpooled;
     if (amode == dv::CONV_A_UNPOOL) {  // materialize the unpooled map, then a plain DMA conv
@@ -248,7 +261,8 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     // 3x3 s1 p1 convs with 64/128 output channels at large maps: halo-stream kernel (every input
     // pixel fetched once per 32-channel chunk instead of once per tap)
     if (impl == 0 && amode == dv::CONV_A_FWD && (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_POOL) &&
-        !mask.has_value() && !a.res && !a.emask && !a.accumulate && (int64_t)a.H * a.W >= 64 * 64 && a.W >= 64) {
+        !mask.has_value() && !a.res && !a.emask && !a.ucode && !a.accumulate && (int64_t)a.H * a.W >= 64 * 64 &&
+        a.W >= 64) {
       const int rc = dv::conv3x3_hs_launch(a, (int)epi, cur_stream());
       if (rc >= 0) {
         check_rc(rc, "conv_halo_stream");
@@ -260,7 +274,8 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     const int64_t imgs_per_tile = 512 / std::max(1, a.OH * a.OW) + 2;
     TORCH_CHECK((int64_t)a.H * a.W * a.x_ld * 2 * imgs_per_tile < 0x7FFFFFF0LL, "conv dma: image too large");
     // split-K when the tile grid would leave most CUs idle (plain epilogues only)
-    const bool plain_epi = (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && !a.accumulate && !a.res && !a.emask;
+    const bool plain_epi =
+        (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && !a.accumulate && !a.res && !a.emask && !a.ucode;
     const int ks = plain_epi ? dv::conv_dma_splitk(a) : 1;
     Tensor ws;
     if (ks > 1) {
@@ -524,7 +539,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("out_code"), py::arg("code"),
         py::arg("mask"), py::arg("geom"), py::arg("amode"), py::arg("epi"), py::arg("impl"),
         py::arg("res") = py::none(), py::arg("emask") = py::none(), py::arg("stats") = py::none(),
-        py::arg("stats_div") = 1);
+        py::arg("stats_div") = 1, py::arg("ucode") = py::none(), py::arg("ucode_div") = 1);
   m.def("pool", &pool, "k x k max/avg pooling forward/backward");
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");

@@ -585,6 +585,27 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
       v.z = mask_pos_pk(v.z, em.z);
       v.w = mask_pos_pk(v.w, em.w);
     }
+    if (a.ucode) {  // max-unpool: the value goes to the window position its switch code names, 0 elsewhere
+      const int hw = a.OH * a.OW;
+      const int n = grow / hw, rem = grow - n * hw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      const uint2 cd = *reinterpret_cast<const uint2*>(a.ucode + ((long long)(n / a.ucode_div) * hw + rem) * a.OC + gcol);
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      const long long ob = (((long long)n * 2 * a.OH + 2 * oh) * 2 * a.OW + 2 * ow) * a.out_ld + gcol;
+#pragma unroll
+      for (int pos = 0; pos < 4; ++pos) {
+        uint32_t ov[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t cw = e < 2 ? cd.x : cd.y;
+          const uint32_t c0 = (cw >> (16 * (e & 1))) & 0xFFu, c1 = (cw >> (16 * (e & 1) + 8)) & 0xFFu;
+          ov[e] = (c0 == (uint32_t)pos ? vv[e] & 0xFFFFu : 0u) | (c1 == (uint32_t)pos ? vv[e] & 0xFFFF0000u : 0u);
+        }
+        const long long po = ob + ((long long)(pos >> 1) * 2 * a.OW + (pos & 1)) * a.out_ld;
+        *reinterpret_cast<uint4*>(out + po) = uint4{ov[0], ov[1], ov[2], ov[3]};
+      }
+      continue;
+    }
     *reinterpret_cast<uint4*>(out + o) = v;
   }
 }

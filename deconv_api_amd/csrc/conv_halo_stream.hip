@@ -288,6 +288,195 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// hs16: the same halo-stream scheme on 16 x 16 output tiles for maps whose sides are multiples of 16
+// (VGG16 112x112: the 16 x 32 tiles above waste 12.5 % there), with `v_mfma_f32_16x16x32_*`:
+// A = weights (16 output channels x 32 K = one whole (chunk, tap) step), B = pixels (32 K x 16 pixels
+// of one tile row); C: lane = pixel, its 4 registers = 4 consecutive output channels (8-B store).
+// 4 waves (256 threads), wave w owns tile rows 4w..4w+3; 72 KiB of LDS -> 2 workgroups per CU, so
+// one workgroup's barrier stalls hide behind the other's MFMAs.
+// LDS: halo pixels and weight rows are 64 B (4 chunks) with the chunk XOR-swizzled by bit 2 of the
+// row/pixel index (q ^ 2*((p >> 2) & 1)): for every ds_read_b128 lane group the 16 (pixel, chunk)
+// pairs of a 16-row fragment hit 16 distinct bank slots for ANY base pixel (brute-force checked over
+// strides 4..13 and swizzles on p mod 2..16: the smallest conflict-free layout), i.e. every tap shift.
+// Exact DMA counts: halo 18 x 18 x 64 B = 20.25 KiB -> 6 x 1 KiB per wave (overrun into the buffer's
+// tail), weights OC x 64 B = 8 / 4 KiB -> 2 / 1 per wave.
+namespace {
+constexpr int H16_T = 16, H16_HW = 18;
+constexpr int H16_HI = 6;                     // halo DMA instructions per wave (24 x 64 slots >= 18*18*4)
+constexpr int H16_HBUF = H16_HI * 4 * 1024;   // 24 KiB per halo buffer
+__device__ __forceinline__ int h16_swz(int p) { return ((p >> 2) & 1) << 1; }
+}  // namespace
+
+template <int DT, int OCT, bool POOL>
+__global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+  constexpr int FN = OCT / 16;                // output-channel blocks
+  constexpr int BI = OCT / 64;                // weight DMA instructions per wave and step (OCT*64 B / 4 KiB)
+  constexpr int BSLOT = OCT * 64;
+  constexpr int RING = 3;
+  constexpr int STEPS_PER_CHUNK = 9;
+  typedef typename Vec8<DT>::type v8;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * H16_HBUF + RING * BSLOT];
+  uint8_t* halo = smem;
+  uint8_t* ring = smem + 2 * H16_HBUF;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, px = lane & 15;
+  const int H = a.H, W = a.W, C = a.C;
+  const int per_img = tiles_x * tiles_y;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / per_img;
+  const int tr = bid - n * per_img;
+  const int ty0 = (tr / tiles_x) * H16_T, tx0 = (tr % tiles_x) * H16_T;
+
+  const long long img = (long long)H * W * a.x_ld;
+  const hs_i32x4 xr = hs_rsrc(a.x + (long long)n * img, img * 2);
+  const hs_i32x4 wr = hs_rsrc(a.w, (long long)a.OCpad * a.Kpad * 2);
+
+  uint32_t hoff[H16_HI];
+#pragma unroll
+  for (int u = 0; u < H16_HI; ++u) {
+    const int s = (u * 4 + wave) * 64 + lane;
+    const int p = s >> 2, ch = (s & 3) ^ h16_swz(s >> 2);
+    const int hy = p / H16_HW, hx = p - H16_HW * (p / H16_HW);
+    const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+    const bool ok = p < H16_HW * H16_HW && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    hoff[u] = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + ch * 8) * 2) : HS_OOB;
+  }
+  uint32_t woff[BI];
+#pragma unroll
+  for (int u = 0; u < BI; ++u) {
+    const int s = (u * 4 + wave) * 64 + lane;
+    const int r = s >> 2, ch = (s & 3) ^ h16_swz(s >> 2);
+    woff[u] = (uint32_t)(((long long)r * a.Kpad + ch * 8) * 2);
+  }
+  const int nch = C / 32;
+  const int nsteps = nch * STEPS_PER_CHUNK;
+  auto issue_halo = [&](int c, int buf) {
+    const uint32_t add = c < nch ? (uint32_t)(c * 64) : HS_OOB;
+#pragma unroll
+    for (int u = 0; u < H16_HI; ++u)
+      hs_dma16(xr, halo + buf * H16_HBUF + (u * 4 + wave) * 1024,
+               hoff[u] == HS_OOB || add == HS_OOB ? HS_OOB : hoff[u] + add);
+  };
+  auto issue_w = [&](int k) {
+    const int c = k / STEPS_PER_CHUNK, t = k - STEPS_PER_CHUNK * (k / STEPS_PER_CHUNK);
+    const uint32_t add = k < nsteps ? (uint32_t)((t * C + c * 32) * 2) : HS_OOB;
+    uint8_t* dst = ring + (k % RING) * BSLOT;
+#pragma unroll
+    for (int u = 0; u < BI; ++u)
+      hs_dma16(wr, dst + (u * 4 + wave) * 1024, add == HS_OOB ? HS_OOB : woff[u] + add);
+  };
+
+  f32x4 acc[4][FN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // weight row 16j + px: the swizzle term depends on bit 2 of the row, the same for every j
+  const int wrd = px * 64 + ((q ^ h16_swz(px)) << 4);
+  // pixel reads: halo pixel (4 wave + i + kh) * 18 + px + kw; its swizzle term varies with kw only
+  // through (px + kw) (the row term 18 * r shifts bit 2 too, so it is folded per (i + kh) at compile
+  // time via the row's base pixel index)
+  issue_halo(0, 0);
+  issue_w(0);
+  issue_w(1);
+  for (int c = 0; c < nch; ++c) {
+    const uint8_t* hb = halo + (c & 1) * H16_HBUF;
+#pragma unroll
+    for (int t = 0; t < STEPS_PER_CHUNK; ++t) {
+      const int k = c * STEPS_PER_CHUNK + t;
+      if (t == 1) hs_wait<BI + H16_HI>();
+      else hs_wait<BI>();
+      __builtin_amdgcn_s_barrier();
+      if (t == 0) issue_halo(c + 1, (c + 1) & 1);
+      issue_w(k + 2);
+      const uint8_t* wb = ring + (k % RING) * BSLOT + wrd;
+      const int kh = t / 3, kw = t % 3;
+      v8 wf[FN], pf[4];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) wf[j] = *reinterpret_cast<const v8*>(wb + j * 16 * 64);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = (4 * wave + i + kh) * H16_HW + px + kw;
+        pf[i] = *reinterpret_cast<const v8*>(hb + p * 64 + ((q ^ h16_swz(p)) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(wf[j], pf[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  hs_wait<0>();
+
+  // epilogue: lane = pixel (tile row 4 wave + i, column px); register r of block j = channel 16j + 4q + r
+  const int ox = tx0 + px;
+  float4 bv[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+    bv[j] = a.bias ? *reinterpret_cast<const float4*>(a.bias + 16 * j + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float lo = a.relu ? 0.f : -INFINITY;
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+  if constexpr (POOL) {  // windows (rows 4w+i, 4w+i+1) x (px, px^1): i = 0, 2; the odd column via DPP
+    const int PH = H >> 1, PW = W >> 1;
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+      const long long prow = ((long long)n * PH + ((ty0 >> 1) + 2 * wave + (i >> 1))) * PW + (ox >> 1);
+      const bool st = (px & 1) == 0;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int oc = 16 * j + 4 * q;
+        const float b4[4] = {bv[j].x, bv[j].y, bv[j].z, bv[j].w};
+        float best[4];
+        uint32_t codes = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float w4[4];
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const float v = to_f<DT>(from_f<DT>(fmaxf(acc[i + d][j][r] + b4[r], lo)));
+            w4[2 * d] = v;
+            w4[2 * d + 1] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+          }
+          float m = w4[0];
+          uint32_t cc = 0;
+#pragma unroll
+          for (int e = 1; e < 4; ++e)
+            if (w4[e] > m) {
+              m = w4[e];
+              cc = e;
+            }
+          best[r] = m;
+          codes |= cc << (8 * r);
+        }
+        if (st && oc < a.OC) {
+          *reinterpret_cast<uint2*>(out + prow * a.out_ld + oc) =
+              make_uint2(pack2<DT>(best[0], best[1]), pack2<DT>(best[2], best[3]));
+          *reinterpret_cast<uint32_t*>(a.out_code + prow * a.OC + oc) = codes;
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int oy = ty0 + 4 * wave + i;
+    uint16_t* orow = out + (((long long)n * H + oy) * W + ox) * a.out_ld;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int oc = 16 * j + 4 * q;
+      if (oc >= a.OC) continue;
+      const float v0 = fmaxf(acc[i][j][0] + bv[j].x, lo), v1 = fmaxf(acc[i][j][1] + bv[j].y, lo);
+      const float v2 = fmaxf(acc[i][j][2] + bv[j].z, lo), v3 = fmaxf(acc[i][j][3] + bv[j].w, lo);
+      *reinterpret_cast<uint2*>(orow + oc) = make_uint2(pack2<DT>(v0, v1), pack2<DT>(v2, v3));
+    }
+  }
+}
+
 // weight ring depth (slots; B(k + ring - 1) is prefetched at step k). DV_HS_RING = 3 / 4 / 5 (A/B)
 static int hs_ring() {
   static int v = [] {
@@ -322,6 +511,26 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
   if (pool && (a.H % 2 || a.W % 2 || a.out_code == nullptr || a.OC % 4 || a.dtype != DT_BF16 ||
                (reinterpret_cast<uintptr_t>(a.out_code) & 3)))
     return -4;
+  // exact 16 x 16 tiling (OC % 4 == 0: whole 8-B channel quads) -> hs16
+  if (a.H % 16 == 0 && a.W % 16 == 0 && a.OC % 4 == 0 && std::getenv("DV_NO_HS16") == nullptr) {
+    const int t16x = a.W / 16, t16y = a.H / 16;
+    const long long n16 = (long long)a.N * t16x * t16y;
+    if (n16 <= 0 || n16 > 0x7fffffffLL) return -2;
+    const dim3 g16((unsigned)n16), b16(256);
+#define HS16(DT_, OCT_, POOL_) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_, OCT_, POOL_>), g16, b16, 0, s, a, t16x, t16y)
+    if (pool) {
+      if (a.OCpad == 128) HS16(DT_BF16, 128, true);
+      else HS16(DT_BF16, 64, true);
+    } else if (a.dtype == DT_F16) {
+      if (a.OCpad == 128) HS16(DT_F16, 128, false);
+      else HS16(DT_F16, 64, false);
+    } else {
+      if (a.OCpad == 128) HS16(DT_BF16, 128, false);
+      else HS16(DT_BF16, 64, false);
+    }
+#undef HS16
+    return (int)hipGetLastError();
+  }
   const int tx = (a.W + HS_TW - 1) / HS_TW, ty = (a.H + HS_TH - 1) / HS_TH;
   const long long nwg = (long long)a.N * tx * ty;
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;

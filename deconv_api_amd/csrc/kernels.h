@@ -50,6 +50,8 @@ struct ConvArgs {
   int ksplit;
   double* stats;          // optional (row-streaming kernel): stats[n / stats_div] += {sum out, sum out^2}
   int stats_div;
+  const uint8_t* ucode;   // optional (LDS-DMA, vector epilogue): max-unpool the output with these switch
+  int ucode_div;          //   codes [N/ucode_div][OH][OW][OC]; out is then [N][2 OH][2 OW] rows of out_ld
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);

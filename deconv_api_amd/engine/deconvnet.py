@@ -227,9 +227,19 @@ class DeconvNet:
             # down = ReLU(convT(ReLU(signal))) (app/deepdream.py:110,260). The input ReLU only acts on
             # an unpooled signal (the unpool consumes it for free): every other input is already a
             # ReLU output (seed stencil, conv-down epilogues), so relu_in would be a no-op pass
+            # a conv-down feeding an unpool writes the unpooled map straight from its epilogue (no pooled
+            # round trip, no separate unpool pass) unless the consumer is a 64-channel conv, whose
+            # halo kernel fuses the unpool into its input staging instead (reads 1/4 of the bytes)
+            below = self.specs[j - 1] if j >= 2 else None
+            fuse_unpool = (below is not None and below.kind == "pool" and j >= 3 and pending_code is None and
+                           cl.dec.cout % 8 == 0 and
+                           (not d.is_cuda or self.rt.convs[self.specs[j - 2].name].dec.cin != 64))
             if pending_code is not None:
                 d = ops.conv2d(d, cl.dec, in_mode="unpool", code=pending_code, code_div=K, relu_in=True, **kw)
                 pending_code = None
+            elif fuse_unpool:
+                d = ops.conv2d(d, cl.dec, unpool_out=st.codes[below.name], unpool_div=K, **kw)
+                j -= 1  # the pool's unpool is done
             else:
                 d = ops.conv2d(d, cl.dec, **kw)
             if last:

@@ -215,7 +215,8 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
            code_div: int = 1, mask: Optional[torch.Tensor] = None, epilogue: str = "bf16",
            out: Optional[torch.Tensor] = None, accumulate: bool = False, out_hw=None,
            use_bias: bool = True, res: Optional[torch.Tensor] = None, emask: Optional[torch.Tensor] = None,
-           stats: Optional[torch.Tensor] = None, stats_div: int = 1):
+           stats: Optional[torch.Tensor] = None, stats_div: int = 1, unpool_out: Optional[torch.Tensor] = None,
+           unpool_div: int = 1):
     """NHWC convolution.
 
     x: [N, H, W, C] (channel-slice views allowed: stride(3) == 1). For ``in_mode='unpool'`` x is
@@ -225,6 +226,8 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     ``emask`` (with ``res``): the result is zeroed where emask <= 0.
     ``stats`` (GPU, fp32 epilogue): fp64 [N / stats_div, 2] receives {sum, sum of squares} of each
     group of ``stats_div`` output images (the single-pass mosaic deprocess consumes it).
+    ``unpool_out``: switch codes [N / unpool_div, OH, OW, OC]; the result is max-unpooled in the
+    epilogue and returned at [N, 2 OH, 2 OW, OC] (the deconvnet's conv-down feeding an unpool).
     """
     if pad is None:
         pad = (cw.KH // 2, cw.KW // 2)
@@ -249,8 +252,14 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     OC = cw.cout
     if x.is_cuda:
         return _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
-                           mask, epilogue, out, accumulate, use_bias, res, emask, stats, stats_div)
+                           mask, epilogue, out, accumulate, use_bias, res, emask, stats, stats_div, unpool_out,
+                           unpool_div)
     assert stats is None, "conv2d: stats are produced by the GPU kernels only"
+    if unpool_out is not None:
+        assert epilogue == "bf16" and out is None and not accumulate, "conv2d: unpool_out needs a fresh 16-bit output"
+        y = _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
+                        mask, epilogue, None, False, use_bias, res, emask)
+        return unpool_ref(y, unpool_out, unpool_div).contiguous()
     return _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
                        mask, epilogue, out, accumulate, use_bias, res, emask)
 
@@ -303,7 +312,8 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
 
 
 def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
-                epilogue, out, accumulate, use_bias, res=None, emask=None, stats=None, stats_div=1):
+                epilogue, out, accumulate, use_bias, res=None, emask=None, stats=None, stats_div=1,
+                unpool_out=None, unpool_div=1):
     lib = native.lib()
     dt = x.dtype
     assert dt in (torch.bfloat16, torch.float16) and x.stride(3) == 1, \
@@ -319,6 +329,11 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
         if out is None:
             out = torch.empty(N, OH // 2, OW // 2, OC, dtype=dt, device=x.device)
         out_code = torch.empty(N, OH // 2, OW // 2, OC, dtype=torch.uint8, device=x.device)
+    elif unpool_out is not None:
+        assert epilogue == "bf16" and out is None and not accumulate, "conv2d: unpool_out needs a fresh 16-bit output"
+        out_code = None
+        out = torch.empty(N, 2 * OH, 2 * OW, OC, dtype=dt, device=x.device)
+        unpool_out = unpool_out.contiguous()
     else:
         out_code = None
         if out is None:
@@ -336,8 +351,8 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
             int(relu), int(relu_in), int(accumulate), int(code_div), x_ld, mask_ld, out_ld]
     bias = cw.bias_pad if use_bias else None
     lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
-             IMPL[_policy["impl"]] if res is None and emask is None else IMPL["dma"], res, emask,  # DMA-only epilogues
-             stats, stats_div)
+             IMPL[_policy["impl"]] if res is None and emask is None and unpool_out is None else IMPL["dma"],
+             res, emask, stats, stats_div, unpool_out, unpool_div)  # res / emask / unpool_out: DMA-only epilogues
     if epilogue == "pool":
         return out, out_code
     return out

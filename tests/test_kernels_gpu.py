@@ -152,9 +152,9 @@ def test_conv_first_layer_stream(native_lib, N, H, W, OC):
 
 @pytest.mark.parametrize("N,H,W,C,OC", [(6, 112, 112, 128, 128), (11, 112, 112, 128, 64), (5, 115, 121, 64, 128)])
 def test_conv_large_m_ks2_tiles(native_lib, conv_impl, N, H, W, C, OC):
-    """Large-M launches of the 128- and 64-output-channel layers take the in-workgroup K-split
-    (KS2) 256x128 / 512x64 tiles (>= one tile per CU): bf16 vector epilogue, unaligned row
-    stride (per-element epilogue), f32 epilogue, fused pool+switch and the transposed dgrad."""
+    """Large-M launches of the 128- and 64-output-channel layers (>= one 256x128 / 512x64 tile per
+    CU; with DV_KS2=1 in the environment, the in-workgroup K-split variants): bf16 vector epilogue,
+    f32 epilogue, fused pool+switch and the transposed dgrad."""
     g = torch.Generator().manual_seed(21)
     x = torch.randn(N, H, W, C, generator=g)
     cw = _cw(OC, C)
@@ -188,29 +188,33 @@ def test_conv_halo_stream(native_lib, dt, N, H, W, C, OC, bias, relu):
     ref = ops.conv2d(x.to(dt).float(), cw, relu=relu, use_bias=bias)
     got = ops.conv2d(xd, cw.to_device(DEV, dt), relu=relu, use_bias=bias)
     assert got.shape == ref.shape and got.dtype == dt and _rel(got, ref) < 1e-2
-    os.environ["DV_NO_HS"] = "1"
-    try:
-        alt = ops.conv2d(xd, cw.to_device(DEV, dt), relu=relu, use_bias=bias)
-    finally:
-        del os.environ["DV_NO_HS"]
-    assert _rel(got, alt) < 1e-2
+    for env in ("DV_NO_HS", "DV_NO_HS16"):  # implicit GEMM; 16x32-tile kernel instead of 16x16
+        os.environ[env] = "1"
+        try:
+            alt = ops.conv2d(xd, cw.to_device(DEV, dt), relu=relu, use_bias=bias)
+        finally:
+            del os.environ[env]
+        assert _rel(got, alt) < 1e-2, env
 
 
-def test_conv_halo_stream_slices(native_lib):
-    """Halo-stream kernel on a channel-slice input view (x_ld > C) writing into a channel-slice
-    output view (out_ld > OC, concat layout) of a larger buffer: no byte outside the slices changes."""
+@pytest.mark.parametrize("H,W", [(72, 80), (64, 80)])
+def test_conv_halo_stream_slices(native_lib, H, W):
+    """Halo-stream kernels (16x32 tiles; 16x16 tiles when H, W % 16 == 0) on a channel-slice input
+    view (x_ld > C) writing into a channel-slice output view (out_ld > OC, concat layout) of a larger
+    buffer: no byte outside the slices changes."""
     g = torch.Generator().manual_seed(37)
-    big = torch.randn(2, 72, 80, 160, generator=g).to(torch.bfloat16).to(DEV)
+    big = torch.randn(2, H, W, 160, generator=g).to(torch.bfloat16).to(DEV)
     cw = _cw(128, 96)
     x = big[..., 32:128]
     ref = ops.conv2d(big[..., 32:128].float().cpu(), cw, relu=True)
-    buf = torch.full((2, 72, 80, 192), 7.0, dtype=torch.bfloat16, device=DEV)
+    buf = torch.full((2, H, W, 192), 7.0, dtype=torch.bfloat16, device=DEV)
     got = ops.conv2d(x, cw.to_device(DEV), relu=True, out=buf[..., 40:168])
     assert _rel(got, ref) < 1e-2
     assert (buf[..., :40] == 7).all() and (buf[..., 168:] == 7).all()
 
 
-@pytest.mark.parametrize("N,H,W,C,OC", [(2, 112, 112, 128, 128), (1, 64, 96, 64, 128), (1, 80, 70, 96, 64)])
+@pytest.mark.parametrize("N,H,W,C,OC", [(2, 112, 112, 128, 128), (1, 64, 96, 64, 128), (1, 80, 70, 96, 64),
+                                        (2, 48, 32, 32, 64)])
 def test_conv_halo_stream_pool(native_lib, N, H, W, C, OC):
     """Fused 2x2 max-pool + switch epilogue of the halo-stream kernel (DPP pair exchange) vs the fp32
     reference: pooled values, and switch codes wherever the window max is not a near-tie."""
@@ -244,6 +248,26 @@ def test_conv_relu_in_every_kernel(native_lib, conv_impl):
     kw = dict(relu=False, relu_in=True, in_mode="transpose", stride=1, pad=(1, 1), out_hw=(12, 14), use_bias=False)
     ref = ops.conv2d(_bf(x), ct, mask=_bf(mask), **kw)
     got = ops.conv2d(x.to(torch.bfloat16).to(DEV), ct.to_device(DEV), mask=mask.to(torch.bfloat16).to(DEV), **kw)
+    assert _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,OC,div", [(8, 14, 512, 512, 4), (4, 28, 256, 256, 2), (2, 56, 256, 128, 1),
+                                          (3, 9, 64, 24, 3)])
+def test_conv_unpool_out_epilogue(native_lib, N, H, C, OC, div):
+    """Max-unpool fused into the conv epilogue (unpool_out) == unpool of the plain conv output (the
+    plain launch may split K at small M: summation order differs) and == the fp32 reference path."""
+    g = torch.Generator().manual_seed(47)
+    x = torch.relu(torch.randn(N, H, H, C, generator=g)).to(torch.bfloat16)
+    code = torch.randint(0, 4, (N // div, H, H, OC), generator=g, dtype=torch.uint8)
+    cw = _cw(OC, C, bias=False)
+    cwd = cw.to_device(DEV)
+    got = ops.conv2d(x.to(DEV), cwd, relu=True, use_bias=False, unpool_out=code.to(DEV), unpool_div=div)
+    plain = ops.conv2d(x.to(DEV), cwd, relu=True, use_bias=False)
+    assert got.shape == (N, 2 * H, 2 * H, OC)
+    want = ops.unpool_ref(plain, code.to(DEV), div)
+    assert _rel(got, want) < 1e-2
+    assert ((got != 0) & (want == 0)).sum() == 0  # nothing lands off the switch position
+    ref = ops.conv2d(x.float(), cw, relu=True, use_bias=False, unpool_out=code, unpool_div=div)
     assert _rel(got, ref) < 1e-2
 
 

@@ -41,9 +41,12 @@ def main():
         OH, OW = out.shape[1], out.shape[2]
         if kw.get("epilogue") == "pool":
             OH, OW = OH * 2, OW * 2
+        if kw.get("unpool_out") is not None:  # the output was max-unpooled in the epilogue
+            OH, OW = OH // 2, OW // 2
         M = N * OH * OW
         flops = 2.0 * M * cw.cout * cw.KH * cw.KW * cw.cin
-        records.append((kw.get("in_mode", "plain"), kw.get("epilogue", "bf16"), M, cw.cout, cw.K, flops, s, e))
+        mode = "unpoolo" if kw.get("unpool_out") is not None else kw.get("in_mode", "plain")
+        records.append((mode, kw.get("epilogue", "bf16"), M, cw.cout, cw.K, flops, s, e))
         return r
 
     ops.conv2d = timed
