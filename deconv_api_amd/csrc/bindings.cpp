@@ -213,6 +213,15 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       return;
     }
   }
+  // unpool -> conv (64/128 out, full-res sides % 16): hs16 with the pooled halo expanded in LDS
+  if (impl == 0 && amode == dv::CONV_A_UNPOOL && epi == dv::CONV_E_BF16 && !mask.has_value()) {
+    const int rc = dv::conv3x3_hs_unpool_launch(a, cur_stream());
+    if (rc >= 0) {
+      check_rc(rc, "conv_halo_stream_unpool");
+      finish_stats();
+      return;
+    }
+  }
   if (impl == 3 || (impl == 0 && halo_auto)) {
     TORCH_CHECK(halo_ok, "conv: halo-tile kernel does not support this shape/mode");
     check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream(), &stats_done),

@@ -308,17 +308,28 @@ constexpr int H16_HBUF = H16_HI * 4 * 1024;   // 24 KiB per halo buffer
 __device__ __forceinline__ int h16_swz(int p) { return ((p >> 2) & 1) << 1; }
 }  // namespace
 
-template <int DT, int OCT, bool POOL>
+// UNPOOL: the input is a max-pooled map (H/2 x W/2, a.x) + switch codes (a.code, per image n/code_div)
+// and the conv reads its max-unpooled, ReLU'd version (the deconvnet's unpool -> conv-down). Per chunk
+// the 10 x 10 pooled pixels and their codes under the tile are LDS-DMA'd into a staging buffer
+// (3 instructions per wave) and expanded by all threads into the 18 x 18 full-resolution halo layout
+// at the end of the previous chunk's last step: a quarter of the input bytes of a materialized unpool.
+constexpr int HU_PI = 2, HU_CI = 1;           // pooled-value / code DMA instructions per wave and chunk
+constexpr int HU_PBUF = HU_PI * 4 * 1024, HU_CBUF = HU_CI * 4 * 1024;
+
+template <int DT, int OCT, bool POOL, bool UNPOOL>
 __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
   constexpr int FN = OCT / 16;                // output-channel blocks
   constexpr int BI = OCT / 64;                // weight DMA instructions per wave and step (OCT*64 B / 4 KiB)
   constexpr int BSLOT = OCT * 64;
   constexpr int RING = 3;
   constexpr int STEPS_PER_CHUNK = 9;
+  constexpr int HI = UNPOOL ? HU_PI + HU_CI : H16_HI;  // input DMA instructions per wave and chunk
   typedef typename Vec8<DT>::type v8;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * H16_HBUF + RING * BSLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * H16_HBUF + RING * BSLOT + (UNPOOL ? HU_PBUF + HU_CBUF : 0)];
   uint8_t* halo = smem;
   uint8_t* ring = smem + 2 * H16_HBUF;
+  uint8_t* pstage = ring + RING * BSLOT;      // UNPOOL: pooled values [100 px][64 B], codes [100 px][32 B]
+  uint8_t* cstage = pstage + HU_PBUF;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -330,19 +341,43 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
   const int tr = bid - n * per_img;
   const int ty0 = (tr / tiles_x) * H16_T, tx0 = (tr % tiles_x) * H16_T;
 
-  const long long img = (long long)H * W * a.x_ld;
+  const int PH = H >> 1, PW = W >> 1;
+  const long long img = UNPOOL ? (long long)PH * PW * a.x_ld : (long long)H * W * a.x_ld;
   const hs_i32x4 xr = hs_rsrc(a.x + (long long)n * img, img * 2);
   const hs_i32x4 wr = hs_rsrc(a.w, (long long)a.OCpad * a.Kpad * 2);
+  const long long cimg = (long long)PH * PW * C;  // UNPOOL: code bytes per image
+  const hs_i32x4 cr = hs_rsrc(UNPOOL ? a.code + (long long)(n / a.code_div) * cimg : a.code, cimg);
 
-  uint32_t hoff[H16_HI];
+  uint32_t hoff[HI];
+  if constexpr (UNPOOL) {
+    // pooled staging: slot s -> pooled pixel sp = s / 4 of the 10 x 10 block (rows ty0/2 - 1 ..), chunk s % 4;
+    // codes: slot s -> pooled pixel s / 2, 16-B half s % 2 (32 channel codes = 32 B per pixel)
+    const int py0 = (ty0 >> 1) - 1, px0 = (tx0 >> 1) - 1;
 #pragma unroll
-  for (int u = 0; u < H16_HI; ++u) {
-    const int s = (u * 4 + wave) * 64 + lane;
-    const int p = s >> 2, ch = (s & 3) ^ h16_swz(s >> 2);
-    const int hy = p / H16_HW, hx = p - H16_HW * (p / H16_HW);
-    const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
-    const bool ok = p < H16_HW * H16_HW && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-    hoff[u] = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + ch * 8) * 2) : HS_OOB;
+    for (int u = 0; u < HU_PI; ++u) {
+      const int s = (u * 4 + wave) * 64 + lane;
+      const int sp = s >> 2, ch = s & 3;
+      const int y = py0 + sp / 10, x = px0 + sp % 10;
+      const bool ok = sp < 100 && (unsigned)y < (unsigned)PH && (unsigned)x < (unsigned)PW;
+      hoff[u] = ok ? (uint32_t)((((long long)y * PW + x) * a.x_ld + ch * 8) * 2) : HS_OOB;
+    }
+    {
+      const int s = wave * 64 + lane;
+      const int sp = s >> 1, hf = s & 1;
+      const int y = py0 + sp / 10, x = px0 + sp % 10;
+      const bool ok = sp < 100 && (unsigned)y < (unsigned)PH && (unsigned)x < (unsigned)PW;
+      hoff[HU_PI] = ok ? (uint32_t)(((long long)y * PW + x) * C + hf * 16) : HS_OOB;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < H16_HI; ++u) {
+      const int s = (u * 4 + wave) * 64 + lane;
+      const int p = s >> 2, ch = (s & 3) ^ h16_swz(s >> 2);
+      const int hy = p / H16_HW, hx = p - H16_HW * (p / H16_HW);
+      const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+      const bool ok = p < H16_HW * H16_HW && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      hoff[u] = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + ch * 8) * 2) : HS_OOB;
+    }
   }
   uint32_t woff[BI];
 #pragma unroll
@@ -355,10 +390,46 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
   const int nsteps = nch * STEPS_PER_CHUNK;
   auto issue_halo = [&](int c, int buf) {
     const uint32_t add = c < nch ? (uint32_t)(c * 64) : HS_OOB;
+    if constexpr (UNPOOL) {
 #pragma unroll
-    for (int u = 0; u < H16_HI; ++u)
-      hs_dma16(xr, halo + buf * H16_HBUF + (u * 4 + wave) * 1024,
-               hoff[u] == HS_OOB || add == HS_OOB ? HS_OOB : hoff[u] + add);
+      for (int u = 0; u < HU_PI; ++u)
+        hs_dma16(xr, pstage + (u * 4 + wave) * 1024, hoff[u] == HS_OOB || add == HS_OOB ? HS_OOB : hoff[u] + add);
+      const uint32_t cadd = c < nch ? (uint32_t)(c * 32) : HS_OOB;
+      hs_dma16(cr, cstage + wave * 1024, hoff[HU_PI] == HS_OOB || cadd == HS_OOB ? HS_OOB : hoff[HU_PI] + cadd);
+    } else {
+#pragma unroll
+      for (int u = 0; u < H16_HI; ++u)
+        hs_dma16(xr, halo + buf * H16_HBUF + (u * 4 + wave) * 1024,
+                 hoff[u] == HS_OOB || add == HS_OOB ? HS_OOB : hoff[u] + add);
+    }
+  };
+  // UNPOOL: staged pooled chunk -> full-resolution halo buffer `buf` (ReLU, switch select, zero
+  // outside the image); 18 x 18 pixels x 4 chunks of 16 B over 256 threads
+  auto expand = [&](int buf) {
+    uint8_t* hd = halo + buf * H16_HBUF;
+    for (int it = tid; it < H16_HW * H16_HW * 4; it += 256) {
+      const int p = it >> 2, ch = it & 3;
+      const int hy = p / H16_HW, hx = p - H16_HW * (p / H16_HW);
+      const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
+        const int sp = ((y >> 1) - ((ty0 >> 1) - 1)) * 10 + ((x >> 1) - ((tx0 >> 1) - 1));
+        const uint4 pv = *reinterpret_cast<const uint4*>(pstage + sp * 64 + ch * 16);
+        const uint2 cd = *reinterpret_cast<const uint2*>(cstage + sp * 32 + ch * 8);
+        const uint32_t pos = (uint32_t)(((y & 1) << 1) | (x & 1));
+        const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+        uint32_t ov[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t cw = e < 2 ? cd.x : cd.y;
+          const uint32_t c0 = (cw >> (16 * (e & 1))) & 0xFFu, c1 = (cw >> (16 * (e & 1) + 8)) & 0xFFu;
+          const uint32_t r = relu_bf2(pw[e]);  // sign-bit test: valid for fp16 bit patterns too
+          ov[e] = (c0 == pos ? r & 0xFFFFu : 0u) | (c1 == pos ? r & 0xFFFF0000u : 0u);
+        }
+        v = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+      }
+      *reinterpret_cast<uint4*>(hd + p * 64 + ((ch ^ h16_swz(p)) << 4)) = v;
+    }
   };
   auto issue_w = [&](int k) {
     const int c = k / STEPS_PER_CHUNK, t = k - STEPS_PER_CHUNK * (k / STEPS_PER_CHUNK);
@@ -381,6 +452,12 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
   // through (px + kw) (the row term 18 * r shifts bit 2 too, so it is folded per (i + kh) at compile
   // time via the row's base pixel index)
   issue_halo(0, 0);
+  if constexpr (UNPOOL) {
+    hs_wait<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's share of the staging DMA has landed
+    expand(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before readers by step 0's barrier
+  }
   issue_w(0);
   issue_w(1);
   for (int c = 0; c < nch; ++c) {
@@ -388,7 +465,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
 #pragma unroll
     for (int t = 0; t < STEPS_PER_CHUNK; ++t) {
       const int k = c * STEPS_PER_CHUNK + t;
-      if (t == 1) hs_wait<BI + H16_HI>();
+      if (t == 1) hs_wait<BI + HI>();
       else hs_wait<BI>();
       __builtin_amdgcn_s_barrier();
       if (t == 0) issue_halo(c + 1, (c + 1) & 1);
@@ -409,6 +486,16 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(wf[j], pf[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (UNPOOL) {
+        // last step of chunk c: expand chunk c+1 (staged at step 9c; younger than it: the 9 weight
+        // DMAs of steps 9c..9c+8) into the other halo buffer, last read during chunk c-1
+        if (t == STEPS_PER_CHUNK - 1 && c + 1 < nch) {
+          hs_wait<STEPS_PER_CHUNK * BI>();
+          __builtin_amdgcn_s_barrier();  // every wave's share of the staging DMA has landed
+          expand((c + 1) & 1);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+      }
     }
   }
   hs_wait<0>();
@@ -517,7 +604,7 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
     const long long n16 = (long long)a.N * t16x * t16y;
     if (n16 <= 0 || n16 > 0x7fffffffLL) return -2;
     const dim3 g16((unsigned)n16), b16(256);
-#define HS16(DT_, OCT_, POOL_) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_, OCT_, POOL_>), g16, b16, 0, s, a, t16x, t16y)
+#define HS16(DT_, OCT_, POOL_) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_, OCT_, POOL_, false>), g16, b16, 0, s, a, t16x, t16y)
     if (pool) {
       if (a.OCpad == 128) HS16(DT_BF16, 128, true);
       else HS16(DT_BF16, 64, true);
@@ -545,6 +632,37 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
   } else {
     if (a.OCpad == 128) HS_LAUNCH(DT_BF16, 128, false);
     else HS_LAUNCH(DT_BF16, 64, false);
+  }
+  return (int)hipGetLastError();
+}
+
+// unpool (pooled map + switch codes, ReLU) -> 3x3 conv on the hs16 kernel: the deconvnet's conv-down
+// of a pooled signal at maps whose full-resolution sides are multiples of 16 (< 0: unsupported).
+// Opt-in (DV_HSU=1): on VGG16 block1_conv2.down (224^2, 64 -> 64, only 2 channel chunks per tile, so the
+// synchronous first expansion is not amortized) it measured 5.23 ms vs 4.57 ms for the weight-resident
+// halo kernel (profiles/layers_r1_hsu_{off,on}.txt); the 128-channel unpools are fused into the
+// producing conv-down's epilogue instead (ucode).
+int conv3x3_hs_unpool_launch(const ConvArgs& a, hipStream_t s) {
+  const char* on = std::getenv("DV_HSU");
+  if (on == nullptr || std::atoi(on) == 0 || std::getenv("DV_NO_HSU") != nullptr) return -4;
+  if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH || a.W != a.OW ||
+      a.H % 16 || a.W % 16 || a.C % 32 || a.x_ld % 8 || (a.OCpad != 64 && a.OCpad != 128) || a.OC % 4 ||
+      !a.relu_in || a.code == nullptr || a.code_div < 1 || a.N % a.code_div || a.accumulate || a.mask || a.res ||
+      a.emask || a.ws || a.stats || a.ucode || a.out_ld % 4 || (reinterpret_cast<uintptr_t>(a.out) & 7) ||
+      (reinterpret_cast<uintptr_t>(a.x) & 15) || (reinterpret_cast<uintptr_t>(a.bias) & 15) ||
+      (reinterpret_cast<uintptr_t>(a.code) & 15) || (long long)a.Kpad < 9LL * a.C ||
+      (long long)(a.H / 2) * (a.W / 2) * a.x_ld * 2 > 0x7FFFFFF0LL)
+    return -4;
+  const int t16x = a.W / 16, t16y = a.H / 16;
+  const long long n16 = (long long)a.N * t16x * t16y;
+  if (n16 <= 0 || n16 > 0x7fffffffLL) return -2;
+  const dim3 g16((unsigned)n16), b16(256);
+  if (a.dtype == DT_F16) {
+    if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_F16, 128, false, true>), g16, b16, 0, s, a, t16x, t16y);
+    else hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_F16, 64, false, true>), g16, b16, 0, s, a, t16x, t16y);
+  } else {
+    if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_BF16, 128, false, true>), g16, b16, 0, s, a, t16x, t16y);
+    else hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_BF16, 64, false, true>), g16, b16, 0, s, a, t16x, t16y);
   }
   return (int)hipGetLastError();
 }

@@ -115,4 +115,6 @@ int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s);
 // halo-stream 3x3 s1 p1 conv, C % 32 == 0 -> OCpad 64 / 128, 16-bit out or fused 2x2 max-pool +
 // switch (epi CONV_E_BF16 / CONV_E_POOL; < 0: unsupported)
 int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s);
+// unpool (pooled map + switch codes, input ReLU) -> 3x3 conv, 16-bit out, on the hs16 kernel (< 0: unsupported)
+int conv3x3_hs_unpool_launch(const ConvArgs& a, hipStream_t s);
 }  // namespace dv
