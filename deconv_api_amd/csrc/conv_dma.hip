@@ -633,7 +633,9 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
 // DV_DMA_VARIANT: 0 (default) 2-stage BK64 except 256x128 (3-stage); 1: all 2-stage BK64;
 // 2: BK32 x 4-stage rings for 256x256 and 512x64; 3: 128x256 3-stage for OC%256;
 // 4: register double-buffered fragments + s_setprio around MFMA runs (default for 256x256; v1
-// there selects the plain fragment loop) (A/B testing).
+// there selects the plain fragment loop) (A/B testing). Measured and removed: 4-wave 256x128 /
+// 128x256 workgroups (BK=32 x 3 stages, 72 KiB -> 2 per CU) on the 256/512-channel layers ran at
+// 0.53-0.72 PF/s vs 0.99-1.28 (profiles/layers_r1_dmav{0,5,6}.txt): 1.5x the staged bytes per FLOP.
 static int dma_variant() {
   static int v = [] {
     const char* e = std::getenv("DV_DMA_VARIANT");

@@ -150,11 +150,12 @@ def test_conv_first_layer_stream(native_lib, N, H, W, OC):
     assert _rel(got, alt) < 1e-2
 
 
-@pytest.mark.parametrize("N,H,W,C,OC", [(6, 112, 112, 128, 128), (11, 112, 112, 128, 64), (5, 115, 121, 64, 128)])
+@pytest.mark.parametrize("N,H,W,C,OC", [(6, 112, 112, 128, 128), (11, 112, 112, 128, 64), (5, 115, 121, 64, 128),
+                                        (21, 56, 56, 256, 256)])
 def test_conv_large_m_ks2_tiles(native_lib, conv_impl, N, H, W, C, OC):
-    """Large-M launches of the 128- and 64-output-channel layers (>= one 256x128 / 512x64 tile per
-    CU; with DV_KS2=1 in the environment, the in-workgroup K-split variants): bf16 vector epilogue,
-    f32 epilogue, fused pool+switch and the transposed dgrad."""
+    """Large-M launches (>= one 256x128 / 512x64 tile per CU; with DV_KS2=1 in the environment the
+    in-workgroup K-split variants, with DV_DMA_VARIANT=5/6 the 4-wave 256-channel tiles): bf16 vector
+    epilogue, f32 epilogue, fused pool+switch and the transposed dgrad."""
     g = torch.Generator().manual_seed(21)
     x = torch.randn(N, H, W, C, generator=g)
     cw = _cw(OC, C)
