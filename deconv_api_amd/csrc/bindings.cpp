@@ -191,11 +191,17 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                        (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && (a.OC <= 16 || a.OCpad == 64) &&
                        a.res == nullptr && a.emask == nullptr && a.ucode == nullptr;
   // persistent weight-resident halo kernel: 64-channel inputs at large maps (block1 of VGG16)
-  const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112 && a.res == nullptr && a.emask == nullptr;
+  // the 16 x 16-tile halo-stream kernel (conv_halo_stream.hip) beats the weight-resident halo kernel
+  // on plain 16-bit-output convs whose sides are multiples of 16 (measured on the pool variant:
+  // VGG16 block1_conv2 fwd 1.28 -> 1.04 ms, profiles/layers_r1_ab{0,1}.txt)
+  const bool hs16_ok = a.H % 16 == 0 && a.W % 16 == 0 && a.C % 32 == 0 && a.OC % 4 == 0 && !a.relu_in &&
+                       (a.OCpad == 64 || a.OCpad == 128) && std::getenv("DV_NO_HS") == nullptr;
+  const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112 && a.res == nullptr && a.emask == nullptr &&
+                         !(hs16_ok && amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16);
   // conv 64 -> 64 + fused 2x2 max-pool at large maps (VGG16 block1_conv2 forward): weight-resident
   // halo kernel with LDS-DMA staging and the pool in registers
   if (epi == dv::CONV_E_POOL && amode == dv::CONV_A_FWD && (impl == 0 || impl == 3) && a.H * a.W >= 112 * 112 &&
-      !mask.has_value() && std::getenv("DV_NO_POOL_V3") == nullptr) {
+      !mask.has_value() && std::getenv("DV_NO_POOL_V3") == nullptr && (impl == 3 || !hs16_ok)) {
     const int rc = dv::conv3x3_pool_v3_launch(a, cur_stream());
     if (rc >= 0) {
       check_rc(rc, "conv_pool_v3");
