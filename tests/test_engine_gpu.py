@@ -66,13 +66,22 @@ def test_graphed_engine_equals_eager(native_lib):
     eager = eng.run(x, "block4_pool", k=4)
     res = gd.run(x, "block4_pool")  # bucket 4, padded with a zero image
     assert bucket_for(3) == 4 and gd.captured == [("block4_pool", 4)]
-    # padding the batch changes M, which may change the split-K factor of small-M layers (fp32
-    # summation order), so results agree to rounding rather than bit-for-bit
     assert torch.equal(res.filters[:3], eager.filters)
-    assert (res.mosaic[:3].int() - eager.mosaic.int()).abs().max() <= 2
-    x2 = _x8(3, 224, 5).to(torch.bfloat16).cuda()  # replay with new data
-    d = gd.run(x2, "block4_pool").mosaic[:3].int() - eng.run(x2, "block4_pool", k=4).mosaic.int()
-    assert d.abs().max() <= 2
+    # the graph replays exactly the eager computation of the padded batch (bucket 4 = the 3 images +
+    # a zero image); vs the unpadded batch only to rounding: padding changes M, hence the split-K
+    # factor (fp32 summation order) of small-M layers, and a rounding-level change can flip a
+    # near-tied max-pool switch, which moves a few reconstruction pixels (measured: up to 30/255 on
+    # single mosaic pixels, tools/diag_graph.py), so that comparison is on the mean
+    for seed in (4, 5):
+        x = _x8(3, 224, seed).to(torch.bfloat16).cuda()
+        got = gd.run(x, "block4_pool")
+        gm, gf = got.mosaic[:3].clone(), got.filters[:3].clone()
+        pad = eng.run(torch.cat([x, torch.zeros_like(x[:1])]), "block4_pool", k=4)
+        assert torch.equal(gf, pad.filters[:3])
+        assert (gm.int() - pad.mosaic[:3].int()).abs().max() <= 1
+        un = eng.run(x, "block4_pool", k=4)
+        assert torch.equal(gf, un.filters)
+        assert (gm.float() - un.mosaic.float()).abs().mean() < 0.5
 
 
 def test_service_end_to_end_gpu(native_lib):
