@@ -610,6 +610,175 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// KW3: 3x3 / stride 1 / pad 1 forward conv, 256 x 256 tile, where the three kw taps of a kernel row
+// share ONE staged A tile. Output rows are pixels in natural (n, oh, ow) order, so the kw-tap input
+// pixel of output row r is the kw=1 input pixel of output row r + kw - 1: one A tile of 258 rows
+// (output rows m0-1 .. m0+256, each row's kw=1 pixel of input row oh + kh - 1) serves all three
+// taps through a row shift of the fragment reads; the two rows per image row where the shift crosses
+// the image border (ow = 0 for kw = 0, ow = W-1 for kw = 2) are zeroed in registers (the conv's zero
+// padding). A K step is (kernel row kh, 32-channel chunk): A 258 x 64 B + B 3 x 256 x 64 B, i.e.
+// 1.47x fewer staged bytes per FLOP than the plain implicit GEMM (which stages A once per tap), for
+// the 256/512-channel layers whose DMA kernel moves ~9.6 TB/s of staging at 1.1-1.28 PF/s.
+// LDS rows are 64 B with the 16-B chunk XOR-swizzled by bit 2 of the row (q ^ 2((row >> 2) & 1)):
+// conflict-free ds_read_b128 fragment reads for ANY 16-row base (the shifted A reads).
+namespace {
+__device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; }
+}  // namespace
+
+template <int DT, int EPI>
+__global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
+  constexpr int WN = 4, FM = 8, FN = 4, NW = 8;
+  constexpr int BM = 256, BN = 256;
+  constexpr int A_I = 3;                   // A DMA instructions (16 rows each) per wave: 384 >= 258 rows
+  constexpr int B_I = 6;                   // B: 3 kw sub-tiles x 256 rows = 48 instructions
+  constexpr int A_BYTES = A_I * NW * 1024, B_BYTES = 3 * BN * 64;
+  constexpr int STAGE = A_BYTES + B_BYTES;  // 72 KiB
+  static_assert(BM * BN * 2 <= 2 * STAGE, "C tile must fit in the operand stages");
+  typedef typename Vec8<DT>::type v8;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = wgid % tiles_n, tile_m = wgid / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int H = a.H, W = a.W, C = a.C, HW = a.H * a.W;
+
+  const int n_base = (m0 < a.M ? m0 : a.M - 1) / HW;
+  const long long img_elems = (long long)HW * a.x_ld;
+  const long long x_total = (long long)a.N * img_elems;
+  const __amdgpu_buffer_rsrc_t xr =
+      make_rsrc(a.x + (long long)n_base * img_elems, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
+
+  // DMA lanes: 16 rows x 4 chunks per instruction; row group bases are multiples of 16
+  const int lrow = lane >> 2;
+  const int lchunk = (lane & 3) ^ kw3_swz(lrow);
+  int r_pix[A_I], r_oh[A_I];
+#pragma unroll
+  for (int u = 0; u < A_I; ++u) {
+    const int s = (u * NW + wave) * 16 + lrow;  // staged row <-> output row m0 - 1 + s
+    const int m = m0 - 1 + s;
+    const int n = m >= 0 ? m / HW : -1;
+    const bool valid = s < BM + 2 && m >= 0 && m < a.M && n >= n_base;
+    const int rem = m - n * HW;
+    const int oh = rem / W;
+    r_pix[u] = valid ? (n - n_base) * HW + rem : 0;
+    r_oh[u] = valid ? oh : -(1 << 28);
+  }
+  // A-fragment rows whose kw = 0 / kw = 2 neighbour lies in the zero padding
+  uint32_t left = 0, right = 0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ow = (m0 + wm * FM * 16 + i * 16 + (lane & 15)) % W;
+    left |= (ow == 0 ? 1u : 0u) << i;
+    right |= (ow == W - 1 ? 1u : 0u) << i;
+  }
+  const int nch = C / 32;
+  const int nsteps = 3 * nch;
+  auto issue = [&](int step, int buf) {
+    const int kh = step / nch, cc = step - kh * nch;
+    uint8_t* As = smem + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int u = 0; u < A_I; ++u) {
+      const bool ok = (unsigned)(r_oh[u] + kh - 1) < (unsigned)H;
+      const uint32_t voff =
+          ok ? (uint32_t)((((long long)(r_pix[u] + (kh - 1) * W)) * a.x_ld + cc * 32 + lchunk * 8) * 2) : kOOB;
+      dma16(xr, As + (u * NW + wave) * 1024, voff);
+    }
+#pragma unroll
+    for (int u = 0; u < B_I; ++u) {
+      const int v = u * NW + wave;  // kw sub-tile v >> 4, rows (v & 15) * 16 + lrow
+      const int kw = v >> 4, brow = (v & 15) * 16 + lrow;
+      const uint32_t voff =
+          (uint32_t)((((long long)(n0 + brow)) * a.Kpad + (kh * 3 + kw) * C + cc * 32 + lchunk * 8) * 2);
+      dma16(wr, Bs + v * 1024, voff);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q = lane >> 4;
+  const int arow0 = wm * FM * 16 + (lane & 15);
+  const int brow0 = wn * FN * 16 + (lane & 15);
+  const int bswz = ((q ^ kw3_swz(brow0)) << 4);  // brow0 + 16 j: same bit 2
+
+  issue(0, 0);
+  for (int k = 0; k < nsteps; ++k) {
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
+    const uint8_t* As = smem + (k & 1) * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      v8 bf[FN], af[FM];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bf[j] = *reinterpret_cast<const v8*>(Bs + kw * (BN * 64) + (brow0 + j * 16) * 64 + bswz);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int sr = arow0 + i * 16 + kw;
+        af[i] = *reinterpret_cast<const v8*>(As + sr * 64 + ((q ^ kw3_swz(sr)) << 4));
+        if ((kw == 0 && ((left >> i) & 1)) || (kw == 2 && ((right >> i) & 1)))
+          af[i] = __builtin_bit_cast(v8, make_uint4(0u, 0u, 0u, 0u));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bf[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  wait_vm<0>();
+
+  if constexpr (EPI == CONV_E_BF16) {
+    if (a.vec_epi) {
+      __syncthreads();
+      epilogue_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+      return;
+    }
+    if (a.res || a.emask) {
+      epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+      return;
+    }
+  }
+  if (a.accumulate)
+    epilogue<DT, FM, FN, EPI, true>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+  else
+    epilogue<DT, FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+}
+
+// DV_KW3: 0 disables the shared-kw-tap kernel (A/B), 2 forces it for every eligible launch regardless
+// of the grid size (tests: small shapes with many image borders per tile). Read per launch.
+static int kw3_mode() {
+  const char* e = std::getenv("DV_KW3");
+  return e ? std::atoi(e) : 1;
+}
+
+template <int DT, int AMODE, int EPI>
+static int kw3_try(const ConvArgs& a, hipStream_t s) {
+  if constexpr (AMODE != CONV_A_FWD || EPI == CONV_E_POOL) {
+    return -4;
+  } else {
+    if (kw3_mode() == 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH ||
+        a.W != a.OW || a.C % 32 || a.mask || a.ws || a.OCpad % 256 || (long long)a.Kpad < 9LL * a.C)
+      return -4;
+    const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / 256;
+    const long long nwg = (long long)tiles_m * tiles_n;
+    if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
+    hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
+    return (int)hipGetLastError();
+  }
+}
+
 template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI, bool MASK = false,
           bool FP = false, bool KS2 = false>
 static int dma_cfg(const ConvArgs& a, hipStream_t s) {
@@ -676,6 +845,10 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
   const long long cus = num_cus();
   auto nwg = [&](int BM, int BN) { return (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN); };
   if (a.OCpad % 256 == 0 && a.OC > 128) {
+    if (kw3_mode() == 2) {
+      const int rc = kw3_try<DT, AMODE, EPI>(a, s);
+      if (rc != -4) return rc;
+    }
     if constexpr (DT == DT_BF16) {
       if (v == 2) return dma_cfg<DT, 2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
       if (v == 1 && nwg(256, 256) >= cus) return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);
@@ -683,6 +856,10 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
     if (v == 3 || (nwg(256, 256) < cus && nwg(128, 256) >= cus))
       return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
     if (nwg(256, 256) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
+    {  // 3x3 s1 p1 forward: the three kw taps share one staged A tile
+      const int rc = kw3_try<DT, AMODE, EPI>(a, s);
+      if (rc != -4) return rc;
+    }
     // 256 x 256 with register double-buffered fragments: +3% on the big VGG layers (profiles/)
     return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI, false, true>(a, s);
   }

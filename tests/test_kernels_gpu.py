@@ -295,6 +295,42 @@ def test_conv_hs_unpool(native_lib, N, H, W, C, OC, div):
     assert _rel(got, alt) < 1e-2
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,W,C,OC", [(5, 7, 7, 64, 256), (3, 14, 13, 96, 512), (2, 28, 28, 256, 256), (1, 9, 1, 32, 256)])
+def test_conv_kw3_shared_taps(native_lib, monkeypatch, dt, N, H, W, C, OC):
+    """3x3 convs whose three kw taps share one staged A tile (conv_dma_kw3_kernel), forced on small
+    shapes so most tiles cross image rows and images: bf16/fp16 out, f32 out, accumulate, residual
+    + emask epilogues and the fused unpool-out epilogue, vs the fp32 reference."""
+    monkeypatch.setenv("DV_KW3", "2")
+    monkeypatch.setenv("DV_NO_SPLITK", "1")
+    g = torch.Generator().manual_seed(59)
+    x = torch.randn(N, H, W, C, generator=g).to(dt)
+    cw = _cw(OC, C)
+    xd, cwd = x.to(DEV), cw.to_device(DEV, dt)
+    ref = ops.conv2d(x.float(), cw, relu=True)
+    got = ops.conv2d(xd, cwd, relu=True)
+    assert got.dtype == dt and _rel(got, ref) < 1e-2
+    if dt == torch.bfloat16:
+        ref = ops.conv2d(x.float(), cw, relu=False, epilogue="f32")
+        assert _rel(ops.conv2d(xd, cwd, relu=False, epilogue="f32"), ref) < 1e-3
+        base = torch.randn(N, H, W, OC, generator=g).to(dt)
+        out_d = base.to(DEV)
+        ops.conv2d(xd, cwd, relu=False, out=out_d, accumulate=True)
+        out_r = base.float().clone()
+        ops.conv2d(x.float(), cw, relu=False, out=out_r, accumulate=True)
+        assert _rel(out_d, out_r) < 1e-2
+        if H % 2 == 0 and W % 2 == 0:
+            code = torch.randint(0, 4, (N, H, W, OC), generator=g, dtype=torch.uint8)
+            got = ops.conv2d(xd, cwd, relu=True, use_bias=False, unpool_out=code.to(DEV))
+            ref = ops.conv2d(x.float(), cw, relu=True, use_bias=False, unpool_out=code)
+            assert _rel(got, ref) < 1e-2
+    res = torch.randn(N, H, W, OC, generator=g).to(dt)
+    em = torch.randn(N, H, W, OC, generator=g).to(dt)
+    ref = ops.conv2d(x.float(), cw, relu=True, res=res.float(), emask=em.float())
+    got = ops.conv2d(xd, cwd, relu=True, res=res.to(DEV), emask=em.to(DEV))
+    assert _rel(got, ref) < 1e-2
+
+
 def test_conv_unpool_gather(native_lib):
     g = torch.Generator().manual_seed(5)
     K = 2
