@@ -626,14 +626,15 @@ namespace {
 __device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; }
 }  // namespace
 
-template <int DT, int EPI>
+// BN_: 256 (8 waves of 128 x 64) or 128 (8 waves of 64 x 64) output channels per workgroup
+template <int DT, int EPI, bool FP, int BN_ = 256>
 __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
-  constexpr int WN = 4, FM = 8, FN = 4, NW = 8;
-  constexpr int BM = 256, BN = 256;
+  constexpr int BN = BN_, BM = 256, NW = 8;
+  constexpr int WN = BN == 256 ? 4 : 2, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
   constexpr int A_I = 3;                   // A DMA instructions (16 rows each) per wave: 384 >= 258 rows
-  constexpr int B_I = 6;                   // B: 3 kw sub-tiles x 256 rows = 48 instructions
+  constexpr int B_I = 3 * BN / 16 / NW;    // B: 3 kw sub-tiles x BN rows (6 / 3 per wave)
   constexpr int A_BYTES = A_I * NW * 1024, B_BYTES = 3 * BN * 64;
-  constexpr int STAGE = A_BYTES + B_BYTES;  // 72 KiB
+  constexpr int STAGE = A_BYTES + B_BYTES;  // 72 / 48 KiB
   static_assert(BM * BN * 2 <= 2 * STAGE, "C tile must fit in the operand stages");
   typedef typename Vec8<DT>::type v8;
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
@@ -692,7 +693,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
 #pragma unroll
     for (int u = 0; u < B_I; ++u) {
       const int v = u * NW + wave;  // kw sub-tile v >> 4, rows (v & 15) * 16 + lrow
-      const int kw = v >> 4, brow = (v & 15) * 16 + lrow;
+      const int kw = v / (BN / 16), brow = (v % (BN / 16)) * 16 + lrow;
       const uint32_t voff =
           (uint32_t)((((long long)(n0 + brow)) * a.Kpad + (kh * 3 + kw) * C + cc * 32 + lchunk * 8) * 2);
       dma16(wr, Bs + v * 1024, voff);
@@ -716,6 +717,36 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
     if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
     const uint8_t* As = smem + (k & 1) * STAGE;
     const uint8_t* Bs = As + A_BYTES;
+    if constexpr (FP) {
+      // the next kw's B fragments are read before this kw's MFMAs (a full A+B double buffer spills);
+      // each A fragment is read right before its row of MFMAs
+      v8 bf[2][FN];
+      auto ldb = [&](int kw, int b) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bf[b][j] = *reinterpret_cast<const v8*>(Bs + kw * (BN * 64) + (brow0 + j * 16) * 64 + bswz);
+      };
+      ldb(0, 0);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        if (kw < 2) ldb(kw + 1, (kw + 1) & 1);
+        v8 af[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int sr = arow0 + i * 16 + kw;
+          af[i] = *reinterpret_cast<const v8*>(As + sr * 64 + ((q ^ kw3_swz(sr)) << 4));
+          if ((kw == 0 && ((left >> i) & 1)) || (kw == 2 && ((right >> i) & 1)))
+            af[i] = __builtin_bit_cast(v8, make_uint4(0u, 0u, 0u, 0u));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bf[kw & 1][j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      continue;
+    }
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       v8 bf[FN], af[FM];
@@ -763,18 +794,24 @@ static int kw3_mode() {
   return e ? std::atoi(e) : 1;
 }
 
-template <int DT, int AMODE, int EPI>
+template <int DT, int AMODE, int EPI, int BN = 256>
 static int kw3_try(const ConvArgs& a, hipStream_t s) {
   if constexpr (AMODE != CONV_A_FWD || EPI == CONV_E_POOL) {
     return -4;
   } else {
     if (kw3_mode() == 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH ||
-        a.W != a.OW || a.C % 32 || a.mask || a.ws || a.OCpad % 256 || (long long)a.Kpad < 9LL * a.C)
+        a.W != a.OW || a.C % 32 || a.mask || a.ws || a.OCpad % BN || (long long)a.Kpad < 9LL * a.C)
       return -4;
-    const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / 256;
+    const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / BN;
     const long long nwg = (long long)tiles_m * tiles_n;
     if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
-    hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
+    // DV_KW3_FP=1: B fragments double-buffered across the kw sub-steps (measured equal to the plain
+    // loop, profiles/layers_r1_kw3_{nofp,on}.txt; a full A+B double buffer spills)
+    const char* fp = std::getenv("DV_KW3_FP");
+    if (fp != nullptr && std::atoi(fp) != 0)
+      hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, true, BN>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
+    else
+      hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, false, BN>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
     return (int)hipGetLastError();
   }
 }
@@ -867,6 +904,10 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
     if constexpr (DT == DT_BF16) {
       if (v == 1) return dma_cfg<DT, 4, 2, 4, 4, 64, 2, AMODE, EPI>(a, s);
       if (v == 4 && nwg(256, 128) >= cus) return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI, false, true>(a, s);
+    }
+    if (kw3_mode() == 2 || nwg(256, 128) >= cus) {  // 3x3 s1 p1 forward: shared-kw-tap 256 x 128 tile
+      const int rc = kw3_try<DT, AMODE, EPI, 128>(a, s);
+      if (rc != -4) return rc;
     }
     if (nwg(256, 128) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
     if (ks2_on()) return dma_cfg<DT, 2, 2, 8, 4, 64, 3, AMODE, EPI, false, false, true>(a, s);  // 256 x 128, KS2

@@ -296,7 +296,8 @@ def test_conv_hs_unpool(native_lib, N, H, W, C, OC, div):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("N,H,W,C,OC", [(5, 7, 7, 64, 256), (3, 14, 13, 96, 512), (2, 28, 28, 256, 256), (1, 9, 1, 32, 256)])
+@pytest.mark.parametrize("N,H,W,C,OC", [(5, 7, 7, 64, 256), (3, 14, 13, 96, 512), (2, 28, 28, 256, 256), (1, 9, 1, 32, 256),
+                                        (4, 10, 9, 64, 128), (2, 56, 56, 256, 128)])
 def test_conv_kw3_shared_taps(native_lib, monkeypatch, dt, N, H, W, C, OC):
     """3x3 convs whose three kw taps share one staged A tile (conv_dma_kw3_kernel), forced on small
     shapes so most tiles cross image rows and images: bf16/fp16 out, f32 out, accumulate, residual
