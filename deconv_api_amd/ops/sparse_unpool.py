@@ -170,3 +170,27 @@ def smfmac_counts(M: int, Co: int, Ci: int):
     dense = M * Ci * 9 * Co // (32 * 32 * 16)
     sparse = M * Ci * (Co // CHUNK) * STEPS * KSTEP // (32 * 32 * 32)
     return dense, sparse
+
+
+def pack_for_kernel(w_oihw: torch.Tensor, device=None) -> torch.Tensor:
+    """Packed weights in the HIP kernel's layout: [4 phases, C/16, Ci, 160] bf16 (K-contiguous rows,
+    one 320-byte row per output channel, staged verbatim into the kernel's LDS B tile)."""
+    p = pack_phase_weights(w_oihw.float().cpu())
+    return p.permute(0, 1, 3, 2).contiguous().to(device=device, dtype=torch.bfloat16)
+
+
+def sparse_unpool_conv(v: torch.Tensor, code: torch.Tensor, wt: torch.Tensor, code_div: int = 1,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """ReLU(convT(ReLU(unpool(v, code)), W)) on the GPU via csrc/conv_sparse.hip (bf16 NHWC).
+    ``wt`` comes from :func:`pack_for_kernel`; ``code`` is shared by ``code_div`` consecutive
+    images (the B*K filter batch). CPU tensors take :func:`sparse_unpool_conv_ref`."""
+    if not v.is_cuda:
+        raise ValueError("sparse_unpool_conv: device op (use sparse_unpool_conv_ref on CPU)")
+    from . import native
+
+    NB, PH, PW, C = v.shape
+    Ci = wt.shape[2]
+    if out is None:
+        out = torch.empty(NB, 2 * PH, 2 * PW, Ci, dtype=torch.bfloat16, device=v.device)
+    native.lib().sparse_unpool_conv(v.contiguous(), code.contiguous(), wt, out, code_div)
+    return out
