@@ -27,7 +27,9 @@ typedef __attribute__((ext_vector_type(8))) uint32_t u32x8;
 
 namespace {
 constexpr int SP_BM = 128, SP_BN = 128, SP_KC = 160, SP_LDB = 168, SP_LDO = 136;
-constexpr int SP_PX = 256;  // staged pooled pixels per chunk: 128 + PW + 1, PW <= 127
+constexpr int SP_PX = 256;
+// wave tile: SP_MI x SP_NJ blocks of 32x32; 4 waves as (4 / SP_WN) x SP_WN over the 128 x 128 tile
+constexpr int SP_MI = 1, SP_NJ = 4, SP_WN = 1;  // staged pooled pixels per chunk: 128 + PW + 1, PW <= 127
 
 __device__ __forceinline__ uint32_t relu_bf(uint32_t x) { return (x & 0x8000u) ? 0u : x; }
 
@@ -79,7 +81,7 @@ __global__ void __launch_bounds__(256, 1)
   __shared__ __attribute__((aligned(16))) uint32_t sAv[2][SP_PX * 10];
   __shared__ __attribute__((aligned(16))) uint32_t sAk[2][SP_PX * 5];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave / SP_WN, wn = wave % SP_WN;
   const int h = lane >> 5, r32 = lane & 31;
   const int ph = blockIdx.z, a = ph >> 1, b = ph & 1;
   const int da = a ? 1 : -1, db = b ? 1 : -1;
@@ -96,11 +98,11 @@ __global__ void __launch_bounds__(256, 1)
   const int lo = min(min(sh[0], sh[1]), min(sh[2], sh[3])), hi = max(max(sh[0], sh[1]), max(sh[2], sh[3]));
   const int npx = SP_BM + hi - lo;
   const long long base = m0 + lo;
-  int L[2][4];
-  bool ok[2][4];
+  int L[SP_MI][4];
+  bool ok[SP_MI][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long long P = m0 + 64 * wm + 32 * i + r32;
+  for (int i = 0; i < SP_MI; ++i) {
+    const long long P = m0 + 32 * SP_MI * wm + 32 * i + r32;
     const bool valid = P < Mp;
     const long long Pc = valid ? P : 0;
     const int n = (int)(Pc / ((long long)PH * PW));
@@ -110,7 +112,7 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       ok[i][t] = valid && ys[t] >= 0 && ys[t] < PH && xs[t] >= 0 && xs[t] < PW;
-      L[i][t] = 64 * wm + 32 * i + r32 + sh[t] - lo;
+      L[i][t] = 32 * SP_MI * wm + 32 * i + r32 + sh[t] - lo;
     }
   }
   u32x4 areg[3];
@@ -170,11 +172,11 @@ __global__ void __launch_bounds__(256, 1)
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[SP_MI][SP_NJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < SP_MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    for (int j = 0; j < SP_NJ; ++j) acc[i][j] = f32x16{};
 
   load_b(0);
   store_b(0);
@@ -190,12 +192,12 @@ __global__ void __launch_bounds__(256, 1)
     }
     // this lane's operands from the staged chunk: centre/row/col channel pairs at {2h, 4+2h, 8+2h,
     // 12+2h}, corner quads at {4h, 8+4h}
-    uint32_t xv[2][3][4], kv[2][3][4], kd[2][2];
-    uint2 xd[2][2];
+    uint32_t xv[SP_MI][3][4], kv[SP_MI][3][4], kd[SP_MI][2];
+    uint2 xd[SP_MI][2];
     const uint32_t* av_s = sAv[ch & 1];
     const uint32_t* ak_s = sAk[ch & 1];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < SP_MI; ++i) {
 #pragma unroll
       for (int t = 0; t < 3; ++t)
 #pragma unroll
@@ -212,10 +214,10 @@ __global__ void __launch_bounds__(256, 1)
     const uint16_t* bb = sB[ch & 1];
 #pragma unroll
     for (int step = 0; step < 5; ++step) {
-      bf16x16 bf[2];
+      bf16x16 bf[SP_NJ];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint16_t* src = bb + (64 * wn + 32 * j + r32) * SP_LDB + step * 32 + h * 16;
+      for (int j = 0; j < SP_NJ; ++j) {
+        const uint16_t* src = bb + (32 * SP_NJ * wn + 32 * j + r32) * SP_LDB + step * 32 + h * 16;
         u32x8 t;
         const u32x4 lo = *reinterpret_cast<const u32x4*>(src), hi = *reinterpret_cast<const u32x4*>(src + 8);
         t.s0123 = lo;
@@ -223,7 +225,7 @@ __global__ void __launch_bounds__(256, 1)
         bf[j] = __builtin_bit_cast(bf16x16, t);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < SP_MI; ++i) {
         uint32_t aw[4];
         uint32_t idx;
         if (step < 2) {  // S1: groups (2h,2h+1) <- pair j=2*step, groups (4+2h,5+2h) <- pair 2*step+1
@@ -246,7 +248,7 @@ __global__ void __launch_bounds__(256, 1)
         const u32x4 av = {aw[0], aw[1], aw[2], aw[3]};
         const bf16x8 af = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < SP_NJ; ++j)
           acc[i][j] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(af, bf[j], acc[i][j], (int)idx, 0, 0);
       }
     }
@@ -260,13 +262,13 @@ __global__ void __launch_bounds__(256, 1)
   // ---- epilogue: ReLU -> bf16 via LDS -> 16-byte rows of the phase's output pixels ----
   uint16_t* sO = &sB[0][0];  // 128 x 136 bf16 = 34.8 KB, fits in buffer 0 (+1)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < SP_MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < SP_NJ; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int row = 64 * wm + 32 * i + (e >> 2) * 8 + h * 4 + (e & 3);
-        const int col = 64 * wn + 32 * j + r32;
+        const int row = 32 * SP_MI * wm + 32 * i + (e >> 2) * 8 + h * 4 + (e & 3);
+        const int col = 32 * SP_NJ * wn + 32 * j + r32;
         sO[row * SP_LDO + col] = f2bf(fmaxf(acc[i][j][e], 0.f));
       }
   __syncthreads();
