@@ -306,29 +306,58 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   finish_stats();
 }
 
-// kind 0 max / 1 avg; dir 0 fwd (in=x, out=y) / 1 bwd (in=gy, out=gx); geom = N,H,W,C,OH,OW,k,s,pad
-void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_t dir, std::vector<int64_t> g) {
+// kind 0 max / 1 avg; dir 0 fwd (in=x, out=y) / 1 bwd (in=gy, out=gx); geom = N,H,W,C,OH,OW,k,s,pad.
+// x/gx and y/gy may be channel-slice views (dense pixels, channel stride 1, pixel stride % 8 == 0):
+// the InceptionV3 blocks pool straight out of / into their concat buffers. avgpool fwd may add a
+// per-channel fp32 bias and apply ReLU (the block's pool branch with its 1x1 conv commuted first).
+static int64_t pix_ld(const Tensor& t, int64_t H, int64_t W, int64_t C, const char* name) {
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, name, ": NHWC with channel stride 1");
+  const int64_t ld = t.stride(2);
+  TORCH_CHECK(ld >= C && ld % 8 == 0 && t.stride(1) == W * ld && t.stride(0) == H * W * ld &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, ": dense pixels with a pixel stride % 8 == 0, 16-B aligned");
+  return ld;
+}
+
+void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_t dir, std::vector<int64_t> g,
+          c10::optional<Tensor> bias, bool relu) {
   check_cuda(in, "in");
+  check_cuda(out, "out");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(in.device());
   TORCH_CHECK(g.size() == 9, "pool: geometry");
   const int64_t N = g[0], H = g[1], W = g[2], C = g[3], OH = g[4], OW = g[5], k = g[6], s = g[7], pad = g[8];
   TORCH_CHECK(C % 8 == 0 && k >= 1 && s >= 1 && pad >= 0 && pad < k, "pool: C%8, k, s, pad");
   TORCH_CHECK(OH == (H + 2 * pad - k) / s + 1 && OW == (W + 2 * pad - k) / s + 1, "pool: output size");
   const auto dt = in.scalar_type();
-  TORCH_CHECK((dt == at::kBFloat16 || dt == at::kHalf) && in.is_contiguous() && out.scalar_type() == dt &&
-                  out.is_contiguous(),
-              "pool: bf16 or fp16 contiguous tensors of one dtype");
-  const int64_t small = N * OH * OW * C, big = N * H * W * C;
-  TORCH_CHECK(in.numel() == (dir == 0 ? big : small) && out.numel() == (dir == 0 ? small : big), "pool: sizes");
+  TORCH_CHECK((dt == at::kBFloat16 || dt == at::kHalf) && out.scalar_type() == dt, "pool: bf16 or fp16, one dtype");
+  const Tensor& full = dir == 0 ? in : out;
+  const Tensor& pooled = dir == 0 ? out : in;
+  TORCH_CHECK(full.size(0) == N && full.size(1) == H && full.size(2) == W && full.size(3) == C, "pool: x shape");
+  TORCH_CHECK(pooled.size(0) == N && pooled.size(1) == OH && pooled.size(2) == OW && pooled.size(3) == C,
+              "pool: y shape");
+  const int64_t x_ld = pix_ld(full, H, W, C, "pool x"), y_ld = pix_ld(pooled, OH, OW, C, "pool y");
+  need(full, ((N * H * W - 1) * x_ld + C) * 2, "pool x");
+  need(pooled, ((N * OH * OW - 1) * y_ld + C) * 2, "pool y");
   uint8_t* ip = nullptr;
   if (kind == 0) {
-    TORCH_CHECK(idx.has_value() && idx->scalar_type() == at::kByte && idx->is_contiguous() && idx->numel() == small,
+    TORCH_CHECK(idx.has_value() && idx->scalar_type() == at::kByte && idx->is_contiguous() &&
+                    idx->numel() == N * OH * OW * C,
                 "maxpool: idx [N,OH,OW,C] u8");
     ip = idx->data_ptr<uint8_t>();
   }
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(kind == 1 && dir == 0 && bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
+                    bias->numel() >= C,
+                "pool bias: avgpool forward, fp32 [>= C]");
+    bp = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(!relu || (kind == 1 && dir == 0), "pool relu: avgpool forward only");
   check_rc(dv::pool_launch((int)kind, (int)dir, reinterpret_cast<const uint16_t*>(in.data_ptr()),
                            reinterpret_cast<uint16_t*>(out.data_ptr()), ip, (int)N, (int)H, (int)W, (int)C, (int)OH,
-                           (int)OW, (int)k, (int)s, (int)pad, dt == at::kHalf ? dv::DT_F16 : dv::DT_BF16, cur_stream()),
+                           (int)OW, (int)k, (int)s, (int)pad, dt == at::kHalf ? dv::DT_F16 : dv::DT_BF16, cur_stream(),
+                           x_ld, y_ld, bp, relu ? 1 : 0),
            "pool");
 }
 
@@ -580,7 +609,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mask"), py::arg("geom"), py::arg("amode"), py::arg("epi"), py::arg("impl"),
         py::arg("res") = py::none(), py::arg("emask") = py::none(), py::arg("stats") = py::none(),
         py::arg("stats_div") = 1, py::arg("ucode") = py::none(), py::arg("ucode_div") = 1);
-  m.def("pool", &pool, "k x k max/avg pooling forward/backward");
+  m.def("dma_tune", [](int64_t cfg, int64_t ks) { dv::conv_dma_tune((int)cfg, (int)ks); },
+        "force the LDS-DMA conv tile config / split-K factor (0 = automatic); tuning only");
+  m.def("pool", &pool, "k x k max/avg pooling forward/backward", py::arg("in"), py::arg("out"), py::arg("idx"),
+        py::arg("kind"), py::arg("dir"), py::arg("geom"), py::arg("bias") = py::none(), py::arg("relu") = false);
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");

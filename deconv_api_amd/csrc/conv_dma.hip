@@ -443,8 +443,11 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
       for (int r = 0; r < 4; ++r) {
         const int row = mw + i * 16 + row_l + r;
         if (row >= a.M) continue;
-        float v = acc[i][j][r] + bias + to_f<DT>(rv[i][r]);
-        if (a.relu) v = fmaxf(v, 0.f);
+        float v = acc[i][j][r] + bias;
+        if (a.relu && !a.res) v = fmaxf(v, 0.f);  // same order as epilogue_lds
+        v += to_f<DT>(rv[i][r]);
+        if (a.accumulate) v += to_f<DT>(out[(long long)row * a.out_ld + col]);
+        if (a.relu && a.res) v = fmaxf(v, 0.f);
         const uint32_t e = ev[i][r];
         if (e == 0u || (e & 0x8000u)) v = 0.f;
         out[(long long)row * a.out_ld + col] = from_f<DT>(v);
@@ -871,11 +874,40 @@ static int num_cus() {
   return n;
 }
 
+// Tuning override (tools/tune_dma.py): force tile config `g_cfg` (> 0) and split-K factor
+// `g_ks` (> 0) for every DMA conv launch until reset to 0. Host-side globals, set between launches.
+static int g_cfg = 0, g_ks = 0;
+void conv_dma_tune(int cfg, int ks) {
+  g_cfg = cfg;
+  g_ks = ks;
+}
+
+// every tile config the DMA kernel is instantiated with; -5 = config does not fit this problem
+template <int DT, int AMODE, int EPI>
+static int dma_forced(const ConvArgs& a, hipStream_t s, int cfg) {
+  auto okn = [&](int bn) { return a.OCpad % bn == 0; };
+  switch (cfg) {
+    case 1: return okn(256) ? dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI, false, true>(a, s) : -5;  // 256x256
+    case 2: return okn(256) ? dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s) : -5;               // 128x256
+    case 3: return okn(128) ? dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s) : -5;               // 128x128
+    case 4: return okn(128) ? dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s) : -5;               // 256x128
+    case 5: return okn(64) ? dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, EPI>(a, s) : -5;                // 256x64
+    case 6: return okn(64) ? dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s) : -5;                // 512x64
+    case 7: return okn(64) ? dma_cfg<DT, 4, 1, 2, 4, 64, 3, AMODE, EPI>(a, s) : -5;                // 128x64, 4 waves
+    case 8: return okn(64) ? dma_cfg<DT, 2, 2, 2, 2, 64, 3, AMODE, EPI>(a, s) : -5;                // 64x64, 4 waves
+    case 9: return okn(128) ? dma_cfg<DT, 2, 2, 4, 4, 64, 2, AMODE, EPI>(a, s) : -5;               // 128x128, 4 waves
+    case 10: return okn(128) ? dma_cfg<DT, 2, 2, 2, 4, 64, 3, AMODE, EPI>(a, s) : -5;              // 64x128, 4 waves
+    case 11: return okn(64) ? dma_cfg<DT, 4, 1, 4, 4, 64, 2, AMODE, EPI>(a, s) : -5;               // 256x64, 4 waves
+    default: return -5;
+  }
+}
+
 // Tile choice: the largest tile (best MFMA:LDS ratio) unless it leaves CUs idle. A problem with
 // fewer big tiles than the chip has CUs (deep layers at small batch, strong-scaled tiles) drops to
 // the next smaller tile, which doubles the workgroup count and fits 2 workgroups per CU in LDS.
 template <int DT, int AMODE, int EPI>
 static int dma_bn(const ConvArgs& a, hipStream_t s) {
+  if (g_cfg > 0) return dma_forced<DT, AMODE, EPI>(a, s, g_cfg);
   // measured (profiles/layers_r1_pipeline.txt): BK=32 x 4-stage rings lose to 2-stage BK=64 on the
   // 256x256 and 512x64 tiles; the 3-stage BK=64 ring wins slightly on 256x128.
   const int v = DT == DT_BF16 ? dma_variant() : 0;  // A/B variants are bf16-only
@@ -970,6 +1002,7 @@ static void dma_tile_dims(const ConvArgs& a, bool mask, int& BM, int& BN) {
 // Split-K factor for a launch that would leave most CUs idle: small M (batch-1 serving, deep
 // layers of strong-scaled DeepDream tiles, dense layers) with a long K. 1 = no split.
 int conv_dma_splitk(const ConvArgs& a) {
+  if (g_ks > 0) return std::min(g_ks, a.Kpad / 64);
   if (std::getenv("DV_NO_SPLITK")) return 1;
   int BM, BN;
   dma_tile_dims(a, a.mask != nullptr, BM, BN);

@@ -59,6 +59,8 @@ int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream)
 int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
 // split-K planning (1 = none) and the reduction epilogue (bias, ReLU, 16-bit / fp32 out)
 int conv_dma_splitk(const ConvArgs& a);
+// tuning override: force DMA tile config cfg (> 0, conv_dma.hip:dma_forced) and split-K ks (> 0); 0 = auto
+void conv_dma_tune(int cfg, int ks);
 int splitk_reduce_launch(const ConvArgs& a, int epi, hipStream_t stream);
 
 // ---- misc kernels (misc.hip) ----
@@ -96,7 +98,8 @@ namespace dv {
 // k x k pooling (pool.hip). kind 0 max (idx = uint8 window position), 1 avg (count_include_pad=0);
 // dir 0 forward (in = x [N,H,W,C], out = y [N,OH,OW,C]), 1 backward (in = gy, out = gx)
 int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C,
-                int OH, int OW, int k, int s, int pad, int dtype, hipStream_t st);
+                int OH, int OW, int k, int s, int pad, int dtype, hipStream_t st, long long x_ld = 0,
+                long long y_ld = 0, const float* bias = nullptr, int relu = 0);
 // DeepDream loss: per-(image, block) partial sums of x^2 over the map minus a b-pixel border
 // (part [N][parts]), and its gradient gx = 2*scale[n]*x in the core, 0 on the border
 int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, int W, int C, int b, int dtype,

@@ -11,6 +11,10 @@ namespace dv {
 
 struct PoolGeom {
   int N, H, W, C, OH, OW, k, s, pad;
+  long long x_ld, y_ld;  // elements between consecutive pixels of the full-res (x / gx) and pooled (y / gy)
+                         // maps: channel-slice views of concat buffers (InceptionV3 blocks)
+  const float* bias;     // avgpool fwd: + bias[c] (the commuted 1x1 conv's bias), or null
+  int relu;              // avgpool fwd: ReLU on the output
 };
 
 template <int DT>
@@ -37,7 +41,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
       for (int kw = 0; kw < g.k; ++kw) {
         const int iw = ow * g.s - g.pad + kw;
         if ((unsigned)iw >= (unsigned)g.W) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.C + ch * 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.x_ld + ch * 8);
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
         const int pos = kh * g.k + kw;
 #pragma unroll
@@ -55,7 +59,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
     o.y = pack2<DT>(best[2], best[3]);
     o.z = pack2<DT>(best[4], best[5]);
     o.w = pack2<DT>(best[6], best[7]);
-    *reinterpret_cast<uint4*>(y + pix * g.C + ch * 8) = o;
+    *reinterpret_cast<uint4*>(y + pix * g.y_ld + ch * 8) = o;
     uint2 ix;
     ix.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
     ix.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
@@ -85,9 +89,9 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
         const int kw = w + g.pad - ow * g.s;
         if (kw < 0 || kw >= g.k) continue;
         const uint32_t pos = (uint32_t)(kh * g.k + kw);
-        const long long o = ((n * g.OH + oh) * g.OW + ow) * g.C + ch * 8;
-        const uint4 v = *reinterpret_cast<const uint4*>(gy + o);
-        const uint2 ix = *reinterpret_cast<const uint2*>(idx + o);
+        const long long op = (n * g.OH + oh) * g.OW + ow;
+        const uint4 v = *reinterpret_cast<const uint4*>(gy + op * g.y_ld + ch * 8);
+        const uint2 ix = *reinterpret_cast<const uint2*>(idx + op * g.C + ch * 8);
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -101,7 +105,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
     o.y = pack2<DT>(acc[2], acc[3]);
     o.z = pack2<DT>(acc[4], acc[5]);
     o.w = pack2<DT>(acc[6], acc[7]);
-    *reinterpret_cast<uint4*>(gx + pix * g.C + ch * 8) = o;
+    *reinterpret_cast<uint4*>(gx + pix * g.x_ld + ch * 8) = o;
   }
 }
 
@@ -128,19 +132,24 @@ __global__ void __launch_bounds__(256) avgpool_fwd_kernel(const uint16_t* __rest
       for (int kw = 0; kw < g.k; ++kw) {
         const int iw = ow * g.s - g.pad + kw;
         if ((unsigned)iw >= (unsigned)g.W) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.C + ch * 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.x_ld + ch * 8);
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
       }
     }
     const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, g.k, g.H) * win_count(ow, g.s, g.pad, g.k, g.W));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc[e] = acc[e] * inv + (g.bias ? g.bias[ch * 8 + e] : 0.f);
+      if (g.relu) acc[e] = fmaxf(acc[e], 0.f);
+    }
     uint4 o;
-    o.x = pack2<DT>(acc[0] * inv, acc[1] * inv);
-    o.y = pack2<DT>(acc[2] * inv, acc[3] * inv);
-    o.z = pack2<DT>(acc[4] * inv, acc[5] * inv);
-    o.w = pack2<DT>(acc[6] * inv, acc[7] * inv);
-    *reinterpret_cast<uint4*>(y + pix * g.C + ch * 8) = o;
+    o.x = pack2<DT>(acc[0], acc[1]);
+    o.y = pack2<DT>(acc[2], acc[3]);
+    o.z = pack2<DT>(acc[4], acc[5]);
+    o.w = pack2<DT>(acc[6], acc[7]);
+    *reinterpret_cast<uint4*>(y + pix * g.y_ld + ch * 8) = o;
   }
 }
 
@@ -165,7 +174,7 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __rest
         const int kw = w + g.pad - ow * g.s;
         if (kw < 0 || kw >= g.k) continue;
         const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, g.k, g.H) * win_count(ow, g.s, g.pad, g.k, g.W));
-        const uint4 v = *reinterpret_cast<const uint4*>(gy + ((n * g.OH + oh) * g.OW + ow) * g.C + ch * 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(gy + ((n * g.OH + oh) * g.OW + ow) * g.y_ld + ch * 8);
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += inv * to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
@@ -176,7 +185,7 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __rest
     o.y = pack2<DT>(acc[2], acc[3]);
     o.z = pack2<DT>(acc[4], acc[5]);
     o.w = pack2<DT>(acc[6], acc[7]);
-    *reinterpret_cast<uint4*>(gx + pix * g.C + ch * 8) = o;
+    *reinterpret_cast<uint4*>(gx + pix * g.x_ld + ch * 8) = o;
   }
 }
 
@@ -202,9 +211,13 @@ static int pool_dt(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t
 }
 
 int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C, int OH,
-                int OW, int k, int s, int pad, int dtype, hipStream_t st) {
+                int OW, int k, int s, int pad, int dtype, hipStream_t st, long long x_ld, long long y_ld,
+                const float* bias, int relu) {
   if (C % 8 != 0 || k <= 0 || s <= 0 || k > 15) return -1;
-  const PoolGeom g{N, H, W, C, OH, OW, k, s, pad};
+  if (x_ld <= 0) x_ld = C;
+  if (y_ld <= 0) y_ld = C;
+  if (x_ld % 8 || y_ld % 8 || x_ld < C || y_ld < C) return -1;
+  const PoolGeom g{N, H, W, C, OH, OW, k, s, pad, x_ld, y_ld, bias, relu};
   return dtype == DT_F16 ? pool_dt<DT_F16>(kind, dir, in, out, idx, g, st)
                          : pool_dt<DT_BF16>(kind, dir, in, out, idx, g, st);
 }

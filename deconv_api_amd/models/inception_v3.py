@@ -10,11 +10,20 @@ deepest requested layer (DeepDream's loss never reaches mixed6..mixed10).
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Iterable, List, Optional
 
 import torch
 
 from ..ops.autograd import ConvUnit, avg_pool, cat_channels, max_pool
+from ..ops.inception import InceptionBlock
+from ..runtime.streams import run_parallel
+
+# DV_BRANCH_STREAMS=1: unfused blocks run their branches on side streams (measured no gain in a
+# graph: the launches already fill the CUs, profiles/kstats_c3_streams.txt); DV_INCEPTION_FUSED=0:
+# per-op autograd units + torch.cat instead of the one-node blocks of ops/inception.py (A/B)
+BRANCH_STREAMS = os.environ.get("DV_BRANCH_STREAMS", "0") != "0"
+FUSED_BLOCKS = os.environ.get("DV_INCEPTION_FUSED", "1") != "0"
 
 MIXED = [f"mixed{i}" for i in range(11)]
 
@@ -34,6 +43,7 @@ class InceptionV3:
         self._n = 0
         self.device = torch.device("cpu")
         self._define()
+        self.iblocks = [InceptionBlock(name, order, br, self.units) for name, order, br in self.blocks]
 
     # ----------------------------------------------------------------- definition
     def _conv(self, cin, cout, kh, kw, stride=1, padding="same") -> str:
@@ -115,7 +125,12 @@ class InceptionV3:
         for bi, (name, order, br) in enumerate(self.blocks):
             if bi > last:
                 break
-            x = cat_channels([self._branch(x, br[k]) for k in order])
+            if x.is_cuda and FUSED_BLOCKS:
+                x = self.iblocks[bi](x)
+            elif x.is_cuda and BRANCH_STREAMS:
+                x = cat_channels(run_parallel([lambda xx, ops_=br[k]: self._branch(xx, ops_) for k in order], x))
+            else:
+                x = cat_channels([self._branch(x, br[k]) for k in order])
             if name in want:
                 out[name] = x
         return out

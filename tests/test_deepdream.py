@@ -268,3 +268,36 @@ def test_gpu_bottleneck_block_grad(native_lib, stride, proj, premasked):
     (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.bfloat16).cuda())
     a, b = gd.float().cpu().flatten().double(), gc.flatten().double()
     assert float(a @ b / (a.norm() * b.norm())) > 0.99
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bi,hw", [(0, 11), (3, 11), (4, 9), (8, 9), (9, 5)])
+@pytest.mark.parametrize("premasked", [False, True])
+def test_gpu_inception_block_grad(native_lib, bi, hw, premasked):
+    """One-node InceptionV3 mixed block (direct concat-slice writes, commuted avg-pool branch,
+    accumulate/emask epilogues) vs CPU autograd of the unfused block: mixed0 (A), mixed3 (B),
+    mixed4 (C), mixed8 (D, strided + max), mixed9 (E, split convs)."""
+    from deconv_api_amd.ops import autograd as AG
+
+    cpu, gpu = InceptionV3(0).build("cpu"), InceptionV3(0).build("cuda")
+    cin = [192, 256, 288, 288, 768, 768, 768, 768, 768, 1280, 2048][bi]
+    g = torch.Generator().manual_seed(bi + 17 * premasked)
+    x = torch.randn(2, hw, hw, cin, generator=g).clamp_min(0).to(torch.bfloat16).float()
+    xc = x.clone().requires_grad_(True)
+    yc = cpu.iblocks[bi](xc)
+    gy = torch.randn(*yc.shape, generator=g)
+    if premasked:
+        gy = gy * (yc.detach() > 0)
+    (gc,) = torch.autograd.grad(yc, xc, gy)
+    if premasked:
+        gc = gc * (x > 0)
+    xd = x.to(torch.bfloat16).cuda().requires_grad_(True)
+    if premasked:
+        with AG.premasked_grads():
+            yd = gpu.iblocks[bi](AG.tag_relu_output(xd))
+    else:
+        yd = gpu.iblocks[bi](xd)
+    assert yd.shape == yc.shape
+    assert _cos(yd.float().cpu(), yc.detach()) > 0.999
+    (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.bfloat16).cuda())
+    assert _cos(gd.float().cpu(), gc) > 0.995

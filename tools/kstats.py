@@ -44,7 +44,19 @@ def main(argv=None):
         lo = s if lo is None else min(lo, s)
         hi = e if hi is None else max(hi, e)
     span = (hi - lo) / 1e3 if lo is not None else 0.0
-    print(f"window: {span / 1e3:.1f} ms wall, {busy / 1e3:.1f} ms kernel-busy ({100 * busy / max(span, 1e-9):.0f}%)")
+    # union of dispatch intervals (busy above double-counts kernels that run concurrently)
+    ev = sorted((s, e) for _, s, e, _, _ in rows if s >= cut)
+    union = 0.0
+    cs, ce = (ev[0] if ev else (0, 0))
+    for s, e in ev[1:]:
+        if s > ce:
+            union += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    union = (union + ce - cs) / 1e3
+    print(f"window: {span / 1e3:.1f} ms wall, {busy / 1e3:.1f} ms kernel-busy ({100 * busy / max(span, 1e-9):.0f}%), "
+          f"{union / 1e3:.1f} ms with >= 1 kernel in flight (concurrency {busy / max(union, 1e-9):.2f}x)")
     print(f"{'total_ms':>9} {'%':>5} {'calls':>7} {'avg_us':>8}  kernel")
     for name, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
         print(f"{us / 1e3:9.2f} {100 * us / busy:5.1f} {n:7d} {us / n:8.1f}  {name}")
