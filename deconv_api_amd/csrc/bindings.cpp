@@ -393,6 +393,39 @@ void sumsq_core_bwd(Tensor x, Tensor scale, Tensor gx, int64_t b) {
            "sumsq_core_bwd");
 }
 
+// Fused DeepDream update (engine/deepdream.py): g [N,H,W,8] 16-bit input gradient, x [N,H,W,3] fp32
+// master image (updated in place), xin [N,H,W,8] next network input, gpart [N, P] scratch, lpart
+// [L, N, LP] sumsq partials of the L loss layers, lcoef [L] fp32 coefficient / numel, done u8 [N],
+// loss fp32 [N]; max_loss < 0 disables the early stop.
+void dream_update(Tensor g, Tensor x, Tensor xin, Tensor gpart, Tensor lpart, Tensor lcoef, Tensor done, Tensor loss,
+                  double step, double max_loss) {
+  check_cuda(g, "g");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  TORCH_CHECK(g.dim() == 4 && g.size(3) == 8 && g.is_contiguous(), "dream_update: g [N,H,W,8] contiguous");
+  const int64_t N = g.size(0), H = g.size(1), W = g.size(2);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(0) == N && x.size(1) == H &&
+                  x.size(2) == W && x.size(3) == 3,
+              "dream_update: x fp32 [N,H,W,3] contiguous");
+  TORCH_CHECK(xin.sizes() == g.sizes() && xin.scalar_type() == g.scalar_type() && xin.is_contiguous(),
+              "dream_update: xin like g");
+  TORCH_CHECK(gpart.scalar_type() == at::kFloat && gpart.is_contiguous() && gpart.dim() == 2 && gpart.size(0) == N,
+              "dream_update: gpart fp32 [N, P]");
+  TORCH_CHECK(lpart.scalar_type() == at::kFloat && lpart.is_contiguous() && lpart.dim() == 3 && lpart.size(1) == N,
+              "dream_update: lpart fp32 [L, N, LP]");
+  TORCH_CHECK(lcoef.scalar_type() == at::kFloat && lcoef.is_contiguous() && lcoef.numel() == lpart.size(0),
+              "dream_update: lcoef fp32 [L]");
+  TORCH_CHECK(done.scalar_type() == at::kByte && done.is_contiguous() && done.numel() == N, "dream_update: done u8 [N]");
+  TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.is_contiguous() && loss.numel() == N, "dream_update: loss [N]");
+  for (const Tensor* t : {&x, &xin, &gpart, &lpart, &lcoef, &done, &loss}) check_cuda(*t, "dream_update operand");
+  check_rc(dv::dream_update_launch(reinterpret_cast<const uint16_t*>(g.data_ptr()), x.data_ptr<float>(),
+                                   reinterpret_cast<uint16_t*>(xin.data_ptr()), gpart.data_ptr<float>(),
+                                   (int)gpart.size(1), lpart.data_ptr<float>(), lcoef.data_ptr<float>(),
+                                   (int)lpart.size(0), (int)lpart.size(2), done.data_ptr<uint8_t>(),
+                                   loss.data_ptr<float>(), (float)step, (float)max_loss, (int)N, (int)H, (int)W,
+                                   dt_of(g), cur_stream()),
+           "dream_update");
+}
+
 // geom: KH, KW, stride, pad_h, pad_w, Cr; cols [N, OH, OW, J_ld] (J = KH*KW*Cr), gx [N, H, W, 8]
 void col2im(Tensor cols, Tensor gx, std::vector<int64_t> g) {
   check_cuda(cols, "cols");
@@ -615,6 +648,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("kind"), py::arg("dir"), py::arg("geom"), py::arg("bias") = py::none(), py::arg("relu") = false);
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
+  m.def("dream_update", &dream_update, "fused DeepDream normalize + update + next network input");
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
   m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");
   m.def("softmax_rows", &softmax_rows, "row softmax (classifier head)");

@@ -60,6 +60,96 @@ __global__ void __launch_bounds__(256) sumsq_core_bwd_kernel(const uint16_t* __r
   }
 }
 
+// ---- fused DeepDream step tail (engine/deepdream.py:DeepDream._fused_step) ----
+// part[n][p] = sum of |g| over channels 0..2 of the network-input gradient g [N, H, W, 8]
+template <int DT>
+__global__ void __launch_bounds__(256) absmean_part_kernel(const uint16_t* __restrict__ g, float* __restrict__ part,
+                                                           int HW) {
+  const int n = blockIdx.y;
+  const uint16_t* gn = g + (long long)n * HW * 8;
+  float acc = 0.f;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+    const uint2 v = *reinterpret_cast<const uint2*>(gn + (long long)p * 8);  // channels 0..3
+    acc += fabsf(to_f<DT>(v.x & 0xFFFFu)) + fabsf(to_f<DT>(v.x >> 16)) + fabsf(to_f<DT>(v.y & 0xFFFFu));
+  }
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[(long long)n * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// One gradient-ascent update, per image n (blockIdx.y):
+//   loss[n] = sum_l lcoef[l] * sum_p lpart[l][n][p]            (the DeepDream loss)
+//   done[n] |= loss[n] > max_loss (max_loss < 0: disabled)      (device-side max_loss early stop)
+//   x[n] += step * (!done[n]) * g[n] / max(mean |g[n]|, 1e-7)   (fp32 master image, 3 channels)
+//   xin[n] = (x[n], 0, 0, 0, 0, 0) in the 16-bit network-input layout (8 channels)
+// Every block recomputes the per-image scalars from the partials (a few hundred floats from L2);
+// block 0 publishes done/loss (the others compute the same values, so the write is idempotent).
+template <int DT>
+__global__ void __launch_bounds__(256) dream_update_kernel(const uint16_t* __restrict__ g, float* __restrict__ x,
+                                                           uint16_t* __restrict__ xin, const float* __restrict__ gpart,
+                                                           int gparts, const float* __restrict__ lpart,
+                                                           const float* __restrict__ lcoef, int L, int lparts, int N,
+                                                           uint8_t* __restrict__ done, float* __restrict__ loss,
+                                                           float step, float max_loss, int HW) {
+  const int n = blockIdx.y;
+  __shared__ float sh[3];
+  if (threadIdx.x < 64) {
+    float gs = 0.f;
+    for (int p = threadIdx.x; p < gparts; p += 64) gs += gpart[(long long)n * gparts + p];
+    gs = wave_sum(gs);
+    float ls = 0.f;
+    for (int l = 0; l < L; ++l) {
+      float t = 0.f;
+      for (int p = threadIdx.x; p < lparts; p += 64) t += lpart[((long long)l * N + n) * lparts + p];
+      ls += lcoef[l] * wave_sum(t);
+    }
+    if (threadIdx.x == 0) {
+      const bool dn = done[n] != 0 || (max_loss >= 0.f && ls > max_loss);
+      sh[0] = dn ? 0.f : step / fmaxf(gs / (3.f * (float)HW), 1e-7f);
+      if (blockIdx.x == 0) {
+        done[n] = dn ? 1 : 0;
+        loss[n] = ls;
+      }
+    }
+  }
+  __syncthreads();
+  const float sc = sh[0];
+  const uint16_t* gn = g + (long long)n * HW * 8;
+  float* xn = x + (long long)n * HW * 3;
+  uint16_t* in = xin + (long long)n * HW * 8;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+    const uint2 v = *reinterpret_cast<const uint2*>(gn + (long long)p * 8);
+    const float x0 = xn[p * 3 + 0] + sc * to_f<DT>(v.x & 0xFFFFu);
+    const float x1 = xn[p * 3 + 1] + sc * to_f<DT>(v.x >> 16);
+    const float x2 = xn[p * 3 + 2] + sc * to_f<DT>(v.y & 0xFFFFu);
+    xn[p * 3 + 0] = x0;
+    xn[p * 3 + 1] = x1;
+    xn[p * 3 + 2] = x2;
+    *reinterpret_cast<uint4*>(in + (long long)p * 8) = uint4{pack2<DT>(x0, x1), pack2<DT>(x2, 0.f), 0u, 0u};
+  }
+}
+
+int dream_update_launch(const uint16_t* g, float* x, uint16_t* xin, float* gpart, int gparts, const float* lpart,
+                        const float* lcoef, int L, int lparts, uint8_t* done, float* loss, float step, float max_loss,
+                        int N, int H, int W, int dtype, hipStream_t s) {
+  if (gparts < 1 || N < 1 || N > 65535) return -1;
+  const int HW = H * W;
+  const dim3 gp((unsigned)gparts, (unsigned)N);
+  const unsigned ub = (unsigned)std::min(std::max((HW + 255) / 256, 1), 64);
+  if (dtype == DT_F16) {
+    hipLaunchKernelGGL(absmean_part_kernel<DT_F16>, gp, dim3(256), 0, s, g, gpart, HW);
+    hipLaunchKernelGGL(dream_update_kernel<DT_F16>, dim3(ub, (unsigned)N), dim3(256), 0, s, g, x, xin, gpart, gparts,
+                       lpart, lcoef, L, lparts, N, done, loss, step, max_loss, HW);
+  } else {
+    hipLaunchKernelGGL(absmean_part_kernel<DT_BF16>, gp, dim3(256), 0, s, g, gpart, HW);
+    hipLaunchKernelGGL(dream_update_kernel<DT_BF16>, dim3(ub, (unsigned)N), dim3(256), 0, s, g, x, xin, gpart, gparts,
+                       lpart, lcoef, L, lparts, N, done, loss, step, max_loss, HW);
+  }
+  return (int)hipGetLastError();
+}
+
 int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, int W, int C, int b, int dtype,
                       hipStream_t s) {
   if (C % 8 != 0 || H <= 2 * b || W <= 2 * b || parts < 1) return -1;

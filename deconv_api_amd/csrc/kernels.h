@@ -102,6 +102,11 @@ int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* i
                 long long y_ld = 0, const float* bias = nullptr, int relu = 0);
 // DeepDream loss: per-(image, block) partial sums of x^2 over the map minus a b-pixel border
 // (part [N][parts]), and its gradient gx = 2*scale[n]*x in the core, 0 on the border
+// fused DeepDream update: per-image mean |g| partials, loss from the sumsq partials, device-side
+// max_loss flag, x += step * g / mean|g| (fp32) and the next 16-bit network input (8 channels)
+int dream_update_launch(const uint16_t* g, float* x, uint16_t* xin, float* gpart, int gparts, const float* lpart,
+                        const float* lcoef, int L, int lparts, uint8_t* done, float* loss, float step, float max_loss,
+                        int N, int H, int W, int dtype, hipStream_t s);
 int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, int W, int C, int b, int dtype,
                       hipStream_t s);
 int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, uint16_t* gx, int N, int H, int W, int C, int b,

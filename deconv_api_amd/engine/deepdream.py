@@ -20,13 +20,22 @@ MI355X design:
 """
 from __future__ import annotations
 
+import os
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
 
+from ..ops import native
 from ..ops.autograd import premasked_grads, sumsq_core
+
+# DV_DREAM_FUSED=0: the step tail (loss, normalization, update) as torch ops instead of the fused
+# HIP kernels (A/B); DV_DREAM_GRAPHS: hipGraph cache entries (octave shapes) kept, LRU-evicted
+FUSED_STEP = os.environ.get("DV_DREAM_FUSED", "1") != "0"
+GRAPH_CACHE = int(os.environ.get("DV_DREAM_GRAPHS", "8"))
+LOSS_PARTS = 32
 
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
 
@@ -67,7 +76,9 @@ class DeepDream:
             dtype = getattr(net, "dtype", torch.bfloat16) if self.device.type == "cuda" else torch.float32
         self.dtype = dtype
         self.use_graphs = use_graphs and self.device.type == "cuda"
-        self._graphs: Dict[tuple, tuple] = {}
+        self.fused = FUSED_STEP and self.device.type == "cuda"
+        self._graphs: "OrderedDict[tuple, object]" = OrderedDict()
+        self.graph_cache = GRAPH_CACHE
 
     # ------------------------------------------------------------------ one step
     def _net_input(self, x: torch.Tensor) -> torch.Tensor:
@@ -100,10 +111,78 @@ class DeepDream:
         x.add_(g * ((~done).to(g.dtype) * self.s.step).view(-1, 1, 1, 1))
         return loss
 
+    # ------------------------------------------------------------------ fused GPU step
+    def _state(self, B: int, hw: Tuple[int, int]):
+        """Static buffers of one octave shape: fp32 master image x, the 16-bit network input xin
+        (an autograd leaf), loss/|g| partials, per-layer loss scales, done/loss flags."""
+        dev = self.device
+        names = list(self.s.layers.keys())
+        st = type("DreamState", (), {})()
+        st.x = torch.zeros(B, *hw, 3, device=dev)
+        st.xin = torch.zeros(B, *hw, 8, device=dev, dtype=self.dtype, requires_grad=True)
+        st.gpart = torch.zeros(B, 32, device=dev)
+        st.lpart = torch.zeros(len(names), B, LOSS_PARTS, device=dev)
+        st.done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        st.loss = torch.zeros(B, device=dev)
+        st.lcoef = None  # filled on the first step (needs the activation shapes)
+        st.scales = None
+        st.graph = None
+        return st
+
+    def _fused_step(self, st) -> None:
+        """forward -> per-layer sumsq partials + loss gradients (HIP) -> autograd backward of the
+        network only -> one fused normalize/update kernel that also writes the next xin."""
+        lib = native.lib()
+        names = list(self.s.layers.keys())
+        b = self.s.border
+        with premasked_grads():  # the loss gradient 2*act/numel vanishes where act does
+            acts = self.net.forward(st.xin, names)
+        outs = [acts[n].contiguous() for n in names]
+        if st.lcoef is None:
+            coef = [self.s.layers[n] / float(a[0].numel()) for n, a in zip(names, outs)]
+            st.lcoef = torch.tensor(coef, dtype=torch.float32, device=self.device)
+            st.scales = [torch.full((outs[0].shape[0],), c, dtype=torch.float32, device=self.device) for c in coef]
+        gacts = []
+        for i, a in enumerate(outs):
+            lib.sumsq_core(a, st.lpart[i], b)
+            ga = torch.empty_like(a)
+            lib.sumsq_core_bwd(a, st.scales[i], ga, b)
+            gacts.append(ga)
+        (g,) = torch.autograd.grad(outs, st.xin, gacts)
+        ml = -1.0 if self.s.max_loss is None else float(self.s.max_loss)
+        lib.dream_update(g.contiguous(), st.x, st.xin, st.gpart, st.lpart, st.lcoef, st.done, st.loss,
+                         float(self.s.step), ml)
+
+    def _fused_state(self, B: int, hw: Tuple[int, int]):
+        key = (B, tuple(hw))
+        if key in self._graphs:
+            self._graphs.move_to_end(key)
+            return self._graphs[key]
+        st = self._state(B, hw)
+        if self.use_graphs:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):  # warm up allocator / autograd on a side stream before capture
+                    self._fused_step(st)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            st.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(st.graph):
+                self._fused_step(st)
+        self._cache_put(key, st)
+        return st
+
+    def _cache_put(self, key, val):
+        self._graphs[key] = val
+        while len(self._graphs) > max(1, self.graph_cache):  # bounded: request shapes vary
+            self._graphs.popitem(last=False)
+            torch.cuda.empty_cache()
+
     # ------------------------------------------------------------------ hipGraph per shape
     def _graph(self, B: int, hw: Tuple[int, int]):
         key = (B, tuple(hw))
         if key in self._graphs:
+            self._graphs.move_to_end(key)
             return self._graphs[key]
         x = torch.zeros(B, *hw, 3, device=self.device)
         done = torch.zeros(B, dtype=torch.bool, device=self.device)
@@ -116,11 +195,24 @@ class DeepDream:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             loss = self._step(x, done)
-        self._graphs[key] = (g, x, done, loss)
+        self._cache_put(key, (g, x, done, loss))
         return self._graphs[key]
 
     def gradient_ascent(self, x: torch.Tensor) -> torch.Tensor:
         B, H, W, _ = x.shape
+        if self.fused:
+            st = self._fused_state(B, (H, W))
+            with torch.no_grad():
+                st.x.copy_(x)
+                st.xin.zero_()
+                st.xin[..., :3].copy_(x)
+            st.done.zero_()
+            for _ in range(self.s.iterations):
+                if st.graph is not None:
+                    st.graph.replay()
+                else:
+                    self._fused_step(st)
+            return st.x.clone()
         if self.use_graphs:
             g, gx, gdone, gloss = self._graph(B, (H, W))
             gx.copy_(x)
@@ -180,6 +272,7 @@ class TiledDeepDream(DeepDream):
     def __init__(self, net, settings: Optional[DreamSettings] = None, tile: int = 512, info=None, seed: int = 0,
                  dtype=None, use_graphs: bool = True):
         super().__init__(net, settings, use_graphs=False, dtype=dtype)
+        self.fused = False  # the tiled step assembles the gradient across tiles/ranks (below)
         self.tile = tile
         self.info = info
         self.gen = torch.Generator().manual_seed(seed)

@@ -301,3 +301,25 @@ def test_gpu_inception_block_grad(native_lib, bi, hw, premasked):
     assert _cos(yd.float().cpu(), yc.detach()) > 0.999
     (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.bfloat16).cuda())
     assert _cos(gd.float().cpu(), gc) > 0.995
+
+
+@pytest.mark.gpu
+def test_gpu_fused_step_equals_unfused(native_lib):
+    """Fused step tail (HIP sumsq partials + loss gradients, one normalize/update kernel writing the
+    next network input, device-side max_loss) == the torch-op step, eager and graph-replayed."""
+    net = InceptionV3(0).build("cuda")
+    x = (torch.rand(2, 150, 150, 3, generator=torch.Generator().manual_seed(6)) * 2 - 1).cuda()
+    for max_loss in (None, 1e-9):  # 1e-9: every image stops at its first step (device-side flag)
+        for iters, octs in ((1, 1), (3, 2)):
+            s = DreamSettings(iterations=iters, octaves=octs, max_loss=max_loss)
+            ref = DeepDream(net, s, use_graphs=False)
+            ref.fused = False
+            want = ref.run(x)
+            for graphs in (False, True):
+                dd = DeepDream(net, s, use_graphs=graphs)
+                assert dd.fused
+                got = dd.run(x)
+                if iters == 1:  # one step: equal up to the fp32 rounding of the update
+                    assert (got - want).abs().max() < 1e-4, (max_loss, graphs)
+                else:  # later steps see bf16 inputs that may round differently: compare the dream
+                    assert _cos(got - x, want - x) > 0.99 if max_loss is None else (got - want).abs().max() < 1e-4
