@@ -902,12 +902,27 @@ static int dma_forced(const ConvArgs& a, hipStream_t s, int cfg) {
   }
 }
 
+// Measured override of the size-based choice below for small and narrow-K problems (the DeepDream
+// nets' 1x1 / 1x7 / 5x5 convs and dgrads; tools/tune_dma.py sweep of every launch of configs 3 and 5,
+// profiles/tune_dma_c{3,5}.txt): conv time 9.80 -> 8.52 ms (InceptionV3, 4 octaves) and 6.45 -> 6.07
+// ms (ResNet-50 512^2 x 32). Small problems are bound by per-K-step latency, not MFMA rate: a 64x64
+// 4-wave tile with a 3-stage ring and no split-K; mid-size / short-K ones by the epilogue and DMA
+// issue of one big tile per CU: 128x128. The big-K VGG16 layers keep the large tiles.
+static int auto_cfg(const ConvArgs& a) {
+  if (a.mask != nullptr) return 0;
+  const long long mn = (long long)a.M * a.OCpad;
+  if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= 256) return 8;
+  if (a.OCpad % 128 == 0 && a.OC > 64 && a.Kpad < 4096 && (a.Kpad < 1024 || mn < 50000000LL)) return 3;
+  return 0;
+}
+
 // Tile choice: the largest tile (best MFMA:LDS ratio) unless it leaves CUs idle. A problem with
 // fewer big tiles than the chip has CUs (deep layers at small batch, strong-scaled tiles) drops to
 // the next smaller tile, which doubles the workgroup count and fits 2 workgroups per CU in LDS.
 template <int DT, int AMODE, int EPI>
 static int dma_bn(const ConvArgs& a, hipStream_t s) {
   if (g_cfg > 0) return dma_forced<DT, AMODE, EPI>(a, s, g_cfg);
+  if (const int c = auto_cfg(a)) return dma_forced<DT, AMODE, EPI>(a, s, c);
   // measured (profiles/layers_r1_pipeline.txt): BK=32 x 4-stage rings lose to 2-stage BK=64 on the
   // 256x256 and 512x64 tiles; the 3-stage BK=64 ring wins slightly on 256x128.
   const int v = DT == DT_BF16 ? dma_variant() : 0;  // A/B variants are bf16-only
@@ -978,6 +993,11 @@ static void dma_tile_dims(const ConvArgs& a, bool mask, int& BM, int& BN) {
   auto nwg = [&](int bm, int bn) { return (long long)((a.M + bm - 1) / bm) * (a.OCpad / bn); };
   BM = 256;
   BN = 16;
+  if (!mask) {
+    const int c = auto_cfg(a);
+    if (c == 8) { BM = 64; BN = 64; return; }
+    if (c == 3) { BM = 128; BN = 128; return; }
+  }
   if (mask) {
     if (a.OCpad % 256 == 0 && a.OC > 128) { BM = 128; BN = 256; }
     else if (a.OCpad % 128 == 0 && a.OC > 64) { BM = 128; BN = 128; }
@@ -1004,6 +1024,7 @@ static void dma_tile_dims(const ConvArgs& a, bool mask, int& BM, int& BN) {
 int conv_dma_splitk(const ConvArgs& a) {
   if (g_ks > 0) return std::min(g_ks, a.Kpad / 64);
   if (std::getenv("DV_NO_SPLITK")) return 1;
+  if (g_cfg == 0 && auto_cfg(a) == 8) return 1;
   int BM, BN;
   dma_tile_dims(a, a.mask != nullptr, BM, BN);
   const long long nwg = (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN);
