@@ -426,6 +426,74 @@ void dream_update(Tensor g, Tensor x, Tensor xin, Tensor gpart, Tensor lpart, Te
            "dream_update");
 }
 
+// Tiled DeepDream step (engine/deepdream.py:TiledDeepDream). plan: int32 [units_total, 7] rows
+// {image, tile origin y, x, owned y0, y1, x0, x1 (tile-local)}, validated on the host when built;
+// shift: int32 [2] device (sy, sx). This rank's units are u = rank + k * world, k < xin.size(0).
+static void check_plan(const Tensor& plan, const Tensor& shift) {
+  check_cuda(plan, "plan");
+  check_cuda(shift, "shift");
+  TORCH_CHECK(plan.scalar_type() == at::kInt && plan.is_contiguous() && plan.dim() == 2 && plan.size(1) == 7,
+              "tile plan: int32 [U, 7]");
+  TORCH_CHECK(shift.scalar_type() == at::kInt && shift.numel() >= 2 && shift.stride(-1) == 1, "tile shift: int32 [2]");
+}
+
+void tile_gather(Tensor x, Tensor xin, Tensor plan, Tensor shift, int64_t rank, int64_t world) {
+  check_cuda(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_plan(plan, shift);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3, "tile_gather: x");
+  TORCH_CHECK(xin.dim() == 4 && xin.size(3) == 8 && xin.is_contiguous(), "tile_gather: xin [U, Th, Tw, 8]");
+  const int64_t U = xin.size(0);
+  TORCH_CHECK(world >= 1 && rank >= 0 && rank < world && rank + (U - 1) * world < plan.size(0), "tile_gather: units");
+  check_rc(dv::tile_gather_launch(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(xin.data_ptr()), plan.data_ptr<int>(),
+                                  shift.data_ptr<int>(), (int)U, (int)rank, (int)world, (int)x.size(1), (int)x.size(2),
+                                  (int)xin.size(1), (int)xin.size(2), dt_of(xin), cur_stream()),
+           "tile_gather");
+}
+
+void tile_pack(Tensor g, Tensor pack, Tensor plan, Tensor lpart, Tensor lcoef, int64_t ucap, int64_t rank, int64_t world) {
+  check_cuda(g, "g");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  check_cuda(plan, "plan");
+  TORCH_CHECK(plan.scalar_type() == at::kInt && plan.is_contiguous() && plan.dim() == 2 && plan.size(1) == 7, "plan");
+  TORCH_CHECK(g.dim() == 4 && g.size(3) == 8 && g.is_contiguous(), "tile_pack: g [U, Th, Tw, 8]");
+  const int64_t U = g.size(0), Th = g.size(1), Tw = g.size(2);
+  TORCH_CHECK(U <= ucap && rank + (U - 1) * world < plan.size(0), "tile_pack: units");
+  TORCH_CHECK(pack.scalar_type() == g.scalar_type() && pack.is_contiguous() &&
+                  pack.numel() >= dv::tile_pack_elems((int)ucap, (int)Th, (int)Tw) &&
+                  reinterpret_cast<uintptr_t>(pack.data_ptr()) % 16 == 0,
+              "tile_pack: pack too small / misaligned");
+  TORCH_CHECK(lpart.scalar_type() == at::kFloat && lpart.is_contiguous() && lpart.dim() == 3 && lpart.size(1) == U,
+              "tile_pack: lpart [L, U, LP]");
+  TORCH_CHECK(lcoef.scalar_type() == at::kFloat && lcoef.numel() == lpart.size(0), "tile_pack: lcoef [L]");
+  check_rc(dv::tile_pack_launch(reinterpret_cast<const uint16_t*>(g.data_ptr()), reinterpret_cast<uint16_t*>(pack.data_ptr()),
+                                plan.data_ptr<int>(), lpart.data_ptr<float>(), lcoef.data_ptr<float>(), (int)lpart.size(0),
+                                (int)lpart.size(2), (int)U, (int)ucap, (int)rank, (int)world, (int)Th, (int)Tw, dt_of(g),
+                                cur_stream()),
+           "tile_pack");
+}
+
+void tile_update(Tensor packs, int64_t ucap, Tensor plan, Tensor shift, Tensor x, Tensor done, Tensor loss, double step,
+                 double max_loss, int64_t world, int64_t Th, int64_t Tw) {
+  check_cuda(packs, "packs");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(packs.device());
+  check_plan(plan, shift);
+  const long long pe = dv::tile_pack_elems((int)ucap, (int)Th, (int)Tw);
+  TORCH_CHECK(packs.is_contiguous() && packs.numel() == world * pe, "tile_update: packs [world, pack_elems]");
+  TORCH_CHECK(plan.size(0) <= world * ucap, "tile_update: plan larger than the packs");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3, "tile_update: x");
+  TORCH_CHECK(done.scalar_type() == at::kByte && done.numel() == x.size(0) && loss.scalar_type() == at::kFloat &&
+                  loss.numel() == x.size(0),
+              "tile_update: done u8 [B], loss fp32 [B]");
+  check_rc(dv::tile_update_launch(reinterpret_cast<const uint16_t*>(packs.data_ptr()), pe, (int)ucap, plan.data_ptr<int>(),
+                                  (int)plan.size(0), shift.data_ptr<int>(), x.data_ptr<float>(), done.data_ptr<uint8_t>(),
+                                  loss.data_ptr<float>(), (float)step, (float)max_loss, (int)world, (int)x.size(1),
+                                  (int)x.size(2), (int)Th, (int)Tw, dt_of(packs), cur_stream()),
+           "tile_update");
+}
+
+int64_t tile_pack_elems(int64_t ucap, int64_t Th, int64_t Tw) { return dv::tile_pack_elems((int)ucap, (int)Th, (int)Tw); }
+
 // geom: KH, KW, stride, pad_h, pad_w, Cr; cols [N, OH, OW, J_ld] (J = KH*KW*Cr), gx [N, H, W, 8]
 void col2im(Tensor cols, Tensor gx, std::vector<int64_t> g) {
   check_cuda(cols, "cols");
@@ -648,6 +716,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("kind"), py::arg("dir"), py::arg("geom"), py::arg("bias") = py::none(), py::arg("relu") = false);
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
+  m.def("tile_gather", &tile_gather, "tiled DeepDream: rolled tile gather into the 16-bit network input");
+  m.def("tile_pack", &tile_pack, "tiled DeepDream: owned-pixel gradient pack + unit loss / sum|g| tail");
+  m.def("tile_update", &tile_update, "tiled DeepDream: normalize + update the image from every rank's packs");
+  m.def("tile_pack_elems", &tile_pack_elems);
   m.def("dream_update", &dream_update, "fused DeepDream normalize + update + next network input");
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
   m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");

@@ -909,7 +909,8 @@ static int dma_forced(const ConvArgs& a, hipStream_t s, int cfg) {
 // 4-wave tile with a 3-stage ring and no split-K; mid-size / short-K ones by the epilogue and DMA
 // issue of one big tile per CU: 128x128. The big-K VGG16 layers keep the large tiles.
 static int auto_cfg(const ConvArgs& a) {
-  if (a.mask != nullptr) return 0;
+  static const bool off = std::getenv("DV_NO_AUTO_CFG") != nullptr;  // A/B: the size-based choice only
+  if (a.mask != nullptr || off) return 0;
   const long long mn = (long long)a.M * a.OCpad;
   if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= 256) return 8;
   if (a.OCpad % 128 == 0 && a.OC > 64 && a.Kpad < 4096 && (a.Kpad < 1024 || mn < 50000000LL)) return 3;

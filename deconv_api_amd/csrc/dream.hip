@@ -131,6 +131,163 @@ __global__ void __launch_bounds__(256) dream_update_kernel(const uint16_t* __res
   }
 }
 
+// ---- tiled DeepDream step (engine/deepdream.py:TiledDeepDream; BASELINE config 5) ----
+// Work units are (tile, image) pairs; unit u has plan row plan[u] = {image, tile origin y, x,
+// owned rect y0, y1, x0, x1 (tile-local, half-open)}. The image is rolled by shift = (sy, sx)
+// (device int32[2], so one captured graph replays any shift): rolled[Y][X] = x[(Y-sy) mod H][(X-sx) mod W].
+constexpr int TPLAN = 7;
+// elements per unit in a pack (3 channels x tile, rounded to 16 B so the fp32 tail stays aligned)
+__host__ __device__ inline long long tile_ustride(int Th, int Tw) { return ((long long)Th * Tw * 3 + 7) & ~7LL; }
+
+// xin[k] (this rank's k-th unit, global unit u = rank + k * world) <- rolled-image tile, 8-channel 16-bit
+template <int DT>
+__global__ void __launch_bounds__(256) tile_gather_kernel(const float* __restrict__ x, uint16_t* __restrict__ xin,
+                                                          const int* __restrict__ plan, const int* __restrict__ shift,
+                                                          int rank, int world, int H, int W, int Th, int Tw) {
+  const int k = blockIdx.y;
+  const int* pu = plan + (long long)(rank + k * world) * TPLAN;
+  const int b = pu[0], oy = pu[1], ox = pu[2];
+  const int sy = shift[0], sx = shift[1];
+  const float* xb = x + (long long)b * H * W * 3;
+  uint16_t* dst = xin + (long long)k * Th * Tw * 8;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < Th * Tw; p += gridDim.x * 256) {
+    const int ty = p / Tw, tx = p - ty * Tw;
+    int yy = (oy + ty - sy) % H, xx = (ox + tx - sx) % W;
+    yy += yy < 0 ? H : 0;
+    xx += xx < 0 ? W : 0;
+    const float* src = xb + ((long long)yy * W + xx) * 3;
+    *reinterpret_cast<uint4*>(dst + (long long)p * 8) = uint4{pack2<DT>(src[0], src[1]), pack2<DT>(src[2], 0.f), 0u, 0u};
+  }
+}
+
+// pack[k] <- the owned pixels (3 channels, 16-bit, tile-local row-major over the owned rect) of the
+// unit's input gradient g[k]; tail (fp32 pairs after units * Th*Tw*3 elements): {loss, sum |g|}
+// of the unit, loss = sum_l lcoef[l] * sum_p lpart[l][k][p].
+template <int DT>
+__global__ void __launch_bounds__(256) tile_pack_kernel(const uint16_t* __restrict__ g, uint16_t* __restrict__ pack,
+                                                        const int* __restrict__ plan, const float* __restrict__ lpart,
+                                                        const float* __restrict__ lcoef, int L, int lparts, int units,
+                                                        int ucap, int rank, int world, int Th, int Tw) {
+  const int k = blockIdx.x;
+  const int* pu = plan + (long long)(rank + k * world) * TPLAN;
+  const int y0 = pu[3], y1 = pu[4], x0 = pu[5], x1 = pu[6];
+  const int ow = x1 - x0, npix = (y1 - y0) * ow;
+  const uint16_t* gk = g + (long long)k * Th * Tw * 8;
+  uint16_t* dst = pack + (long long)k * tile_ustride(Th, Tw);
+  float asum = 0.f;
+  for (int p = threadIdx.x; p < npix; p += 256) {
+    const int ty = y0 + p / ow, tx = x0 + p % ow;
+    const uint2 v = *reinterpret_cast<const uint2*>(gk + ((long long)ty * Tw + tx) * 8);
+    const uint16_t c0 = (uint16_t)(v.x & 0xFFFFu), c1 = (uint16_t)(v.x >> 16), c2 = (uint16_t)(v.y & 0xFFFFu);
+    dst[p * 3 + 0] = c0;
+    dst[p * 3 + 1] = c1;
+    dst[p * 3 + 2] = c2;
+    asum += fabsf(to_f<DT>(c0)) + fabsf(to_f<DT>(c1)) + fabsf(to_f<DT>(c2));
+  }
+  __shared__ float red[4];
+  asum = wave_sum(asum);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = asum;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float ls = 0.f;
+    for (int l = 0; l < L; ++l) {
+      float t = 0.f;
+      for (int p = threadIdx.x; p < lparts; p += 64) t += lpart[((long long)l * units + k) * lparts + p];
+      ls += lcoef[l] * wave_sum(t);
+    }
+    if (threadIdx.x == 0) {
+      float* tail = reinterpret_cast<float*>(pack + (long long)ucap * tile_ustride(Th, Tw)) + 2 * k;
+      tail[0] = ls;
+      tail[1] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
+  }
+}
+
+// x += step * (!done) * g / max(mean |g|, 1e-7) straight from the gathered packs of every rank
+// (each image pixel is owned by exactly one unit: no races); per-image loss and sum |g| come from
+// the unit tails (every block recomputes them; the done/loss writes are idempotent).
+__global__ void __launch_bounds__(256) tile_update_kernel(const uint16_t* __restrict__ packs, long long pack_elems,
+                                                          int units_per_rank, const int* __restrict__ plan,
+                                                          int nunits, const int* __restrict__ shift, float* __restrict__ x,
+                                                          uint8_t* __restrict__ done, float* __restrict__ loss,
+                                                          float step, float max_loss, int world, int H, int W, int Th,
+                                                          int Tw, int dt) {
+  const int u = blockIdx.y;
+  const int* pu = plan + (long long)u * TPLAN;
+  const int b = pu[0];
+  __shared__ float sh[1];
+  if (threadIdx.x < 64) {
+    float ls = 0.f, as = 0.f;
+    for (int v = threadIdx.x; v < nunits; v += 64) {
+      if (plan[(long long)v * TPLAN] != b) continue;
+      const float* tail = reinterpret_cast<const float*>(packs + (long long)(v % world) * pack_elems +
+                                                         (long long)units_per_rank * tile_ustride(Th, Tw)) +
+                          2 * (v / world);
+      ls += tail[0];
+      as += tail[1];
+    }
+    ls = wave_sum(ls);
+    as = wave_sum(as);
+    if (threadIdx.x == 0) {
+      const bool dn = done[b] != 0 || (max_loss >= 0.f && ls > max_loss);
+      sh[0] = dn ? 0.f : step / fmaxf(as / (3.f * (float)H * (float)W), 1e-7f);
+      done[b] = dn ? 1 : 0;
+      loss[b] = ls;
+    }
+  }
+  __syncthreads();
+  const float sc = sh[0];
+  const int oy = pu[1], ox = pu[2], y0 = pu[3], y1 = pu[4], x0 = pu[5], x1 = pu[6];
+  const int ow = x1 - x0, npix = (y1 - y0) * ow;
+  const int sy = shift[0], sx = shift[1];
+  const uint16_t* src = packs + (long long)(u % world) * pack_elems + (long long)(u / world) * tile_ustride(Th, Tw);
+  float* xb = x + (long long)b * H * W * 3;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < npix; p += gridDim.x * 256) {
+    const int ty = y0 + p / ow, tx = x0 + p % ow;
+    int yy = (oy + ty - sy) % H, xx = (ox + tx - sx) % W;
+    yy += yy < 0 ? H : 0;
+    xx += xx < 0 ? W : 0;
+    float* d = xb + ((long long)yy * W + xx) * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] += sc * (dt == DT_F16 ? to_f<DT_F16>(src[p * 3 + c]) : to_f<DT_BF16>(src[p * 3 + c]));
+  }
+}
+
+long long tile_pack_elems(int ucap, int Th, int Tw) { return (long long)ucap * (tile_ustride(Th, Tw) + 4); }
+
+int tile_gather_launch(const float* x, uint16_t* xin, const int* plan, const int* shift, int units, int rank, int world,
+                       int H, int W, int Th, int Tw, int dtype, hipStream_t s) {
+  if (units < 1 || units > 65535) return -1;
+  const dim3 grid((unsigned)std::min((Th * Tw + 255) / 256, 128), (unsigned)units);
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(tile_gather_kernel<DT_F16>, grid, dim3(256), 0, s, x, xin, plan, shift, rank, world, H, W, Th, Tw);
+  else
+    hipLaunchKernelGGL(tile_gather_kernel<DT_BF16>, grid, dim3(256), 0, s, x, xin, plan, shift, rank, world, H, W, Th, Tw);
+  return (int)hipGetLastError();
+}
+
+int tile_pack_launch(const uint16_t* g, uint16_t* pack, const int* plan, const float* lpart, const float* lcoef, int L,
+                     int lparts, int units, int ucap, int rank, int world, int Th, int Tw, int dtype, hipStream_t s) {
+  if (units < 1 || units > ucap) return -1;
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(tile_pack_kernel<DT_F16>, dim3((unsigned)units), dim3(256), 0, s, g, pack, plan, lpart, lcoef, L,
+                       lparts, units, ucap, rank, world, Th, Tw);
+  else
+    hipLaunchKernelGGL(tile_pack_kernel<DT_BF16>, dim3((unsigned)units), dim3(256), 0, s, g, pack, plan, lpart, lcoef, L,
+                       lparts, units, ucap, rank, world, Th, Tw);
+  return (int)hipGetLastError();
+}
+
+int tile_update_launch(const uint16_t* packs, long long pack_elems, int units_per_rank, const int* plan, int nunits,
+                       const int* shift, float* x, uint8_t* done, float* loss, float step, float max_loss, int world,
+                       int H, int W, int Th, int Tw, int dtype, hipStream_t s) {
+  if (nunits < 1 || nunits > 65535) return -1;
+  const dim3 grid((unsigned)std::min((Th * Tw + 255) / 256, 64), (unsigned)nunits);
+  hipLaunchKernelGGL(tile_update_kernel, grid, dim3(256), 0, s, packs, pack_elems, units_per_rank, plan, nunits, shift, x,
+                     done, loss, step, max_loss, world, H, W, Th, Tw, dtype);
+  return (int)hipGetLastError();
+}
+
 int dream_update_launch(const uint16_t* g, float* x, uint16_t* xin, float* gpart, int gparts, const float* lpart,
                         const float* lcoef, int L, int lparts, uint8_t* done, float* loss, float step, float max_loss,
                         int N, int H, int W, int dtype, hipStream_t s) {

@@ -107,6 +107,16 @@ int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* i
 int dream_update_launch(const uint16_t* g, float* x, uint16_t* xin, float* gpart, int gparts, const float* lpart,
                         const float* lcoef, int L, int lparts, uint8_t* done, float* loss, float step, float max_loss,
                         int N, int H, int W, int dtype, hipStream_t s);
+// tiled DeepDream step: rolled tile gather -> owned-pixel pack (+ unit loss / sum|g| tail) ->
+// [all-gather of packs over ranks] -> update of the fp32 image straight from the packs
+int tile_gather_launch(const float* x, uint16_t* xin, const int* plan, const int* shift, int units, int rank, int world,
+                       int H, int W, int Th, int Tw, int dtype, hipStream_t s);
+int tile_pack_launch(const uint16_t* g, uint16_t* pack, const int* plan, const float* lpart, const float* lcoef, int L,
+                     int lparts, int units, int ucap, int rank, int world, int Th, int Tw, int dtype, hipStream_t s);
+long long tile_pack_elems(int ucap, int Th, int Tw);  // 16-bit elements of one rank's pack
+int tile_update_launch(const uint16_t* packs, long long pack_elems, int units_per_rank, const int* plan, int nunits,
+                       const int* shift, float* x, uint8_t* done, float* loss, float step, float max_loss, int world,
+                       int H, int W, int Th, int Tw, int dtype, hipStream_t s);
 int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, int W, int C, int b, int dtype,
                       hipStream_t s);
 int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, uint16_t* gx, int N, int H, int W, int C, int b,

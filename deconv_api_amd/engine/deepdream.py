@@ -265,9 +265,20 @@ class TiledDeepDream(DeepDream):
     units as ONE batch (tiles are equal-sized: the last row/column of tiles is shifted inwards to
     overlap its neighbour, and each pixel's gradient is taken from exactly one owning tile), so the
     convs see large GEMMs instead of one small launch per tile. The roll, the tile cut and the
-    stitch/un-roll are single gathers/scatters with precomputed indices. The full gradient is
-    assembled with one all-reduce (each pixel has exactly one owner, so the sum is the stitch),
-    normalized by the global per-image mean |g| and applied identically on every rank."""
+    stitch/un-roll are single gathers/scatters with precomputed indices.
+
+    GPU (fused) step, all HIP kernels (csrc/dream.hip):
+      tile_gather   rolled tiles of the fp32 image -> 16-bit network input of this rank's units
+      network       forward + input-gradient backward of all units as one batch
+      tile_pack     owned pixels of each unit's gradient -> a fixed-size pack, + {loss, sum|g|}
+      all_gather    of the packs over the ranks (RCCL; each pixel has ONE owner, so gathering the
+                    owned tiles moves half the bytes of all-reducing the full gradient, and the
+                    unit losses ride along: no separate loss all-reduce)
+      tile_update   per-image mean|g| and loss from the pack tails, device-side max_loss flag,
+                    x += step * g / mean|g| straight from the packs (identical on every rank)
+    On one rank the whole octave (``iterations`` steps, shifts in a device table) is ONE captured
+    hipGraph; with several ranks each step's compute is a graph and the collective runs between
+    replays. CPU tensors use the torch implementation below (the oracle)."""
 
     def __init__(self, net, settings: Optional[DreamSettings] = None, tile: int = 512, info=None, seed: int = 0,
                  dtype=None, use_graphs: bool = True):
@@ -279,7 +290,8 @@ class TiledDeepDream(DeepDream):
         self._plans: Dict[tuple, tuple] = {}
         # one hipGraph per octave shape for the whole tile forward/backward/stitch
         self.tile_graphs = use_graphs and self.device.type == "cuda"
-        self._tgraphs: Dict[tuple, tuple] = {}
+        self._tgraphs: "OrderedDict[tuple, object]" = OrderedDict()
+        self.tile_fused = FUSED_STEP and self.device.type == "cuda"
 
     @staticmethod
     def _axis_tiles(L: int, tile: int):
@@ -349,7 +361,7 @@ class TiledDeepDream(DeepDream):
 
     def _tile_graph(self, x: torch.Tensor, plan):
         """hipGraph of _tile_grad for one octave shape (static buffers: image, shift, grad, loss)."""
-        key = tuple(x.shape)
+        key = ("torch",) + tuple(x.shape)
         if key in self._tgraphs:
             return self._tgraphs[key]
         bx = x.clone()
@@ -368,7 +380,140 @@ class TiledDeepDream(DeepDream):
         self._tgraphs[key] = (g, bx, shift, grad, loss)
         return self._tgraphs[key]
 
+    # ------------------------------------------------------------------ fused GPU tiled step
+    def _gplan(self, B: int, H: int, W: int):
+        """int32 [units, 7] plan rows {image, tile origin y, x, owned y0, y1, x0, x1 (tile-local)}
+        for every unit of every rank (unit u = tile u // B, image u % B), validated on the host
+        (the kernels index with them unchecked)."""
+        Th, Tw, tiles = self._tiles(H, W)
+        rows = []
+        for u in range(len(tiles) * B):
+            (y0, oy0, oy1), (x0, ox0, ox1) = tiles[u // B]
+            rows.append([u % B, y0, x0, oy0 - y0, oy1 - y0, ox0 - x0, ox1 - x0])
+        plan = torch.tensor(rows, dtype=torch.int32)
+        assert ((plan[:, 0] >= 0) & (plan[:, 0] < B)).all()
+        assert ((plan[:, 1] >= 0) & (plan[:, 1] + Th <= H) & (plan[:, 2] >= 0) & (plan[:, 2] + Tw <= W)).all()
+        assert ((plan[:, 3] >= 0) & (plan[:, 3] < plan[:, 4]) & (plan[:, 4] <= Th)).all()
+        assert ((plan[:, 5] >= 0) & (plan[:, 5] < plan[:, 6]) & (plan[:, 6] <= Tw)).all()
+        return Th, Tw, plan, len(tiles)
+
+    def _tstate(self, B: int, H: int, W: int):
+        key = (B, H, W)
+        if key in self._tgraphs:
+            self._tgraphs.move_to_end(key)
+            return self._tgraphs[key]
+        lib = native.lib()
+        dev = self.device
+        world = self.info.world if self.info is not None else 1
+        rank = self.info.rank if self.info is not None else 0
+        Th, Tw, plan, ntiles = self._gplan(B, H, W)
+        nunits = plan.shape[0]
+        ucap = -(-nunits // world)
+        mine = len(range(rank, nunits, world))
+        st = type("TileState", (), {})()
+        st.Th, st.Tw, st.ntiles, st.world, st.rank, st.ucap, st.mine = Th, Tw, ntiles, world, rank, ucap, mine
+        st.plan = plan.to(dev)
+        st.x = torch.zeros(B, H, W, 3, device=dev)
+        st.done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        st.loss = torch.zeros(B, device=dev)
+        st.shifts = torch.zeros(self.s.iterations, 2, dtype=torch.int32, device=dev)
+        pe = lib.tile_pack_elems(ucap, Th, Tw)
+        st.packs = torch.zeros(world, pe, dtype=self.dtype, device=dev)
+        st.pack = st.packs[rank]
+        st.xin = torch.zeros(max(mine, 1), Th, Tw, 8, dtype=self.dtype, device=dev, requires_grad=True)
+        st.lpart = torch.zeros(len(self.s.layers), max(mine, 1), LOSS_PARTS, device=dev)
+        st.lcoef, st.scales, st.graph, st.step_graph = None, None, None, None
+        self._tgraphs[key] = st
+        while len(self._tgraphs) > max(1, self.graph_cache):
+            self._tgraphs.popitem(last=False)
+            torch.cuda.empty_cache()
+        return st
+
+    def _tile_compute(self, st, it: int) -> None:
+        """gather -> network fwd/bwd -> pack, for step ``it`` (shift row it of the device table)."""
+        lib = native.lib()
+        if st.mine == 0:
+            return
+        names = list(self.s.layers.keys())
+        lib.tile_gather(st.x, st.xin, st.plan, st.shifts[it], st.rank, st.world)
+        with premasked_grads():
+            acts = self.net.forward(st.xin, names)
+        outs = [acts[n].contiguous() for n in names]
+        if st.lcoef is None:
+            coef = [self.s.layers[n] / float(a[0].numel()) for n, a in zip(names, outs)]
+            st.lcoef = torch.tensor(coef, dtype=torch.float32, device=self.device)
+            st.scales = [torch.full((st.mine,), c, dtype=torch.float32, device=self.device) for c in coef]
+        gacts = []
+        for i, a in enumerate(outs):
+            lib.sumsq_core(a, st.lpart[i], self.s.border)
+            ga = torch.empty_like(a)
+            lib.sumsq_core_bwd(a, st.scales[i], ga, self.s.border)
+            gacts.append(ga)
+        (g,) = torch.autograd.grad(outs, st.xin, gacts)
+        lib.tile_pack(g.contiguous(), st.pack, st.plan, st.lpart, st.lcoef, st.ucap, st.rank, st.world)
+
+    def _tile_apply(self, st, it: int) -> None:
+        ml = -1.0 if self.s.max_loss is None else float(self.s.max_loss) * st.ntiles
+        native.lib().tile_update(st.packs, st.ucap, st.plan, st.shifts[it], st.x, st.done, st.loss, float(self.s.step),
+                                 ml, st.world, st.Th, st.Tw)
+
+    def _tile_steps(self, st) -> None:
+        import torch.distributed as dist
+
+        for it in range(self.s.iterations):
+            self._tile_compute(st, it)
+            if st.world > 1:
+                dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
+            self._tile_apply(st, it)
+
+    def _gradient_ascent_fused(self, x: torch.Tensor) -> torch.Tensor:
+        import torch.distributed as dist
+
+        B, H, W, _ = x.shape
+        st = self._tstate(B, H, W)
+        shifts = torch.randint(-self.tile // 2, self.tile // 2 + 1, (self.s.iterations, 2), generator=self.gen)
+        st.shifts.copy_(shifts.to(torch.int32))
+        st.x.copy_(x)
+        st.done.zero_()
+        if self.tile_graphs and st.world == 1 and st.graph is None:
+            # warm up on a side stream (autograd / allocator), restore the image, capture the octave
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._tile_compute(st, 0)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            st.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(st.graph):
+                self._tile_steps(st)
+        elif self.tile_graphs and st.world > 1 and st.step_graph is None:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._tile_compute(st, 0)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            st.step_graph = []
+            for it in range(self.s.iterations):  # one graph per step index (each reads its shift row)
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph):
+                    self._tile_compute(st, it)
+                st.step_graph.append(gph)
+        if st.graph is not None:
+            st.graph.replay()
+        elif st.step_graph is not None:
+            for it in range(self.s.iterations):
+                st.step_graph[it].replay()
+                dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
+                self._tile_apply(st, it)
+        else:
+            self._tile_steps(st)
+        return st.x.clone()
+
     def gradient_ascent(self, x: torch.Tensor) -> torch.Tensor:
+        if self.tile_fused and x.is_cuda:
+            return self._gradient_ascent_fused(x)
+        return self._gradient_ascent_torch(x)
+
+    def _gradient_ascent_torch(self, x: torch.Tensor) -> torch.Tensor:
         import torch.distributed as dist
 
         B, H, W, _ = x.shape

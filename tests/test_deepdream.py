@@ -323,3 +323,45 @@ def test_gpu_fused_step_equals_unfused(native_lib):
                     assert (got - want).abs().max() < 1e-4, (max_loss, graphs)
                 else:  # later steps see bf16 inputs that may round differently: compare the dream
                     assert _cos(got - x, want - x) > 0.99 if max_loss is None else (got - want).abs().max() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_loss", [None, 1e-9])
+def test_gpu_tiled_fused_equals_torch(native_lib, max_loss):
+    """Fused tiled step (HIP rolled gather, owned-pixel packs with loss/|g| tails, pack-driven
+    update; one hipGraph per octave incl. all steps) == the torch tiled implementation, on a shape
+    whose tiles overlap (200 x 260 with 128 tiles -> 2 x 3 tiles of 100 x 87)."""
+    net = ResNet50(0).build("cuda", torch.float16)
+    x = (torch.rand(2, 200, 260, 3, generator=torch.Generator().manual_seed(8)) * 2 - 1).cuda()
+    for iters in (1, 3):
+        s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=2, iterations=iters, max_loss=max_loss)
+        ref = TiledDeepDream(net, s, tile=128, seed=3, use_graphs=False)
+        ref.tile_fused = False
+        want = ref.run(x)
+        for graphs in (False, True):
+            dd = TiledDeepDream(net, s, tile=128, seed=3, use_graphs=graphs)
+            assert dd.tile_fused
+            got = dd.run(x)
+            assert torch.isfinite(got).all()
+            if max_loss is not None:  # every image stops at its first step: nothing moves
+                assert (got - want).abs().max() < 1e-5, (iters, graphs)
+            else:  # same gradients up to 16-bit rounding of the first step's inputs (tools/diag_tiled.py)
+                assert _cos(got - x, want - x) > (0.998 if iters == 1 else 0.99), (iters, graphs)
+            got2 = dd.run(x)  # replay of the cached state/graph (fresh shifts from the generator)
+            assert torch.isfinite(got2).all()
+
+
+@pytest.mark.gpu
+def test_gpu_tiled_whole_octave_graph_1024(native_lib):
+    """Regression for the round-1 illegal-address fault: one hipGraph holding every step of a tiled
+    octave at 1024^2 (tile 512, fp16) replays, twice, and matches the eager fused steps."""
+    net = ResNet50(0).build("cuda", torch.float16)
+    s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=2, iterations=2, max_loss=None)
+    x = (torch.rand(1, 1024, 1024, 3, generator=torch.Generator().manual_seed(11)) * 2 - 1).cuda()
+    eager = TiledDeepDream(net, s, tile=512, seed=5, use_graphs=False).run(x)
+    dd = TiledDeepDream(net, s, tile=512, seed=5, use_graphs=True)
+    graph = dd.run(x)
+    torch.cuda.synchronize()
+    assert all(st.graph is not None for st in dd._tgraphs.values())
+    assert torch.isfinite(graph).all() and _cos(graph - x, eager - x) > 0.99
+    assert torch.isfinite(dd.run(x)).all()
