@@ -9,8 +9,15 @@ all-gather of every rank's uint8 mosaics over xGMI (weak scaling: 256 img/GPU). 
 of step i runs asynchronously on RCCL's stream and overlaps step i+1's compute (double-buffered
 output); the clock stops only after the last gather completed on every rank.
 
+Request latency: every step's mosaics are copied back to pinned host memory on a copy stream
+(overlapping the next step's compute, as the service does); ``p50_req_latency_ms`` is the median
+over steps of (step start on the compute stream -> its mosaics on the host), hipEvent-timed.
+
 Run: ``python bench.py [--gpus N --steps K --warmup W]``; for N > 1 under
-``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``
+(also with N = 1: torchrun env -> a real 1-rank RCCL group, the collective path runs).
+``--profile`` re-runs the same command under ``rocprofv3 --kernel-trace`` (before any GPU call)
+and prints a per-kernel table (tools/kstats.py); ``--profile pmc`` adds one counter pass.
 Rank 0 prints ONE JSON line. Weights: seeded random-init VGG16 (no network for ImageNet
 weights); data: synthetic uint8 images. ``--device cpu --tiny`` is a functional rehearsal of the
 same code path (gloo, scaled model) used by the CPU test-suite.
@@ -48,6 +55,8 @@ def parse(argv=None):
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--tiny", action="store_true", help="scaled VGG16 at 32px (CPU rehearsal only)")
     ap.add_argument("--breakdown", action="store_true", help="per-phase timing to stderr (extra syncs)")
+    ap.add_argument("--profile", nargs="?", const="trace", default=None, choices=["trace", "pmc"],
+                    help="re-run under rocprofv3 and print a per-kernel table (trace) [+ PMC pass]")
     return ap.parse_args(argv)
 
 
@@ -64,8 +73,41 @@ class _Sync:
             torch.cuda.synchronize()
 
 
+PMC_PASS = "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS"
+
+
+def profile(argv, mode: str) -> int:
+    """Re-launch this benchmark under rocprofv3 as a CHILD process (nothing in this process has
+    touched the GPU), then summarize the kernel trace (and a PMC pass for ``pmc``)."""
+    import os
+    import subprocess
+    import tempfile
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    child = [a for a in (argv if argv is not None else sys.argv[1:]) if a not in ("--profile", "trace", "pmc")]
+    out = tempfile.mkdtemp(prefix="dv_prof_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = ["rocprofv3", "--kernel-trace", "-d", out, "-o", "bench", "--", sys.executable,
+           os.path.join(here, "bench.py"), *child]
+    rc = subprocess.call(cmd)
+    if rc != 0:
+        return rc
+    db = next((os.path.join(d, f) for d, _, fs in os.walk(out) for f in fs if f.endswith(".db")), None)
+    if db is not None:
+        subprocess.call([sys.executable, os.path.join(here, "tools", "kstats.py"), db, "--top", "30",
+                         "--last-frac", "0.6"])
+    if mode == "pmc":
+        pdir = out + "_pmc"
+        rc = subprocess.call(["rocprofv3", "--pmc", *PMC_PASS.split(), "-d", pdir, "-o", "bench", "--",
+                              sys.executable, os.path.join(here, "bench.py"), *child, "--steps", "2", "--warmup", "1"])
+        if rc == 0:
+            subprocess.call([sys.executable, os.path.join(here, "tools", "pmc_summary.py"), pdir])
+    return rc
+
+
 def main(argv=None):
     args = parse(argv)
+    if args.profile:
+        raise SystemExit(profile(argv, args.profile))
     info = pdist.init(device_type=args.device)
     if info.world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={info.world}; using WORLD_SIZE")
@@ -82,7 +124,7 @@ def main(argv=None):
     # ---- weights: built on rank 0, broadcast once over RCCL ----
     t0 = time.time()
     model = VGG16.random(args.seed if info.is_main else args.seed + 12345, specs=specs)
-    if info.world > 1:
+    if info.backend != "none":  # any real process group (incl. a 1-rank RCCL group under torchrun)
         sd = pdist.broadcast_state(model.state_dict(), info)
         model = VGG16.from_state_dict(sd, specs=specs)
     eng = DeconvNet(model.build(dev, dtype))
@@ -94,15 +136,36 @@ def main(argv=None):
     xbuf = torch.empty(B, S, S, 8, dtype=dtype, device=dev)
     gathered = [torch.empty(info.world * B, 2 * S, 2 * S, 3, dtype=torch.uint8, device=dev) for _ in range(2)]
     pending = [None, None]
+    cuda = dev.type == "cuda"
+    # copy-back of every step's mosaics on its own stream into a pinned double buffer
+    copy_stream = torch.cuda.Stream(dev) if cuda else None
+    host = [torch.empty(B, 2 * S, 2 * S, 3, dtype=torch.uint8, pin_memory=cuda) for _ in range(2)]
+    back_done = [None, None]
+    lat = []  # (start event, copy-back end event) per timed step
 
-    def step(i):
+    def step(i, ev0=None):
         ops.resize_preprocess(images, xbuf)
         res = eng.run(xbuf, args.layer, k=args.k)
-        if info.world > 1:
-            slot = i % 2
+        slot = i % 2
+        if info.backend != "none":
             if pending[slot] is not None:
                 pending[slot].wait()  # the gather that last used this buffer (step i-2)
             pending[slot] = dist.all_gather_into_tensor(gathered[slot], res.mosaic.contiguous(), async_op=True)
+        if cuda:
+            if back_done[slot] is not None:
+                back_done[slot].synchronize()  # host slot free again (its step i-2 copy landed)
+            ready = torch.cuda.Event()
+            ready.record()
+            copy_stream.wait_event(ready)
+            res.mosaic.record_stream(copy_stream)
+            with torch.cuda.stream(copy_stream):
+                host[slot].copy_(res.mosaic, non_blocking=True)
+                back_done[slot] = torch.cuda.Event(enable_timing=True)
+                back_done[slot].record()
+            if ev0 is not None:
+                lat.append((ev0, back_done[slot]))
+        else:
+            host[slot].copy_(res.mosaic)
         return res
 
     def drain():
@@ -119,7 +182,6 @@ def main(argv=None):
     if args.breakdown and info.is_main:
         _breakdown(eng, images, xbuf, args, sync)
 
-    cuda = dev.type == "cuda"
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if cuda else None
     pdist.barrier(info)
     sync()
@@ -129,11 +191,13 @@ def main(argv=None):
     host_steps = []
     for i in range(args.steps):
         ts = time.perf_counter()
-        res = step(i)
+        res = step(i, evs[i] if cuda else None)
         if cuda:
             evs[i + 1].record()
         host_steps.append(time.perf_counter() - ts)
     drain()
+    if cuda:
+        copy_stream.synchronize()
     sync()
     pdist.barrier(info)
     sync()
@@ -144,6 +208,11 @@ def main(argv=None):
     else:
         per_step = sorted(1e3 * t for t in host_steps)
     p50 = pdist.all_reduce_max(per_step[len(per_step) // 2], info)
+    if cuda:
+        req = sorted(a.elapsed_time(b) for a, b in lat)
+    else:
+        req = per_step
+    p50_req = pdist.all_reduce_max(req[len(req) // 2], info)
 
     ms = elapsed / args.steps * 1e3
     value = B * info.world * args.steps / elapsed
@@ -155,12 +224,14 @@ def main(argv=None):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 3),
+        "p50_req_latency_ms": round(p50_req, 3),
         "p50_batch_latency_ms": round(p50, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / REF_IMG_PER_S, 1),
         "baseline_img_per_s": REF_IMG_PER_S,
         "dtype": "bf16" if cuda else "fp32",
+        "process_group": info.backend,
         "data": "synthetic uint8 224x224 images, seeded random-init VGG16 weights",
         "config": {"model": f"vgg16_deconvnet_{args.layer}", "global_batch": B * info.world, "seq_len": S,
                    "image_size": S, "filters_per_image": args.k, "parallelism": f"dp{info.world}"},

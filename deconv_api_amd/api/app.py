@@ -134,20 +134,37 @@ def create_app(service=None, cfg: Optional[Config] = None, dream_service=None) -
     async def deepdream(request: Request):
         """Extension (not in the reference): DeepDream of the uploaded image. Form fields: file,
         optional model (inception_v3 | resnet50), octaves, steps. Same data-URL conventions."""
-        form = parse_form(await request.body(), request.headers.get("content-type"))
-        if "file" not in form:
-            return _missing(["file"])
-        ds = state["dream"]
-        if ds is None:
-            from ..serve.dream_service import DreamService
-
-            ds = state["dream"] = DreamService(cfg)
+        t0 = time.perf_counter()
+        status = "200"
         try:
-            url = await ds.dream(form["file"], form.get("model", "inception_v3"), int(form.get("octaves", 4)),
-                                 int(form.get("steps", 20)))
-        except (ImageDecodeError, ValueError) as e:
-            return JSONResponse(status_code=400, content={"detail": str(e)})
-        return JSONResponse(content=url)
+            try:
+                form = parse_form(await request.body(), request.headers.get("content-type"))
+                if "file" not in form:
+                    status = "422"
+                    return _missing(["file"])
+                model = form.get("model", "inception_v3")
+                octaves, steps = int(form.get("octaves", 4)), int(form.get("steps", 20))
+            except (FormError, ValueError, LookupError) as e:  # bad body / charset / non-numeric field
+                status = "400"
+                return JSONResponse(status_code=400, content={"detail": str(e)})
+            ds = state["dream"]
+            if ds is None:
+                from ..serve.dream_service import DreamService
+
+                ds = state["dream"] = DreamService(cfg)
+            try:
+                url = await ds.dream(form["file"], model, octaves, steps)
+            except (ImageDecodeError, ValueError) as e:
+                status = "400"
+                return JSONResponse(status_code=400, content={"detail": str(e)})
+            except Exception:  # noqa: BLE001
+                status = "500"
+                log.exception("deepdream request failed")
+                return JSONResponse(status_code=500, content={"detail": "internal error"})
+            return JSONResponse(content=url)
+        finally:
+            M.REQUESTS.inc(route="/deepdream", status=status)
+            M.LATENCY.observe(time.perf_counter() - t0, route="/deepdream", layer="-")
 
     return app
 

@@ -75,7 +75,10 @@ def parse_multipart(body: bytes, content_type: str) -> Dict[str, str]:
                 charset = _param(hv, "charset") or charset
         if name is None:
             continue
-        out.setdefault(name, data.decode(charset, errors="replace"))
+        try:
+            out.setdefault(name, data.decode(charset, errors="replace"))
+        except LookupError as e:  # unknown charset name in the part's content-type
+            raise FormError(f"unknown charset {charset!r} in multipart field {name!r}") from e
     return out
 
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 import base64
 import binascii
 import io
+import os
 from urllib.parse import quote
 
 import numpy as np
@@ -31,7 +32,7 @@ class ImageDecodeError(ValueError):
 
 
 def split_data_url(uri: str) -> str:
-    parts = uri.split(",")
+    parts = uri.split(",", 2)  # == uri.split(",")[1] (reference readb64), without splitting the payload
     if len(parts) < 2:
         raise ImageDecodeError("file must be a data URL ('data:<mime>;base64,<payload>')")
     return parts[1]
@@ -44,18 +45,30 @@ def b64decode_lenient(payload: str) -> bytes:
         raise ImageDecodeError(f"bad base64 payload: {e}") from e
 
 
+# service-level cap on decoded pixels (far below PIL's decompression-bomb limit): a request can
+# not make the server decode, pin and upload a ~500 MB image (DV_MAX_PIXELS)
+MAX_PIXELS = int(os.environ.get("DV_MAX_PIXELS", str(64 << 20)))
+
+
 def decode_image(data: bytes) -> np.ndarray:
-    """bytes -> HxWx3 uint8 RGB."""
+    """bytes -> HxWx3 uint8 RGB (EXIF orientation applied, like cv2.imdecode IMREAD_COLOR)."""
     try:
         im = Image.open(io.BytesIO(data))
-        im = ImageOps.exif_transpose(im)
+        if im.size[0] * im.size[1] > MAX_PIXELS:  # header only: nothing decoded yet
+            raise ImageDecodeError(f"image too large: {im.size[0]}x{im.size[1]} > {MAX_PIXELS} pixels")
+        ImageOps.exif_transpose(im, in_place=True)  # no copy when there is nothing to rotate
         if im.mode in ("I;16", "I;16B", "I;16L", "I"):
             arr = np.asarray(im, dtype=np.float64)
             arr = np.clip(arr / 257.0, 0, 255).astype(np.uint8)
             im = Image.fromarray(arr)
-        im = im.convert("RGB")
+        if im.mode != "RGB":  # convert() to the same mode would be a full copy
+            im = im.convert("RGB")
         arr = np.asarray(im, dtype=np.uint8)
+    except Image.DecompressionBombError as e:
+        raise ImageDecodeError(f"image too large: {e}") from e
     except (UnidentifiedImageError, OSError, SyntaxError, ValueError) as e:
+        if isinstance(e, ImageDecodeError):
+            raise
         raise ImageDecodeError(f"undecodable image: {e}") from e
     if arr.ndim != 3 or arr.shape[2] != 3 or arr.shape[0] < 1 or arr.shape[1] < 1:
         raise ImageDecodeError("decoded image has an unexpected shape")

@@ -39,6 +39,7 @@ class Config:
     request_timeout_s: float = 120.0
     codec_workers: int = 8                # decode threads (PIL releases the GIL while decoding)
     encode_threads: int = 16              # native JPEG encoder threads per batch (GIL released)
+    encode_chunk: int = 16                # images per encode call; each chunk is delivered at once
     native_codec: bool = True             # native encoder for responses (PIL fallback when False/unbuilt)
     cors_origins: Tuple[str, ...] = ("*",)  # app/main.py:22-32
     host: str = "0.0.0.0"

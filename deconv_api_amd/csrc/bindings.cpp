@@ -628,6 +628,42 @@ void deprocess_mosaic(Tensor recon, Tensor out, int64_t tiles, bool reverse, c10
            "deprocess_apply");
 }
 
+// blob: u8 [bytes] (device), table: int64 [B, 4] {offset, Hs, Ws, mode} (device; validated on the
+// host by the caller against the blob size: runtime/staging.py), out: bf16 [B, OH, OW, Cpad] or
+// u8 [B, OH, OW, 3]
+void resize_batch(Tensor blob, Tensor table, Tensor out, int64_t max_end) {
+  check_cuda(blob, "blob");
+  check_cuda(table, "table");
+  check_cuda(out, "out");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(blob.device());
+  TORCH_CHECK(blob.scalar_type() == at::kByte && blob.is_contiguous() && blob.dim() == 1, "resize_batch: blob u8 [bytes]");
+  TORCH_CHECK(max_end <= blob.numel(), "resize_batch: table addresses past the blob");
+  TORCH_CHECK(table.scalar_type() == at::kLong && table.is_contiguous() && table.dim() == 2 && table.size(1) == 4,
+              "resize_batch: table int64 [B, 4]");
+  TORCH_CHECK(out.dim() == 4 && out.is_contiguous() && out.size(0) == table.size(0), "resize_batch: out [B, OH, OW, C]");
+  const bool u8 = out.scalar_type() == at::kByte;
+  TORCH_CHECK(u8 ? out.size(3) == 3 : (out.scalar_type() == at::kBFloat16 && out.size(3) >= 3 &&
+                                       reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0),
+              "resize_batch: out u8 [..., 3] or bf16 [..., Cpad]");
+  check_rc(dv::resize_batch_launch(blob.data_ptr<uint8_t>(), reinterpret_cast<const long long*>(table.data_ptr<int64_t>()), (int)table.size(0), out.data_ptr(),
+                                   (int)out.size(1), (int)out.size(2), (int)out.size(3), u8 ? 1 : 0, cur_stream()),
+           "resize_batch");
+}
+
+void preprocess_u8(Tensor in, Tensor out) {
+  check_cuda(in, "in");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(in.device());
+  TORCH_CHECK(in.scalar_type() == at::kByte && in.is_contiguous() && in.dim() == 4 && in.size(3) == 3,
+              "preprocess_u8: in u8 [B, H, W, 3]");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.dim() == 4 && out.size(0) == in.size(0) &&
+                  out.size(1) == in.size(1) && out.size(2) == in.size(2) && out.size(3) >= 3 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "preprocess_u8: out bf16 [B, H, W, Cpad]");
+  check_rc(dv::preprocess_u8_launch(in.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(out.data_ptr()),
+                                    in.numel() / 3, (int)out.size(3), cur_stream()),
+           "preprocess_u8");
+}
+
 void resize_preprocess(Tensor img, Tensor out, int64_t mode) {
   check_cuda(img, "img");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(img.device());
@@ -731,6 +767,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("deprocess_mosaic", &deprocess_mosaic, py::arg("recon"), py::arg("out"), py::arg("tiles"), py::arg("reverse"),
         py::arg("stats") = py::none());
   m.def("resize_preprocess", &resize_preprocess);
+  m.def("resize_batch", &resize_batch, "variable-size batch resize (+preprocess) from one staged blob");
+  m.def("preprocess_u8", &preprocess_u8, "resized RGB u8 -> caffe-preprocessed bf16 network input");
   m.def("maxpool2x2", &maxpool2x2);
   m.def("unpool2x2", &unpool2x2);
   m.def("sparse_unpool_conv", &sparse_unpool_conv, "2:4 sparse-MFMA conv-down on a max-unpooled input");

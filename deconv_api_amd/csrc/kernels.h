@@ -82,6 +82,9 @@ int deprocess_apply_launch(const float* recon, const double* stats, uint8_t* out
 // uint8 [B][Hs][Ws][3] RGB -> bf16 NHWC [B][OH][OW][Cpad]: cv2 INTER_LINEAR resize + caffe mean subtract
 int resize_preprocess_launch(const uint8_t* img, int B, int Hs, int Ws, uint16_t* out, int OH, int OW,
                              int Cpad, int mode, hipStream_t s);
+int resize_batch_launch(const uint8_t* blob, const long long* table, int B, void* out, int OH, int OW, int Cpad,
+                        int out_u8, hipStream_t s);
+int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad, hipStream_t s);
 // standalone 2x2/s2 max pool with switch codes, and its inverse (unpool scatter to full res)
 int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C,
                       hipStream_t s);

@@ -386,15 +386,9 @@ __device__ __forceinline__ void lin_coef(int d, double scale, int ssize, int& s0
   a1 = __float2int_rn(fx * 2048.f);
 }
 
-__global__ void __launch_bounds__(256) resize_preprocess_kernel(const uint8_t* __restrict__ img_b, int Hs, int Ws,
-                                                                uint16_t* __restrict__ out_b, int OH, int OW,
-                                                                int Cpad, int mode) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= OH * OW) return;
-  const uint8_t* img = img_b + (long long)blockIdx.y * Hs * Ws * 3;
-  uint16_t* out = out_b + (long long)blockIdx.y * OH * OW * Cpad;
-  const int ox = p % OW, oy = p / OW;
-  int px[3];
+// one output pixel (ox, oy) of the cv2-compatible resize of img [Hs, Ws, 3] u8
+__device__ __forceinline__ void resize_px(const uint8_t* __restrict__ img, int Hs, int Ws, int OH, int OW, int ox, int oy,
+                                          int mode, int (&px)[3]) {
   if (mode == 2) {
     for (int c = 0; c < 3; ++c) px[c] = img[((long long)oy * Ws + ox) * 3 + c];
   } else if (mode == 1) {
@@ -417,8 +411,11 @@ __global__ void __launch_bounds__(256) resize_preprocess_kernel(const uint8_t* _
       px[c] = v < 0 ? 0 : (v > 255 ? 255 : v);
     }
   }
+}
+
+// caffe preprocess of one pixel into Cpad 16-bit slots (slot c<3 = rgb[c] - mean[c], quirk Q1)
+__device__ __forceinline__ void store_pre(uint16_t* __restrict__ o, const int (&px)[3], int Cpad) {
   const float mean[3] = {103.939f, 116.779f, 123.68f};
-  uint16_t* o = out + (long long)p * Cpad;
   if (Cpad == 8) {  // one 16-B store per pixel
     uint4 v;
     v.x = pack_bf2((float)px[0] - mean[0], (float)px[1] - mean[1]);
@@ -431,11 +428,70 @@ __global__ void __launch_bounds__(256) resize_preprocess_kernel(const uint8_t* _
   }
 }
 
+__global__ void __launch_bounds__(256) resize_preprocess_kernel(const uint8_t* __restrict__ img_b, int Hs, int Ws,
+                                                                uint16_t* __restrict__ out_b, int OH, int OW,
+                                                                int Cpad, int mode) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= OH * OW) return;
+  const uint8_t* img = img_b + (long long)blockIdx.y * Hs * Ws * 3;
+  uint16_t* out = out_b + (long long)blockIdx.y * OH * OW * Cpad;
+  int px[3];
+  resize_px(img, Hs, Ws, OH, OW, p % OW, p / OW, mode, px);
+  store_pre(out + (long long)p * Cpad, px, Cpad);
+}
+
 int resize_preprocess_launch(const uint8_t* img, int B, int Hs, int Ws, uint16_t* out, int OH, int OW, int Cpad,
                              int mode, hipStream_t s) {
   if (Cpad < 3 || mode < 0 || mode > 2 || B <= 0) return -1;
   hipLaunchKernelGGL(resize_preprocess_kernel, dim3((OH * OW + 255) / 256, B), dim3(256), 0, s, img, Hs, Ws, out,
                      OH, OW, Cpad, mode);
+  return (int)hipGetLastError();
+}
+
+// Whole request batch in ONE launch: images of any sizes packed back to back in one u8 blob (one
+// pinned staging slot, one H2D copy; runtime/staging.py), table[b] = {byte offset, Hs, Ws, mode}.
+// out_u8 == 0: preprocessed 16-bit [B, OH, OW, Cpad]; out_u8 == 1: resized RGB u8 [B, OH, OW, 3]
+// (the 150 KB/image form rank 0 scatters to the other GPUs; preprocess_u8 finishes it there).
+__global__ void __launch_bounds__(256) resize_batch_kernel(const uint8_t* __restrict__ blob,
+                                                           const long long* __restrict__ table, void* __restrict__ out,
+                                                           int OH, int OW, int Cpad, int out_u8) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= OH * OW) return;
+  const long long* t = table + (long long)blockIdx.y * 4;
+  int px[3];
+  resize_px(blob + t[0], (int)t[1], (int)t[2], OH, OW, p % OW, p / OW, (int)t[3], px);
+  const long long pix = (long long)blockIdx.y * OH * OW + p;
+  if (out_u8) {
+    uint8_t* o = reinterpret_cast<uint8_t*>(out) + pix * 3;
+    o[0] = (uint8_t)px[0];
+    o[1] = (uint8_t)px[1];
+    o[2] = (uint8_t)px[2];
+  } else {
+    store_pre(reinterpret_cast<uint16_t*>(out) + pix * Cpad, px, Cpad);
+  }
+}
+
+int resize_batch_launch(const uint8_t* blob, const long long* table, int B, void* out, int OH, int OW, int Cpad,
+                        int out_u8, hipStream_t s) {
+  if (B <= 0 || B > 65535 || (!out_u8 && Cpad < 3)) return -1;
+  hipLaunchKernelGGL(resize_batch_kernel, dim3((OH * OW + 255) / 256, B), dim3(256), 0, s, blob, table, out, OH, OW,
+                     Cpad, out_u8);
+  return (int)hipGetLastError();
+}
+
+// resized RGB u8 [P pixels, 3] -> preprocessed 16-bit [P, Cpad] (the scattered shard on a rank)
+__global__ void __launch_bounds__(256) preprocess_u8_kernel(const uint8_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                            long long P, int Cpad) {
+  for (long long p = blockIdx.x * 256LL + threadIdx.x; p < P; p += (long long)gridDim.x * 256) {
+    const int px[3] = {in[p * 3], in[p * 3 + 1], in[p * 3 + 2]};
+    store_pre(out + p * Cpad, px, Cpad);
+  }
+}
+
+int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad, hipStream_t s) {
+  if (P <= 0 || Cpad < 3) return -1;
+  const unsigned grid = (unsigned)std::min<long long>((P + 255) / 256, 256LL * 32);
+  hipLaunchKernelGGL(preprocess_u8_kernel, dim3(grid), dim3(256), 0, s, in, out, P, Cpad);
   return (int)hipGetLastError();
 }
 

@@ -40,7 +40,9 @@ class GraphedDeconv:
                 self.engine.run(x, layer, k=self.k, mode=self.mode)
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local: the service's completion thread keeps synchronizing on earlier batches'
+        # events while the worker captures a new (layer, bucket) graph
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             res = self.engine.run(x, layer, k=self.k, mode=self.mode)
         return g, x, res
 
@@ -50,6 +52,19 @@ class GraphedDeconv:
             if key not in self._cache:
                 self._cache[key] = self._capture(layer, B)
             return self._cache[key]
+
+    def input(self, layer: str, n: int) -> torch.Tensor:
+        """The static input of the (layer, bucket(n)) graph, for a producer that writes straight
+        into it (runtime/staging.py); follow with ``replay``."""
+        return self.get(layer, bucket_for(n))[1]
+
+    def replay(self, layer: str, n: int):
+        B = bucket_for(n)
+        g, xs, res = self.get(layer, B)
+        if n < B:
+            xs[n:].zero_()
+        g.replay()
+        return res
 
     def run(self, x: torch.Tensor, layer: str):
         """x: [n, S, S, 8] bf16 on device (n <= bucket). Returns the (graph-owned) result whose

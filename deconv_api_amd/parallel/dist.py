@@ -7,7 +7,8 @@ Data-parallel deconvnet serving/benchmarking (BASELINE config 4):
     fixed per-rank size so every collective and graph has a static shape);
   * the uint8 output mosaics are all-gathered with ``all_gather_into_tensor`` (one collective,
     602 KB per image) so any rank can encode/serve the whole batch;
-  * a Gloo side group carries control-plane traffic (metadata, heartbeats) off the RCCL rings.
+  * the serving control plane (commands, acks, heartbeats, re-forming the group over survivors)
+    runs over the job's TCPStore (parallel/elastic.py), off the RCCL rings.
 The reference is single-process (Dockerfile:15, app/main.py:46); this layer is new.
 """
 from __future__ import annotations
@@ -52,7 +53,10 @@ def init(backend: Optional[str] = None, device_type: Optional[str] = None, timeo
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world == 1:
+    # torchrun env (even with one rank) or DV_FORCE_PG=1: a real process group, so a 1-rank run
+    # exercises the RCCL collectives; a plain `python x.py` creates none
+    force = os.environ.get("DV_FORCE_PG") == "1" or "TORCHELASTIC_RUN_ID" in os.environ
+    if world == 1 and not (force and "MASTER_PORT" in os.environ):
         return DistInfo(0, 1, 0, device, "none")
     backend = backend or ("nccl" if device_type == "cuda" else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -60,8 +64,7 @@ def init(backend: Optional[str] = None, device_type: Optional[str] = None, timeo
     if backend == "nccl":
         kw["device_id"] = device
     dist.init_process_group(**kw)
-    ctrl = dist.new_group(backend="gloo") if backend == "nccl" else None
-    return DistInfo(rank, world, local, device, backend, ctrl)
+    return DistInfo(rank, world, local, device, backend, None)
 
 
 def shutdown() -> None:
@@ -71,7 +74,7 @@ def shutdown() -> None:
 
 
 def barrier(info: DistInfo) -> None:
-    if info.world > 1:
+    if info.backend != "none":
         if info.backend == "nccl":
             dist.barrier(device_ids=[info.local_rank])
         else:
@@ -82,7 +85,7 @@ def broadcast_state(sd: Dict[str, torch.Tensor], info: DistInfo, src: int = 0,
                     bucket_bytes: int = 256 << 20) -> Dict[str, torch.Tensor]:
     """Broadcast a state dict from ``src`` as flat fp32 buckets (shapes are known on every rank
     because every rank builds the same architecture). Returns tensors on CPU."""
-    if info.world == 1:
+    if info.backend == "none":
         return sd
     names = sorted(sd.keys())
     out: Dict[str, torch.Tensor] = {}
@@ -111,7 +114,7 @@ def broadcast_state(sd: Dict[str, torch.Tensor], info: DistInfo, src: int = 0,
 
 def all_gather_rows(x: torch.Tensor, info: DistInfo, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[b, ...] per rank -> [world*b, ...] on every rank (rank-major order)."""
-    if info.world == 1:
+    if info.backend == "none":
         return x
     if out is None:
         out = torch.empty((info.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
@@ -120,7 +123,7 @@ def all_gather_rows(x: torch.Tensor, info: DistInfo, out: Optional[torch.Tensor]
 
 
 def all_reduce_max(v: float, info: DistInfo) -> float:
-    if info.world == 1:
+    if info.backend == "none":
         return v
     t = torch.tensor([v], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

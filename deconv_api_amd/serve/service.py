@@ -7,10 +7,11 @@ blocking compute, app/main.py:46), so requests serialize and the server stalls. 
   * requests are queued and a single GPU worker thread drains them in batches (same target layer,
     up to ``max_batch``, waiting at most ``batch_timeout_ms`` for stragglers); one batch = one
     engine call over B images x 4 filters, replayed from a hipGraph per (layer, batch bucket);
-  * the worker never waits for the GPU: it uploads (pinned, non_blocking), launches, enqueues the
-    mosaic's D2H copy into pinned memory plus an event, and moves on to the next batch; a
-    completion thread waits on the event and hands results to the requests, whose JPEG encode
-    then overlaps the next batch's GPU work;
+  * the worker never waits for the GPU: the batch's decoded images go into one pinned staging
+    slot, ONE H2D copy on the copy stream, ONE batched resize launch, the engine (graph replay) on
+    the compute stream, and the mosaics' copy-back on a third stream (runtime/staging.py); a
+    completion thread waits on the copy-back event and hands results to the requests, whose JPEG
+    encode then overlaps the next batch's GPU work; per-stage hipEvent times go to /metrics;
   * backpressure: beyond ``max_queue`` pending requests new ones fail fast (HTTP 503);
   * a watchdog marks the service not-ready while a batch exceeds the request timeout.
 """
@@ -77,10 +78,18 @@ class DeconvService:
             engine = DeconvNet(model.build(self.device, dtype))
         self.engine = engine
         self.graphs = None
-        if self.device.type == "cuda" and self.cfg.hip_graphs and runner is None:
-            from ..engine.graphs import GraphedDeconv
+        self.ring = None
+        if self.device.type == "cuda" and runner is None:
+            from ..runtime.staging import StagingRing
 
-            self.graphs = GraphedDeconv(engine, self.cfg.image_size, self.cfg.filters, self.cfg.mode)
+            # pinned staging ring + copy / compute / copy-back streams (runtime/staging.py)
+            self.ring = StagingRing(self.device, max_images=max(self.cfg.max_batch, 1))
+            if self.cfg.hip_graphs:
+                from ..engine.graphs import GraphedDeconv
+
+                self.graphs = GraphedDeconv(engine, self.cfg.image_size, self.cfg.filters, self.cfg.mode)
+        elif runner is not None and runner.graphs is not None:
+            self.graphs = runner.graphs  # the runner replays its own per-(layer, shard) graphs
         self.codec = CodecPool(self.cfg.codec_workers)
         from ..codec.image import _native
 
@@ -177,6 +186,8 @@ class DeconvService:
     def _worker(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+            if self.ring is not None:  # all engine work of this thread on the ring's compute stream
+                torch.cuda.set_stream(self.ring.compute_stream)
         last_beat = time.perf_counter()
         while not self._stop.is_set():
             jobs = self._collect()
@@ -209,11 +220,18 @@ class DeconvService:
             try:
                 mos = self.finish_batch(handle)
                 if self.native_codec:
-                    # one GIL-free call: the batch's JPEG + base64 + quote on native threads (a
-                    # lone request is split into restart segments across the threads)
-                    mos = encode_data_urls(mos, self.cfg.jpeg_quality, self.cfg.encode_threads)
-                for j, m in zip(group, mos):
-                    _deliver(j.loop, _set_result, j.future, m)
+                    # GIL-free native JPEG + base64 + quote, in chunks of ``encode_chunk`` images
+                    # spread over the native threads (a lone request is split into restart
+                    # segments); each chunk is delivered as soon as it is encoded, so the first
+                    # requests of a batch do not wait for the whole batch's encode
+                    step = max(1, self.cfg.encode_chunk)
+                    for c0 in range(0, len(group), step):
+                        urls = encode_data_urls(mos[c0:c0 + step], self.cfg.jpeg_quality, self.cfg.encode_threads)
+                        for j, m in zip(group[c0:c0 + step], urls):
+                            _deliver(j.loop, _set_result, j.future, m)
+                else:
+                    for j, m in zip(group, mos):
+                        _deliver(j.loop, _set_result, j.future, m)
                 dt = time.perf_counter() - t0
                 self.batches += 1
                 self.images += len(group)
@@ -234,13 +252,13 @@ class DeconvService:
 
     # ------------------------------------------------------------------ batch execution
     def preprocess(self, images: List[np.ndarray]) -> torch.Tensor:
+        """Resize + preprocess a batch outside the serving path (tests / tools); the worker stages
+        batches through the pinned ring instead (runtime/staging.py)."""
         B, S = len(images), self.cfg.image_size
         if self.device.type == "cuda":
-            x = torch.empty(B, S, S, 8, dtype=torch.bfloat16, device=self.device)
-            for b, img in enumerate(images):
-                h = torch.from_numpy(np.require(img, requirements=["C", "W"])).pin_memory()
-                ops.resize_preprocess(h.to(self.device, non_blocking=True), x[b])
-            return x
+            from ..runtime.staging import resize_batch
+
+            return resize_batch(images, torch.empty(B, S, S, 8, dtype=torch.bfloat16, device=self.device))
         x = torch.empty(B, S, S, 8, dtype=torch.float32)
         for b, img in enumerate(images):
             x[b] = ops.preprocess_ref(ops.resize_u8_ref(img, S, S), 8, torch.float32)
@@ -249,28 +267,29 @@ class DeconvService:
     def launch_batch(self, layer: str, images: List[np.ndarray]):
         """Enqueue the batch; returns a handle for ``finish_batch`` (GPU work may still run)."""
         if self.runner is not None:
-            return ("host", self.runner.run(layer, images))
+            return ("runner", self.runner.launch(layer, images))
         self.faults.on_batch()
-        x = self.preprocess(images)
         n = len(images)
-        if self.graphs is not None:
-            res = self.graphs.run(x, layer)
-        else:
-            res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
-        if self.device.type != "cuda":
+        if self.ring is None:  # CPU
+            res = self.engine.run(self.preprocess(images), layer, k=self.cfg.filters, mode=self.cfg.mode)
             return ("host", res.mosaic[:n].numpy())
-        host = torch.empty((n, *res.mosaic.shape[1:]), dtype=torch.uint8, pin_memory=True)
-        host.copy_(res.mosaic[:n], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        return ("event", ev, host)
+        S = self.cfg.image_size
+        if self.graphs is not None:  # resize straight into the graph's static input, then replay
+            x = self.graphs.input(layer, n)
+            st = self.ring.stage(images, x)
+            res = self.graphs.replay(layer, n)
+        else:
+            x = torch.empty(n, S, S, 8, dtype=torch.bfloat16, device=self.device)
+            st = self.ring.stage(images, x)
+            res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
+        return ("staged", self.ring.copy_back(st, res.mosaic))
 
     def finish_batch(self, handle) -> np.ndarray:
         if handle[0] == "host":
             return handle[1]
-        _, ev, host = handle
-        ev.synchronize()
-        return host.numpy()
+        if handle[0] == "runner":
+            return self.runner.finish(handle[1])
+        return self.ring.finish(handle[1])
 
     def run_batch(self, layer: str, images: List[np.ndarray]) -> np.ndarray:
         """Synchronous batch (tests / tools)."""

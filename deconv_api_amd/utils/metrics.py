@@ -121,3 +121,5 @@ BATCH_SIZE = REGISTRY.histogram("dv_batch_size", "images per engine batch",
 ENGINE_TIME = REGISTRY.histogram("dv_engine_seconds", "engine time per batch by stage")
 QUEUE_DEPTH = REGISTRY.gauge("dv_queue_depth", "pending requests in the batcher")
 IMAGES = REGISTRY.counter("dv_images_total", "images processed by the engine")
+STAGE_TIME = REGISTRY.histogram("dv_stage_seconds", "per-batch GPU stage time from hipEvents (h2d, compute, d2h)",
+                                (0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 1.0))

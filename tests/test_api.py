@@ -211,3 +211,35 @@ def test_native_jpeg_encoder():
             assert np.array_equal(parse_result_data_url(url).astype(int), dec)  # restart segments
     url = lib.jpeg_data_urls(torch.from_numpy(img[None].copy()), 95, DATA_URL_PREFIX, 1)[0]
     assert url == DATA_URL_PREFIX + quote(base64.b64encode(lib.jpeg_encode(torch.from_numpy(img), 95)).decode())
+
+
+def test_deepdream_bad_inputs_are_400(client):
+    """/deepdream: malformed body, unknown charset and non-numeric fields are client errors."""
+    from deconv_api_amd.api.forms import encode_multipart
+
+    client, _ = client
+    r = client.post("/deepdream", content=b"--x\r\n", headers={"content-type": "multipart/form-data"})
+    assert r.status_code == 400, r.text
+    body = (b'--bb\r\nContent-Disposition: form-data; name="file"\r\nContent-Type: text/plain; charset=nope-9\r\n\r\n'
+            b'data:,x\r\n--bb--\r\n')
+    r = client.post("/deepdream", content=body, headers={"content-type": "multipart/form-data; boundary=bb"})
+    assert r.status_code == 400 and "charset" in r.json()["detail"], r.text
+    b, ct = encode_multipart({"file": "data:image/png;base64,AAAA", "octaves": "x"})
+    r = client.post("/deepdream", content=b, headers={"content-type": ct})
+    assert r.status_code == 400, r.text
+    r = client.post("/", content=body, headers={"content-type": "multipart/form-data; boundary=bb"})
+    assert r.status_code == 400, r.text
+
+
+def test_decoded_pixel_cap(client, monkeypatch):
+    """Images above the service's pixel cap are rejected as 400 before they are decoded."""
+    import numpy as np
+
+    client, _ = client
+    from deconv_api_amd.codec import image as ci
+    from deconv_api_amd.codec import make_data_url
+
+    monkeypatch.setattr(ci, "MAX_PIXELS", 1000)
+    url = make_data_url(np.zeros((40, 40, 3), np.uint8), "PNG")
+    r = client.post("/", data={"file": url, "layer": "block1_conv1"})
+    assert r.status_code == 400 and "too large" in r.json()["detail"], r.text

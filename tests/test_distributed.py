@@ -85,8 +85,7 @@ def _worker_sharded(rank, world, port, q):
             out2 = runner.run("block1_pool", imgs[:1])
             runner.stop()
             single = ShardedRunner(eng, type(info)(), image_size=32)
-            ref = single._prep(imgs)
-            want = eng.run(ref, "block3_conv2", k=4).mosaic.numpy()
+            want = single._local("block3_conv2", imgs).numpy()
             q.put((rank, out.shape, bool(np.array_equal(out, want)), out2.shape))
         else:
             n = runner.follow()
@@ -109,9 +108,9 @@ def test_sharded_deconv_matches_single():
     assert r1[1] == 2, r1
 
 
-def _worker_failover(rank, world, port, q):
+def _worker_failover(rank, world, port, q, dead_rank):
     try:
-        os.environ["DV_FAULT"] = "exit@2/rank=1"  # rank 1 dies when its 2nd batch arrives
+        os.environ["DV_FAULT"] = f"exit@2/rank={dead_rank}"  # that rank dies when its 2nd batch arrives
         from deconv_api_amd.engine.deconvnet import DeconvNet
         from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
         from deconv_api_amd.parallel.sharded import ShardedRunner
@@ -119,38 +118,65 @@ def _worker_failover(rank, world, port, q):
         info = _init(rank, world, port)
         specs = vgg16_specs(width_div=8, image_size=32, fc=64, classes=10)
         eng = DeconvNet(VGG16.random(0, specs=specs).build("cpu", torch.float32))
-        runner = ShardedRunner(eng, info, image_size=32)
+        runner = ShardedRunner(eng, info, image_size=32, hb_timeout=1.0)
         if rank == 0:
             rng = np.random.default_rng(1)
-            imgs = [rng.integers(0, 256, (32, 32, 3), dtype=np.uint8) for _ in range(4)]
-            a = runner.run("block2_conv1", imgs)       # sharded over both ranks
-            b = runner.run("block2_conv1", imgs)       # rank 1 exits mid-batch -> failover
-            c = runner.run("block2_conv1", imgs[:2])   # degraded: rank 0 alone
-            want = runner._local("block2_conv1", imgs).numpy()
-            q.put((rank, bool(np.array_equal(a, want)), bool(np.array_equal(b, want)), runner.degraded,
-                   c.shape))
+            imgs = [rng.integers(0, 256, (32, 32, 3), dtype=np.uint8) for _ in range(5)]
+            a = runner.run("block2_conv1", imgs)      # sharded over every rank
+            w1 = runner.world
+            b = runner.run("block2_conv1", imgs)      # dead_rank exits mid-batch -> re-form, recompute
+            w2 = runner.world
+            c = runner.run("block2_conv1", imgs[:3])  # on the survivors
+            single = ShardedRunner(eng, type(info)(), image_size=32)
+            want = single._local("block2_conv1", imgs).numpy()
+            want_c = single._local("block2_conv1", imgs[:3]).numpy()
+            # the service's /ready reports the re-formed world
+            from deconv_api_amd.serve.service import DeconvService
+
+            svc = DeconvService(engine=eng, runner=runner)
+            st = svc.status()
+            svc.close()
+            runner.stop()
+            q.put((rank, bool(np.array_equal(a, want)), bool(np.array_equal(b, want)),
+                   bool(np.array_equal(c, want_c)), (w1, w2, runner.world, st["world"], runner.reforms)))
         else:
-            runner.follow()
-            q.put((rank, "follower returned", None, None, None))
+            n = runner.follow()
+            q.put((rank, "follower returned", n, runner.world, None))
+        from deconv_api_amd.parallel import dist as pdist
+
+        pdist.shutdown()
     except Exception:  # noqa: BLE001
         import traceback
 
         q.put((rank, traceback.format_exc(), None, None, None))
 
 
-def test_follower_failure_failover():
+@pytest.mark.parametrize("world,dead", [(2, 1), (3, 2), (3, 1)])
+def test_follower_failure_reforms_group(world, dead):
+    """A follower dies during its 2nd batch: rank 0 detects it at the next ack (stale heartbeat),
+    the survivors re-form the process group (renumbered), the batch is recomputed on them and
+    equals the single-process result; /ready reports the new world."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker_failover, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker_failover, args=(r, world, port, q, dead)) for r in range(world)]
     for p in ps:
         p.start()
-    r0 = q.get(timeout=300)
+    res = {}
+    for _ in range(world - 1):  # the dead rank reports nothing
+        r = q.get(timeout=300)
+        res[r[0]] = r
     for p in ps:
         p.join(timeout=60)
-    assert r0[0] == 0, r0
-    assert r0[1] is True and r0[2] is True and r0[3] is True and r0[4] == (2, 64, 64, 3), r0
-    assert ps[1].exitcode == 17
+    assert 0 in res, res
+    r0 = res[0]
+    assert r0[1] is True and r0[2] is True and r0[3] is True, r0
+    assert r0[4] == (world, world - 1, world - 1, world - 1, 1), r0
+    assert ps[dead].exitcode == 17
+    for r in range(1, world):
+        if r != dead:
+            # batch 1, batch 2 recomputed after the re-form, batch 3 (the aborted try does not count)
+            assert res[r][1] == "follower returned" and res[r][2] == 3 and res[r][3] == world - 1, res[r]
 
 
 def test_fault_spec_parse():

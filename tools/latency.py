@@ -77,6 +77,46 @@ async def serve_load(svc, layer, clients, total, size):
             "p50_ms": round(p(lat, 0.5), 2), "p99_ms": round(p(lat, 0.99), 2)}
 
 
+class Sampler:
+    """Poor man's sampling profiler: every ``period`` s, the innermost Python frame of every
+    thread (function, file:line) is counted; shows where the host time of the service goes."""
+
+    def __init__(self, period=0.0005):
+        import collections
+        import threading
+
+        self.period = period
+        self.counts = collections.Counter()
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        import threading
+
+        me = threading.get_ident()
+        names = {}
+        while not self.stop.wait(self.period):
+            for tid, fr in sys._current_frames().items():
+                if tid == me:
+                    continue
+                if tid not in names:
+                    names = {t.ident: t.name for t in threading.enumerate()}
+                key = (names.get(tid, "?").split("_")[0], f"{fr.f_code.co_name} {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}")
+                self.counts[key] += 1
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *a):
+        self.stop.set()
+        self.t.join()
+
+    def top(self, n=40):
+        tot = sum(self.counts.values())
+        return [[th, fn, round(c / tot, 4)] for (th, fn), c in self.counts.most_common(n)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layer", default="block5_conv3")
@@ -85,17 +125,33 @@ def main():
     ap.add_argument("--clients", default="1,16,64")
     ap.add_argument("--requests", type=int, default=256)
     ap.add_argument("--img", type=int, default=320, help="client image side (resized to 224 on GPU)")
+    ap.add_argument("--sample", action="store_true", help="sample Python stacks during the last load run")
+    ap.add_argument("--timeout-ms", type=float, default=2.0, help="batcher straggler wait while the GPU is busy")
+    ap.add_argument("--chunk", type=int, default=16, help="images per encode+deliver chunk")
+    ap.add_argument("--codec-workers", type=int, default=16)
     a = ap.parse_args()
     ops.native.load()
     dev = torch.device("cuda", 0)
     eng = DeconvNet(VGG16.random(0).build(dev, torch.bfloat16))
     res = {"engine": engine_latency(eng, a.layer, [int(s) for s in a.sizes.split(",")], a.reps)}
-    cfg = Config.from_env(device="cuda", max_batch=64, batch_timeout_ms=2.0, codec_workers=16)
+    cfg = Config.from_env(device="cuda", max_batch=64, batch_timeout_ms=a.timeout_ms, codec_workers=a.codec_workers,
+                          encode_chunk=a.chunk)
     svc = DeconvService(cfg, engine=eng)
     res["service"] = []
-    for c in (int(x) for x in a.clients.split(",")):
-        res["service"].append(asyncio.run(serve_load(svc, a.layer, c, max(a.requests, c), a.img)))
+    clients = [int(x) for x in a.clients.split(",")]
+    for i, c in enumerate(clients):
+        if a.sample and i == len(clients) - 1:
+            with Sampler() as smp:
+                res["service"].append(asyncio.run(serve_load(svc, a.layer, c, max(a.requests, c), a.img)))
+            res["samples"] = smp.top()
+        else:
+            res["service"].append(asyncio.run(serve_load(svc, a.layer, c, max(a.requests, c), a.img)))
+    from deconv_api_amd.utils import metrics as M
+
+    res["stage_metrics"] = [l for l in M.REGISTRY.render().splitlines() if l.startswith("dv_stage_seconds_sum")
+                            or l.startswith("dv_stage_seconds_count")]
     res["graphs"] = svc.status()["graphs"]
+    res["settings"] = {"timeout_ms": a.timeout_ms, "chunk": a.chunk, "codec_workers": a.codec_workers}
     svc.close()
     print(json.dumps(res))
 
