@@ -38,8 +38,10 @@ class Config:
     max_queue: int = 4096                 # backpressure: 503 beyond this many pending requests
     request_timeout_s: float = 120.0
     codec_workers: int = 8                # decode threads (PIL releases the GIL while decoding)
-    encode_threads: int = 16              # native JPEG encoder threads per batch (GIL released)
+    encode_threads: int = 8               # native JPEG encoder threads per encode call (GIL released)
+    encode_workers: int = 2               # batches encoded concurrently (tools/latency.py A/B: 2 x 8 best)
     encode_chunk: int = 16                # images per encode call; each chunk is delivered at once
+    gil_switch_us: int = 500              # sys.setswitchinterval for the serving process (0 = leave)
     native_codec: bool = True             # native encoder for responses (PIL fallback when False/unbuilt)
     cors_origins: Tuple[str, ...] = ("*",)  # app/main.py:22-32
     host: str = "0.0.0.0"

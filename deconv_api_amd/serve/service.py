@@ -50,6 +50,9 @@ class _Job:
     loop: asyncio.AbstractEventLoop
     future: asyncio.Future
     t_enq: float = field(default_factory=time.perf_counter)
+    t_launch: float = 0.0
+    t_gpu: float = 0.0
+    t_enc: float = 0.0
 
 
 def load_model(cfg: Config) -> VGG16:
@@ -68,6 +71,12 @@ class DeconvService:
         across all ranks' GPUs and the mosaics all-gathered over RCCL."""
         self.cfg = cfg or Config.from_env()
         self.runner = runner
+        if self.cfg.gil_switch_us > 0:
+            # many short GIL sections hop between ~6 threads per request (event loop, codec pool,
+            # worker, completion); the default 5 ms switch interval turns each hop into a wait
+            import sys
+
+            sys.setswitchinterval(self.cfg.gil_switch_us / 1e6)
         dev = self.cfg.resolve_device() if runner is None else str(runner.info.device)
         self.device = torch.device(dev)
         if self.device.type == "cuda" and self.device.index is None:
@@ -91,6 +100,9 @@ class DeconvService:
         elif runner is not None and runner.graphs is not None:
             self.graphs = runner.graphs  # the runner replays its own per-(layer, shard) graphs
         self.codec = CodecPool(self.cfg.codec_workers)
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.enc_ex = ThreadPoolExecutor(max(1, self.cfg.encode_workers), thread_name_prefix="dv-encode")
         from ..codec.image import _native
 
         self.native_codec = bool(self.cfg.native_codec and _native() is not None)
@@ -103,6 +115,7 @@ class DeconvService:
         self.faults = FaultInjector.from_env()
         self._batch_t0: Optional[float] = None
         self.stalled = False
+        self.trace: Optional[list] = None
         self._thread = threading.Thread(target=self._worker, name="dv-gpu-worker", daemon=True)
         self._thread.start()
         self._completer = threading.Thread(target=self._complete, name="dv-completion", daemon=True)
@@ -127,11 +140,15 @@ class DeconvService:
         if self.q.qsize() >= self.cfg.max_queue:
             raise ServiceOverloaded("request queue is full")
         loop = asyncio.get_running_loop()
+        t0 = time.perf_counter()
         img = await loop.run_in_executor(self.codec.ex, read_data_url, uri)
         fut = loop.create_future()
-        self.q.put(_Job(layer, img, loop, fut))
+        job = _Job(layer, img, loop, fut)
+        self.q.put(job)
         M.QUEUE_DEPTH.set(self.q.qsize())
         res = await asyncio.wait_for(fut, timeout=self.cfg.request_timeout_s)
+        if self.trace is not None:  # per-request stage timestamps (tools/latency.py --trace)
+            self.trace.append((t0, job.t_enq, job.t_launch, job.t_gpu, job.t_enc, time.perf_counter()))
         if isinstance(res, str):  # encoded natively, batch-wide, by the completion thread
             return res
         return await loop.run_in_executor(self.codec.ex, encode_data_url, res, self.cfg.jpeg_quality)
@@ -154,6 +171,7 @@ class DeconvService:
         self._thread.join(timeout=5)
         self.done_q.put(None)
         self._completer.join(timeout=5)
+        self.enc_ex.shutdown(wait=True)
         self.codec.shutdown()
 
     # ------------------------------------------------------------------ GPU worker
@@ -205,6 +223,8 @@ class DeconvService:
                 t0 = time.perf_counter()
                 self._batch_t0 = t0
                 try:
+                    for j in group:
+                        j.t_launch = t0
                     handle = self.launch_batch(layer, [j.image for j in group])
                     self.done_q.put((handle, group, layer, t0))
                 except Exception as e:  # noqa: BLE001 - delivered to every waiting request
@@ -212,6 +232,9 @@ class DeconvService:
                     self._fail(group, e)
 
     def _complete(self):
+        """Waits for each batch's copy-back in launch order, then hands the batch to the encode
+        pool: several batches encode concurrently (a small batch alone cannot keep the native
+        encoder's threads busy, and one serial encoder capped the service at ~2k req/s)."""
         while True:
             item = self.done_q.get()
             if item is None:
@@ -219,30 +242,39 @@ class DeconvService:
             handle, group, layer, t0 = item
             try:
                 mos = self.finish_batch(handle)
-                if self.native_codec:
-                    # GIL-free native JPEG + base64 + quote, in chunks of ``encode_chunk`` images
-                    # spread over the native threads (a lone request is split into restart
-                    # segments); each chunk is delivered as soon as it is encoded, so the first
-                    # requests of a batch do not wait for the whole batch's encode
-                    step = max(1, self.cfg.encode_chunk)
-                    for c0 in range(0, len(group), step):
-                        urls = encode_data_urls(mos[c0:c0 + step], self.cfg.jpeg_quality, self.cfg.encode_threads)
-                        for j, m in zip(group[c0:c0 + step], urls):
-                            _deliver(j.loop, _set_result, j.future, m)
-                else:
-                    for j, m in zip(group, mos):
-                        _deliver(j.loop, _set_result, j.future, m)
-                dt = time.perf_counter() - t0
-                self.batches += 1
-                self.images += len(group)
-                M.BATCH_SIZE.observe(len(group))
-                M.ENGINE_TIME.observe(dt, stage="batch")
-                M.IMAGES.inc(len(group), layer=layer)
+                tg = time.perf_counter()
+                for j in group:
+                    j.t_gpu = tg
+                self.enc_ex.submit(self._encode_deliver, group, mos, layer, t0)
             except Exception as e:  # noqa: BLE001
                 self._fail(group, e)
             finally:
                 if self.done_q.empty():
                     self._batch_t0 = None
+
+    def _encode_deliver(self, group, mos, layer, t0):
+        try:
+            if self.native_codec:
+                # GIL-free native JPEG + base64 + quote, in chunks of ``encode_chunk`` images over
+                # the native threads (a lone request is split into restart segments); each chunk
+                # is delivered as soon as it is encoded
+                step = max(1, self.cfg.encode_chunk)
+                for c0 in range(0, len(group), step):
+                    urls = encode_data_urls(mos[c0:c0 + step], self.cfg.jpeg_quality, self.cfg.encode_threads)
+                    te = time.perf_counter()
+                    for j, m in zip(group[c0:c0 + step], urls):
+                        j.t_enc = te
+                        _deliver(j.loop, _set_result, j.future, m)
+            else:
+                for j, m in zip(group, mos):
+                    _deliver(j.loop, _set_result, j.future, m)
+            self.batches += 1
+            self.images += len(group)
+            M.BATCH_SIZE.observe(len(group))
+            M.ENGINE_TIME.observe(time.perf_counter() - t0, stage="batch")
+            M.IMAGES.inc(len(group), layer=layer)
+        except Exception as e:  # noqa: BLE001
+            self._fail(group, e)
 
     def _fail(self, group, e):
         self.last_error = repr(e)

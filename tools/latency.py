@@ -129,16 +129,22 @@ def main():
     ap.add_argument("--timeout-ms", type=float, default=2.0, help="batcher straggler wait while the GPU is busy")
     ap.add_argument("--chunk", type=int, default=16, help="images per encode+deliver chunk")
     ap.add_argument("--codec-workers", type=int, default=16)
+    ap.add_argument("--max-batch", type=int, default=64)
+    ap.add_argument("--switch-us", type=int, default=500)
+    ap.add_argument("--enc-workers", type=int, default=2)
+    ap.add_argument("--enc-threads", type=int, default=8)
     a = ap.parse_args()
     ops.native.load()
     dev = torch.device("cuda", 0)
     eng = DeconvNet(VGG16.random(0).build(dev, torch.bfloat16))
     res = {"engine": engine_latency(eng, a.layer, [int(s) for s in a.sizes.split(",")], a.reps)}
-    cfg = Config.from_env(device="cuda", max_batch=64, batch_timeout_ms=a.timeout_ms, codec_workers=a.codec_workers,
-                          encode_chunk=a.chunk)
+    cfg = Config.from_env(device="cuda", max_batch=a.max_batch, batch_timeout_ms=a.timeout_ms, codec_workers=a.codec_workers,
+                          encode_chunk=a.chunk, gil_switch_us=a.switch_us,
+                          encode_workers=a.enc_workers, encode_threads=a.enc_threads)
     svc = DeconvService(cfg, engine=eng)
     res["service"] = []
     clients = [int(x) for x in a.clients.split(",")]
+    svc.trace = []
     for i, c in enumerate(clients):
         if a.sample and i == len(clients) - 1:
             with Sampler() as smp:
@@ -148,10 +154,15 @@ def main():
             res["service"].append(asyncio.run(serve_load(svc, a.layer, c, max(a.requests, c), a.img)))
     from deconv_api_amd.utils import metrics as M
 
+    tr = svc.trace[-min(len(svc.trace), 2000):]
+    if tr:
+        names = ["decode", "queue", "gpu+d2h", "encode", "deliver"]
+        res["breakdown_ms"] = {n: round(1e3 * sum(t[i + 1] - t[i] for t in tr) / len(tr), 2) for i, n in enumerate(names)}
+
     res["stage_metrics"] = [l for l in M.REGISTRY.render().splitlines() if l.startswith("dv_stage_seconds_sum")
                             or l.startswith("dv_stage_seconds_count")]
     res["graphs"] = svc.status()["graphs"]
-    res["settings"] = {"timeout_ms": a.timeout_ms, "chunk": a.chunk, "codec_workers": a.codec_workers}
+    res["settings"] = {"enc": [a.enc_workers, a.enc_threads], "switch_us": a.switch_us, "max_batch": a.max_batch, "timeout_ms": a.timeout_ms, "chunk": a.chunk, "codec_workers": a.codec_workers}
     svc.close()
     print(json.dumps(res))
 
