@@ -57,17 +57,20 @@ def _run(cmd):
 
 
 def build(force: bool = False, jobs: int | None = None, debug: bool = False, verbose: bool = False) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
+    # debug objects live apart so switching modes never mixes -DDV_DEBUG and release objects;
+    # -O1 (not -O0): the kernels' inline-asm immediates need constant folding
+    bdir = BUILD.parent / "native-debug" if debug else BUILD
+    bdir.mkdir(parents=True, exist_ok=True)
     inc, libdirs = _torch_paths()
     headers = sorted(CSRC.glob("*.h"))
     hip_srcs = sorted(CSRC.glob("*.hip"))
-    opt = ["-O0", "-g"] if debug else ["-O3"]
+    opt = ["-O1", "-g"] if debug else ["-O3"]
     defs = ["-DDV_DEBUG=1"] if debug else []
     hipcc = _hipcc()
     objs = []
     tasks = []
     for src in hip_srcs:
-        obj = BUILD / (src.stem + ".o")
+        obj = bdir / (src.stem + ".o")
         objs.append(obj)
         if force or _newer([src, *headers], obj):
             tasks.append([hipcc, *opt, *defs, f"--offload-arch={ARCH}", "-fPIC", "-std=c++17",
@@ -75,13 +78,13 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     for src in sorted(CSRC.glob("*.cpp")):  # host-only C++ (no torch / HIP): the JPEG encoder
         if src.name == "bindings.cpp":
             continue
-        obj = BUILD / (src.stem + ".o")
+        obj = bdir / (src.stem + ".o")
         objs.append(obj)
         if force or _newer([src, *headers], obj):
             tasks.append(["g++", *opt, *defs, "-fPIC", "-std=c++17", "-pthread", "-D_GLIBCXX_USE_CXX11_ABI=1",
                           f"-I{CSRC}", "-c", str(src), "-o", str(obj)])
     bsrc = CSRC / "bindings.cpp"
-    bobj = BUILD / "bindings.o"
+    bobj = bdir / "bindings.o"
     objs.append(bobj)
     if force or _newer([bsrc, *headers], bobj):
         py_inc = sysconfig.get_paths()["include"]
@@ -94,7 +97,7 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
             for out in ex.map(_run, tasks):
                 if verbose and out.strip():
                     print(out)
-    if force or tasks or _newer(objs, TARGET):
+    if force or tasks or debug or _newer(objs, TARGET):
         link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *[str(o) for o in objs], "-o", str(TARGET)]
         for d in libdirs:
             link += [f"-L{d}"]

@@ -70,6 +70,8 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
               "conv: x and w must be 16-byte aligned");
   a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
   a.w = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  a.x_elems = avail_bytes(x) / 2;
+  a.out_elems = avail_bytes(out) / (int64_t)out.element_size();
 
   // input extent
   int64_t in_pix = (int64_t)a.N * a.H * a.W;
@@ -126,6 +128,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                 "res: pixels must be dense");
     need(*res, ((int64_t)(a.M - 1) * a.res_ld + a.OC) * 2, "res");
     a.res = reinterpret_cast<const uint16_t*>(res->data_ptr());
+    a.res_elems = avail_bytes(*res) / 2;
     if (emask.has_value()) {
       check_cuda(*emask, "emask");
       TORCH_CHECK(emask->scalar_type() == dt && emask->dim() == 4 && emask->stride(3) == 1, "emask: x's dtype, NHWC");
@@ -134,6 +137,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                   "emask: pixels must be dense");
       need(*emask, ((int64_t)(a.M - 1) * a.emask_ld + a.OC) * 2, "emask");
       a.emask = reinterpret_cast<const uint16_t*>(emask->data_ptr());
+      a.emask_elems = avail_bytes(*emask) / 2;
     }
   }
   if (emask.has_value() && a.emask == nullptr) {  // output mask without a residual
@@ -145,6 +149,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                 "emask: pixels must be dense");
     need(*emask, ((int64_t)(a.M - 1) * a.emask_ld + a.OC) * 2, "emask");
     a.emask = reinterpret_cast<const uint16_t*>(emask->data_ptr());
+    a.emask_elems = avail_bytes(*emask) / 2;
   }
   {  // LDS-staged vector epilogue: 16-bit rows (out / res / emask) 16-B aligned
     auto al = [](const void* p, int64_t ld) { return reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 8 == 0; };
@@ -253,6 +258,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                                     a.C, a.code_div, a.relu_in, cur_stream()),
                "unpool2x2");
       a.x = reinterpret_cast<const uint16_t*>(unpooled.data_ptr());
+      a.x_elems = unpooled.numel();
       a.x_ld = a.C;
       a.relu_in = 0;
       a.code = nullptr;
@@ -265,6 +271,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       const std::vector<int64_t> st{(int64_t)a.H * a.W * a.x_ld, (int64_t)a.W * a.x_ld, (int64_t)a.x_ld, 1};
       relu_x = at::relu(x.as_strided(sz, st));
       a.x = reinterpret_cast<const uint16_t*>(relu_x.data_ptr());
+      a.x_elems = relu_x.numel();
       if (mask.has_value()) {  // the mask is staged with x's offsets: same dense layout
         dense_mask = mask->as_strided(sz, st).contiguous();
         a.mask = reinterpret_cast<const uint16_t*>(dense_mask.data_ptr());

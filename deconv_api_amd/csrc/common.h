@@ -11,6 +11,26 @@
 
 #include "kernels.h"  // DT_BF16 / DT_F16
 
+// ---- DV_DEBUG device bounds checks (python -m deconv_api_amd._build --debug) ----
+// DV_BOUNDS(off, n, extent, what): in a debug build, an access of n elements at element offset
+// `off` outside [0, extent) prints the kernel site and the offending numbers and evaluates to
+// false, so the caller SKIPS the access instead of faulting (a faulting kernel can reset every
+// GPU on the host); in a release build it is the constant true and compiles away.
+#if defined(DV_DEBUG) && DV_DEBUG
+#define DV_BOUNDS(off, n, extent, what)                                                                    \
+  ([&]() -> bool {                                                                                        \
+    const long long o_ = (long long)(off), n_ = (long long)(n), e_ = (long long)(extent);                \
+    if (o_ < 0 || o_ + n_ > e_) {                                                                         \
+      printf("DV_DEBUG %s:%d %s: access [%lld, %lld) outside [0, %lld) (block %d,%d thread %d)\n", __FILE__, \
+             __LINE__, what, o_, o_ + n_, e_, (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x);        \
+      return false;                                                                                       \
+    }                                                                                                     \
+    return true;                                                                                          \
+  }())
+#else
+#define DV_BOUNDS(off, n, extent, what) true
+#endif
+
 namespace dv {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;

@@ -229,6 +229,8 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
         ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
       }
       ok = ok && kval;
+      ok = ok && DV_BOUNDS((long long)n_base * img_elems + ((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch, 8,
+                           a.x_elems, "conv_dma A gather");
       const uint32_t voff =
           ok ? (uint32_t)((((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch) * 2) : kOOB;
       dma16(xr, As + (j * NW + wave) * 1024, voff);
@@ -241,7 +243,8 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
       if (grp < B_GROUPS) {
         const int row = grp * RPI + lrow;
         const uint32_t voff = (uint32_t)((((long long)(n0 + row)) * a.Kpad + kt * BK + lchunk * 8) * 2);
-        dma16(wr, Bs + grp * 1024, voff);
+        if (DV_BOUNDS((long long)voff / 2, 8, (long long)a.OCpad * a.Kpad, "conv_dma B weights"))
+          dma16(wr, Bs + grp * 1024, voff);
       }
     }
   };
@@ -450,7 +453,8 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
         if (a.relu && a.res) v = fmaxf(v, 0.f);
         const uint32_t e = ev[i][r];
         if (e == 0u || (e & 0x8000u)) v = 0.f;
-        out[(long long)row * a.out_ld + col] = from_f<DT>(v);
+        if (DV_BOUNDS((long long)row * a.out_ld + col, 1, a.out_elems, "conv_dma epilogue_res out"))
+          out[(long long)row * a.out_ld + col] = from_f<DT>(v);
       }
   }
 }
@@ -482,6 +486,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
           }
         }
         const long long prow = rowb >> 2;
+        if (!DV_BOUNDS(prow * a.out_ld + col, 1, a.out_elems, "conv_dma pool epilogue out")) continue;
         reinterpret_cast<uint16_t*>(a.out)[prow * a.out_ld + col] = from_f<DT>(best);
         a.out_code[prow * a.OC + col] = (uint8_t)code;
       } else {
@@ -492,6 +497,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
           float v = acc[i][j][r] + bias;
           if (a.relu) v = fmaxf(v, 0.f);
           const long long o = (long long)row * a.out_ld + col;
+          if (!DV_BOUNDS(o, 1, a.out_elems, "conv_dma epilogue out")) continue;
           if constexpr (EPI == CONV_E_F32) {
             float* out = reinterpret_cast<float*>(a.out);
             if (accum) v += out[o];
@@ -546,6 +552,13 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
     if (grow >= a.M || gcol >= a.OC) continue;
     uint4 v = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((cc ^ (row & SWZ)) << 4));
     const long long o = (long long)grow * a.out_ld + gcol;
+    if (!a.ucode && !DV_BOUNDS(o, gcol + 8 > a.OC ? a.OC - gcol : 8, a.out_elems, "conv_dma epilogue_lds out")) continue;
+    if (a.res && !DV_BOUNDS((long long)grow * a.res_ld + gcol, gcol + 8 > a.OC ? a.OC - gcol : 8, a.res_elems,
+                            "conv_dma epilogue_lds res"))
+      continue;
+    if (a.emask && !DV_BOUNDS((long long)grow * a.emask_ld + gcol, gcol + 8 > a.OC ? a.OC - gcol : 8, a.emask_elems,
+                              "conv_dma epilogue_lds emask"))
+      continue;
     if (gcol + 8 > a.OC) {  // a row's last partial chunk: element-wise (no 16-B access past OC)
       const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
       for (int e = 0; e < a.OC - gcol; ++e) {
@@ -605,7 +618,8 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
           ov[e] = (c0 == (uint32_t)pos ? vv[e] & 0xFFFFu : 0u) | (c1 == (uint32_t)pos ? vv[e] & 0xFFFF0000u : 0u);
         }
         const long long po = ob + ((long long)(pos >> 1) * 2 * a.OW + (pos & 1)) * a.out_ld;
-        *reinterpret_cast<uint4*>(out + po) = uint4{ov[0], ov[1], ov[2], ov[3]};
+        if (DV_BOUNDS(po, 8, a.out_elems, "conv_dma unpool-out store"))
+          *reinterpret_cast<uint4*>(out + po) = uint4{ov[0], ov[1], ov[2], ov[3]};
       }
       continue;
     }
@@ -1050,6 +1064,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a, in
     for (int k = 0; k < a.ksplit; ++k) v += w[k * plane];
     if (a.relu) v = fmaxf(v, 0.f);
     const long long o = (long long)row * a.out_ld + col;
+    if (!DV_BOUNDS(o, 1, a.out_elems, "splitk_reduce out")) continue;
     if (epi == CONV_E_F32)
       reinterpret_cast<float*>(a.out)[o] = v;
     else

@@ -251,13 +251,14 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
           best[r] = m;
           codes |= c << (8 * r);
         }
-        if (st && oc + 4 <= a.OC) {
+        if (st && oc + 4 <= a.OC && DV_BOUNDS(prow * a.out_ld + oc, 4, a.out_elems, "halo-stream pool out")) {
           *reinterpret_cast<uint2*>(out + prow * a.out_ld + oc) =
               make_uint2(pack2<DT>(best[0], best[1]), pack2<DT>(best[2], best[3]));
           *reinterpret_cast<uint32_t*>(a.out_code + prow * a.OC + oc) = codes;
         } else if (st && oc < a.OC) {
           for (int r = 0; r < a.OC - oc; ++r) {
-            out[prow * a.out_ld + oc + r] = from_f<DT>(best[r]);
+            if (DV_BOUNDS(prow * a.out_ld + oc + r, 1, a.out_elems, "halo-stream pool out"))
+              out[prow * a.out_ld + oc + r] = from_f<DT>(best[r]);
             a.out_code[prow * a.OC + oc + r] = (uint8_t)(codes >> (8 * r));
           }
         }
@@ -540,7 +541,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
           best[r] = m;
           codes |= cc << (8 * r);
         }
-        if (st && oc < a.OC) {
+        if (st && oc < a.OC && DV_BOUNDS(prow * a.out_ld + oc, 4, a.out_elems, "hs16 pool out")) {
           *reinterpret_cast<uint2*>(out + prow * a.out_ld + oc) =
               make_uint2(pack2<DT>(best[0], best[1]), pack2<DT>(best[2], best[3]));
           *reinterpret_cast<uint32_t*>(a.out_code + prow * a.OC + oc) = codes;
@@ -559,7 +560,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
       if (oc >= a.OC) continue;
       const float v0 = fmaxf(acc[i][j][0] + bv[j].x, lo), v1 = fmaxf(acc[i][j][1] + bv[j].y, lo);
       const float v2 = fmaxf(acc[i][j][2] + bv[j].z, lo), v3 = fmaxf(acc[i][j][3] + bv[j].w, lo);
-      *reinterpret_cast<uint2*>(orow + oc) = make_uint2(pack2<DT>(v0, v1), pack2<DT>(v2, v3));
+      if (DV_BOUNDS((((long long)n * H + oy) * W + ox) * a.out_ld + oc, 4, a.out_elems, "hs16 out"))
+        *reinterpret_cast<uint2*>(orow + oc) = make_uint2(pack2<DT>(v0, v1), pack2<DT>(v2, v3));
     }
   }
 }

@@ -52,6 +52,9 @@ struct ConvArgs {
   int stats_div;
   const uint8_t* ucode;   // optional (LDS-DMA, vector epilogue): max-unpool the output with these switch
   int ucode_div;          //   codes [N/ucode_div][OH][OW][OC]; out is then [N][2 OH][2 OW] rows of out_ld
+  // storage extents in elements from each base pointer (bindings.cpp: storage bytes past the data
+  // pointer); read only by the DV_DEBUG bounds checks (common.h DV_BOUNDS)
+  long long x_elems, out_elems, res_elems, emask_elems;
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
