@@ -192,8 +192,9 @@ __global__ void __launch_bounds__(512, 1) conv3x3_c64_persist_kernel(const ConvA
           float v = acc[i][j][r] + bias;
           if (a.relu) v = fmaxf(v, 0.f);
           const long long o = (((long long)n * H + oy) * W + ox) * a.out_ld + oc;
+          if (!DV_BOUNDS(o, 1, a.out_elems, "halo conv out")) continue;
           if constexpr (EPI == CONV_E_F32)
-            if (DV_BOUNDS(o, 1, a.out_elems, "halo conv out")) reinterpret_cast<float*>(a.out)[o] = v;
+            reinterpret_cast<float*>(a.out)[o] = v;
           else
             reinterpret_cast<uint16_t*>(a.out)[o] = f2bf(v);
         }
@@ -592,8 +593,9 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_stream_kernel(const ConvAr
             st1 += v;
             st2 += (double)v * v;
             const long long o = (obase + (ox - x0)) * a.out_ld + col;
+            if (!DV_BOUNDS(o, 1, a.out_elems, "stream conv out")) continue;
             if constexpr (EPI == CONV_E_F32)
-              if (DV_BOUNDS(o, 1, a.out_elems, "halo conv out")) reinterpret_cast<float*>(a.out)[o] = v;
+              reinterpret_cast<float*>(a.out)[o] = v;
             else
               reinterpret_cast<uint16_t*>(a.out)[o] = f2bf(v);
           }
