@@ -41,7 +41,8 @@ void check_rc(int rc, const char* what) {
 void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
           c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
           int64_t epi, int64_t impl, c10::optional<Tensor> res, c10::optional<Tensor> emask,
-          c10::optional<Tensor> stats, int64_t stats_div, c10::optional<Tensor> ucode, int64_t ucode_div) {
+          c10::optional<Tensor> stats, int64_t stats_div, c10::optional<Tensor> ucode, int64_t ucode_div,
+          int64_t relu_cols) {
   TORCH_CHECK(g.size() == 23, "conv: geometry vector must have 23 entries");
   check_cuda(x, "x");
   check_cuda(w, "w");
@@ -54,6 +55,9 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   a.K = (int)g[13]; a.Kpad = (int)g[14]; a.M = (int)g[15];
   a.relu = (int)g[16]; a.relu_in = (int)g[17]; a.accumulate = (int)g[18];
   a.code_div = (int)g[19]; a.x_ld = g[20]; a.mask_ld = g[21]; a.out_ld = g[22];
+  a.relu_cols = (int)relu_cols;
+  TORCH_CHECK(relu_cols == 0 || (impl == 2 && relu_cols > 0 && relu_cols <= a.OC && epi != dv::CONV_E_POOL),
+              "conv: relu_cols needs the LDS-DMA kernel (impl 2) and 0 < relu_cols <= OC");
 
   const auto dt = x.scalar_type();
   TORCH_CHECK((dt == at::kBFloat16 || dt == at::kHalf) && w.scalar_type() == dt, "conv: x, w must both be bf16 or fp16");
@@ -752,7 +756,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("out_code"), py::arg("code"),
         py::arg("mask"), py::arg("geom"), py::arg("amode"), py::arg("epi"), py::arg("impl"),
         py::arg("res") = py::none(), py::arg("emask") = py::none(), py::arg("stats") = py::none(),
-        py::arg("stats_div") = 1, py::arg("ucode") = py::none(), py::arg("ucode_div") = 1);
+        py::arg("stats_div") = 1, py::arg("ucode") = py::none(), py::arg("ucode_div") = 1,
+        py::arg("relu_cols") = 0);
   m.def("dma_tune", [](int64_t cfg, int64_t ks) { dv::conv_dma_tune((int)cfg, (int)ks); },
         "force the LDS-DMA conv tile config / split-K factor (0 = automatic); tuning only");
   m.def("pool", &pool, "k x k max/avg pooling forward/backward", py::arg("in"), py::arg("out"), py::arg("idx"),

@@ -33,6 +33,13 @@
 
 namespace dv {
 
+// ReLU of output column gcol of a conv (ConvArgs::relu / relu_cols); a template so it also works
+// for argument structs without the field
+template <class A>
+__device__ __forceinline__ bool relu_at(const A& a, int gcol) {
+  return a.relu && (a.relu_cols <= 0 || gcol < a.relu_cols);
+}
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 

@@ -447,10 +447,10 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
         const int row = mw + i * 16 + row_l + r;
         if (row >= a.M) continue;
         float v = acc[i][j][r] + bias;
-        if (a.relu && !a.res) v = fmaxf(v, 0.f);  // same order as epilogue_lds
+        if (relu_at(a, col) && !a.res) v = fmaxf(v, 0.f);  // same order as epilogue_lds
         v += to_f<DT>(rv[i][r]);
         if (a.accumulate) v += to_f<DT>(out[(long long)row * a.out_ld + col]);
-        if (a.relu && a.res) v = fmaxf(v, 0.f);
+        if (relu_at(a, col) && a.res) v = fmaxf(v, 0.f);
         const uint32_t e = ev[i][r];
         if (e == 0u || (e & 0x8000u)) v = 0.f;
         if (DV_BOUNDS((long long)row * a.out_ld + col, 1, a.out_elems, "conv_dma epilogue_res out"))
@@ -495,7 +495,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
           const int row = rowb + r;
           if (row >= a.M) continue;
           float v = acc[i][j][r] + bias;
-          if (a.relu) v = fmaxf(v, 0.f);
+          if (relu_at(a, col)) v = fmaxf(v, 0.f);
           const long long o = (long long)row * a.out_ld + col;
           if (!DV_BOUNDS(o, 1, a.out_elems, "conv_dma epilogue out")) continue;
           if constexpr (EPI == CONV_E_F32) {
@@ -538,7 +538,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
       for (int r = 0; r < 4; ++r) {
         const int row = wm * FM * 16 + i * 16 + row_l + r;
         float v = acc[i][j][r] + bias;
-        if (pre_relu) v = fmaxf(v, 0.f);
+        if (pre_relu && relu_at(a, gcol)) v = fmaxf(v, 0.f);
         *reinterpret_cast<uint16_t*>(smem + row * (BN * 2) + ((((col >> 3) ^ (row & SWZ))) << 4) + (col & 7) * 2) =
             from_f<DT>(v);
       }
@@ -566,7 +566,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
         if (a.accumulate) f += to_f<DT>(out[o + e]);
         if (a.res) {
           f += to_f<DT>(a.res[(long long)grow * a.res_ld + gcol + e]);
-          if (a.relu) f = fmaxf(f, 0.f);
+          if (relu_at(a, gcol + e)) f = fmaxf(f, 0.f);
         }
         if (a.emask) {
           const uint32_t m = a.emask[(long long)grow * a.emask_ld + gcol + e];
@@ -1062,7 +1062,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a, in
     const float* w = a.ws + (long long)row * a.OCpad + col;
     float v = a.bias ? a.bias[col] : 0.f;
     for (int k = 0; k < a.ksplit; ++k) v += w[k * plane];
-    if (a.relu) v = fmaxf(v, 0.f);
+    if (relu_at(a, col)) v = fmaxf(v, 0.f);
     const long long o = (long long)row * a.out_ld + col;
     if (!DV_BOUNDS(o, 1, a.out_elems, "splitk_reduce out")) continue;
     if (epi == CONV_E_F32)

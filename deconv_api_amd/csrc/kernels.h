@@ -55,6 +55,8 @@ struct ConvArgs {
   // storage extents in elements from each base pointer (bindings.cpp: storage bytes past the data
   // pointer); read only by the DV_DEBUG bounds checks (common.h DV_BOUNDS)
   long long x_elems, out_elems, res_elems, emask_elems;
+  int relu_cols;          // > 0: ReLU only on output columns < relu_cols (merged GEMMs whose trailing
+                          //   columns are pre-activation values, ops/inception.py); 0: every column
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);

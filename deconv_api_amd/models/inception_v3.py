@@ -98,6 +98,8 @@ class InceptionV3:
         self.dtype = dtype
         for u in self.units.values():
             u.build(self.device, dtype)
+        for blk in self.iblocks:  # merged head GEMMs (GPU)
+            blk.build(self.device, dtype)
         return self
 
     def num_params(self) -> int:

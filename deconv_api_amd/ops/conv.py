@@ -216,7 +216,7 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
            out: Optional[torch.Tensor] = None, accumulate: bool = False, out_hw=None,
            use_bias: bool = True, res: Optional[torch.Tensor] = None, emask: Optional[torch.Tensor] = None,
            stats: Optional[torch.Tensor] = None, stats_div: int = 1, unpool_out: Optional[torch.Tensor] = None,
-           unpool_div: int = 1):
+           unpool_div: int = 1, relu_cols: int = 0):
     """NHWC convolution.
 
     x: [N, H, W, C] (channel-slice views allowed: stride(3) == 1). For ``in_mode='unpool'`` x is
@@ -228,6 +228,8 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     group of ``stats_div`` output images (the single-pass mosaic deprocess consumes it).
     ``unpool_out``: switch codes [N / unpool_div, OH, OW, OC]; the result is max-unpooled in the
     epilogue and returned at [N, 2 OH, 2 OW, OC] (the deconvnet's conv-down feeding an unpool).
+    ``relu_cols`` > 0: ``relu`` applies to output channels < relu_cols only (a merged GEMM whose
+    trailing channels are pre-activation values; LDS-DMA kernel).
     """
     if pad is None:
         pad = (cw.KH // 2, cw.KW // 2)
@@ -253,7 +255,7 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     if x.is_cuda:
         return _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
                            mask, epilogue, out, accumulate, use_bias, res, emask, stats, stats_div, unpool_out,
-                           unpool_div)
+                           unpool_div, relu_cols)
     assert stats is None, "conv2d: stats are produced by the GPU kernels only"
     if unpool_out is not None:
         assert epilogue == "bf16" and out is None and not accumulate, "conv2d: unpool_out needs a fresh 16-bit output"
@@ -261,11 +263,11 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
                         mask, epilogue, None, False, use_bias, res, emask)
         return unpool_ref(y, unpool_out, unpool_div).contiguous()
     return _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
-                       mask, epilogue, out, accumulate, use_bias, res, emask)
+                       mask, epilogue, out, accumulate, use_bias, res, emask, relu_cols)
 
 
 def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
-                epilogue, out, accumulate, use_bias, res=None, emask=None):
+                epilogue, out, accumulate, use_bias, res=None, emask=None, relu_cols=0):
     dtype = x.dtype
     xf = x.float()
     if in_mode == "unpool":
@@ -290,7 +292,9 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
     y = Y.permute(0, 2, 3, 1)
     if res is not None:
         y = y + res.float()
-    if relu:
+    if relu and relu_cols > 0:
+        y = torch.cat([y[..., :relu_cols].clamp_min(0), y[..., relu_cols:]], dim=-1)
+    elif relu:
         y = y.clamp_min(0)
     if emask is not None:
         y = y * (emask.float() > 0)
@@ -313,7 +317,7 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
 
 def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
                 epilogue, out, accumulate, use_bias, res=None, emask=None, stats=None, stats_div=1,
-                unpool_out=None, unpool_div=1):
+                unpool_out=None, unpool_div=1, relu_cols=0):
     lib = native.lib()
     dt = x.dtype
     assert dt in (torch.bfloat16, torch.float16) and x.stride(3) == 1, \
@@ -350,9 +354,10 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
     geom = [N, H, W, C, OH, OW, OC, cw.OCpad, cw.KH, cw.KW, stride, pad[0], pad[1], cw.K, cw.Kpad, M,
             int(relu), int(relu_in), int(accumulate), int(code_div), x_ld, mask_ld, out_ld]
     bias = cw.bias_pad if use_bias else None
+    dma_only = res is not None or emask is not None or unpool_out is not None or relu_cols > 0
     lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
-             IMPL[_policy["impl"]] if res is None and emask is None and unpool_out is None else IMPL["dma"],
-             res, emask, stats, stats_div, unpool_out, unpool_div)  # res / emask / unpool_out: DMA-only epilogues
+             IMPL["dma"] if dma_only else IMPL[_policy["impl"]],  # DMA-only epilogue features
+             res, emask, stats, stats_div, unpool_out, unpool_div, relu_cols)
     if epilogue == "pool":
         return out, out_code
     return out

@@ -11,6 +11,12 @@ GPU design (every op a HIP kernel, no torch glue):
   * the pool branch ``avg -> 1x1 conv`` runs as ``1x1 conv -> avg + bias + ReLU``: both are
     linear and the pool's divisor does not depend on the channel, so they commute; the pool then
     runs over the conv's 32-192 output channels instead of the 192-768 input channels;
+  * every 1x1 head conv on the block input that is NOT a branch's only op (b5a, b3a, b7a, b7da,
+    the commuted pool conv) is ONE merged GEMM T = x @ [W_b5a | W_b3a | W_pool] with bias + ReLU
+    on the leading columns only (``relu_cols``; the pool columns stay pre-activation); the
+    branches read their heads as channel slices of T. Backward, the heads' gradients are written
+    into the matching slices of one G_T and ONE dgrad GEMM (K = all head channels) accumulates
+    them into gx: 2-3 launches fewer per block each way (the small-map blocks are launch-bound);
   * backward reads gY's channel slices in place; every contribution to the block-input gradient
     gx is written by one kernel epilogue into the same buffer (the first writes, the rest use the
     ``accumulate`` epilogue), with the ReLU mask of x (``emask``) fused there: no add kernels, no
@@ -43,6 +49,40 @@ class InceptionBlock:
         self.order = list(order)
         self.branches = [branches[k] for k in self.order]
         self.units = units
+        self.merge = None  # (fwd ConvWeights, bwd ConvWeights, relu_cols, {branch index: (offset, width)})
+
+    @staticmethod
+    def _is_head(u: ConvUnit) -> bool:
+        return tuple(u.w.shape[2:]) == (1, 1) and u.stride == 1 and tuple(u.pad) == (0, 0)
+
+    def build(self, device, dtype) -> "InceptionBlock":
+        """GPU: pack the merged head GEMM (see module doc) when >= 2 heads qualify."""
+        from .conv import ConvWeights, pad_channels_oihw
+
+        self.merge = None
+        if torch.device(device).type != "cuda":
+            return self
+        relu_m, pre_m = [], []
+        for bi, ops in enumerate(self.branches):
+            if ops[0] == "avg":
+                pre_m.append((bi, self.units[ops[1]]))
+            elif isinstance(ops[0], str) and ops[0] != "max" and len(ops) > 1 and self._is_head(self.units[ops[0]]):
+                relu_m.append((bi, self.units[ops[0]]))
+        members = relu_m + pre_m
+        if len(members) < 2:
+            return self
+        cols, off = {}, 0
+        ws, bs = [], []
+        for k, (bi, u) in enumerate(members):
+            cols[bi] = (off, u.cout)
+            off += u.cout
+            ws.append(u.w)
+            bs.append(u.b if k < len(relu_m) else torch.zeros_like(u.b))  # pool bias: after the avg
+        w = pad_channels_oihw(torch.cat(ws, 0))                             # [Ntot, Cin8, 1, 1]
+        fwd = ConvWeights(w, torch.cat(bs, 0), "fwd").to_device(device, dtype)
+        bwd = ConvWeights(pad_channels_oihw(w.transpose(0, 1).contiguous()), None, "fwd").to_device(device, dtype)
+        self.merge = (fwd, bwd, sum(u.cout for _, u in relu_m), cols)
+        return self
 
     # ------------------------------------------------------------------ shapes
     def branch_width(self, ops, cin: int) -> int:
@@ -104,26 +144,44 @@ class _InceptionFn(torch.autograd.Function):
         widths = blk.widths(Cin)
         Y = torch.empty(N, OH, OW, sum(widths), dtype=x.dtype, device=x.device)
         saved = [x, Y]
-        plan = []  # per branch: (offset, width, kind, [saved tensor indices / unit names])
+        T = None
+        mcols = {}
+        if blk.merge is not None:  # every qualifying 1x1 head in one GEMM (pool columns pre-activation)
+            mfwd, _, relu_n, mcols = blk.merge
+            T = conv2d(x, mfwd, stride=1, pad=(0, 0), relu=True, use_bias=True, relu_cols=relu_n)
+            saved.append(T)
+        plan = []  # per branch: (offset, width, kind, info)
         off = 0
-        for ops, wdt in zip(blk.branches, widths):
+        for bi, (ops, wdt) in enumerate(zip(blk.branches, widths)):
             ysl = Y[..., off:off + wdt]
             if ops[0] == "avg":  # avg -> 1x1 conv  ==  1x1 conv (no bias) -> avg + bias + ReLU
                 assert len(ops) == 2 and isinstance(ops[1], str), "avg branch: avg-pool then one 1x1 conv"
                 u = blk.units[ops[1]]
                 assert u.w.shape[2:] == (1, 1) and u.stride == 1
-                t = _conv_fwd(u, x, relu=False, bias=False)
+                if bi in mcols:
+                    mo, mw = mcols[bi]
+                    t = T[..., mo:mo + mw]
+                else:
+                    t = _conv_fwd(u, x, relu=False, bias=False)
                 lib.pool(t, ysl, None, 1, 0, _pool_geom(N, H, W, u.cout, 3, 1, 1), u.fwd.bias_pad, True)
-                plan.append((off, wdt, "avg", [u.name]))
+                plan.append((off, wdt, "avg", [u.name, mcols.get(bi)]))
             elif ops == ["max"]:
                 idx = torch.empty(N, OH, OW, Cin, dtype=torch.uint8, device=x.device)
                 lib.pool(x, ysl, idx, 0, 0, _pool_geom(N, H, W, Cin, 3, 2, 0))
                 saved.append(idx)
                 plan.append((off, wdt, "max", [len(saved) - 1]))
             else:
-                steps = []  # (unit name(s), index of its saved input)
+                steps = []  # (unit name(s), index of its saved input | ("T", cols) for a merged head)
                 cur, cur_i = x, 0
-                for j, op in enumerate(ops):
+                start = 0
+                if bi in mcols:  # the head ran in the merged GEMM: its output is a slice of T
+                    mo, mw = mcols[bi]
+                    cur = T[..., mo:mo + mw]
+                    cur_i = ("T", mo, mw)
+                    steps.append(((ops[0],), "merged"))
+                    start = 1
+                for j in range(start, len(ops)):
+                    op = ops[j]
                     last = j == len(ops) - 1
                     if isinstance(op, tuple):
                         assert last, "split must end its branch"
@@ -141,6 +199,7 @@ class _InceptionFn(torch.autograd.Function):
             off += wdt
         ctx.blk = blk
         ctx.plan = plan
+        ctx.merged = T is not None
         ctx.premasked = _PREMASKED[0]
         ctx.x_relu = _is_relu_out(x)
         ctx.save_for_backward(*saved)
@@ -152,17 +211,25 @@ class _InceptionFn(torch.autograd.Function):
         blk: InceptionBlock = ctx.blk
         saved = ctx.saved_tensors
         x, Y = saved[0], saved[1]
+        T = saved[2] if ctx.merged else None
         N, H, W, Cin = x.shape
         gY = gY.contiguous()
         if not ctx.premasked:
             gY = torch.ops.aten.threshold_backward(gY, Y, 0)
         emask_x = x if (ctx.premasked and ctx.x_relu) else None
         gx = torch.empty_like(x)
+        GT = torch.empty_like(T) if T is not None else None
         state = {"written": False, "masked": False}
 
-        def contribute_conv(u: ConvUnit, g, emask):
-            """gradient of conv unit u (stride 1) w.r.t. its input, written/accumulated into gx"""
-            conv2d(g, u.bwd, stride=1, pad=u.bwd_pad, relu=False, use_bias=False, out=gx,
+        def inp_of(in_i):
+            if isinstance(in_i, tuple):  # merged head output: slice of T
+                return T[..., in_i[1]:in_i[1] + in_i[2]]
+            return saved[in_i]
+
+        def contribute_conv(cw, g, emask):
+            """gradient of a stride-1 conv (packed transposed weights cw) w.r.t. its input,
+            written (first contribution) or accumulated into gx, x-mask fused when given"""
+            conv2d(g, cw, stride=1, pad=(cw.KH // 2, cw.KW // 2), relu=False, use_bias=False, out=gx,
                    accumulate=state["written"], emask=emask)
             state["written"] = True
             state["masked"] = emask is not None
@@ -175,7 +242,17 @@ class _InceptionFn(torch.autograd.Function):
             state["written"] = True
             state["masked"] = False
 
-        deferred = []  # stride-1 head-conv contributions go last: their epilogue applies the x mask
+        def dgrad_into(u, g, inp, out=None, accumulate=False):
+            """gradient w.r.t. ``inp`` (a ReLU output) of conv unit u, masked by inp > 0"""
+            if u.stride == 1:
+                return conv2d(g, u.bwd, stride=1, pad=u.bwd_pad, relu=False, use_bias=False, emask=inp, out=out,
+                              accumulate=accumulate)
+            r = torch.ops.aten.threshold_backward(_dgrad_strided(u, g, None, (inp.shape[1], inp.shape[2])), inp, 0)
+            if out is None:
+                return r
+            return out.add_(r) if accumulate else out.copy_(r)
+
+        deferred = []  # head-conv contributions on x go last: their epilogue applies the x mask
         for off, wdt, kind, info in ctx.plan:
             gsl = gY[..., off:off + wdt]
             if kind == "max":
@@ -190,41 +267,43 @@ class _InceptionFn(torch.autograd.Function):
                 continue
             if kind == "avg":
                 u = blk.units[info[0]]
-                gp = torch.empty(N, H, W, u.cout, dtype=gY.dtype, device=gY.device)
-                lib.pool(gsl, gp, None, 1, 1, _pool_geom(N, H, W, u.cout, 3, 1, 1))
-                deferred.append((u, gp))
+                if info[1] is not None:  # merged: the pooled gradient lands in its G_T columns
+                    mo, mw = info[1]
+                    lib.pool(gsl, GT[..., mo:mo + mw], None, 1, 1, _pool_geom(N, H, W, u.cout, 3, 1, 1))
+                else:
+                    gp = torch.empty(N, H, W, u.cout, dtype=gY.dtype, device=gY.device)
+                    lib.pool(gsl, gp, None, 1, 1, _pool_geom(N, H, W, u.cout, 3, 1, 1))
+                    deferred.append((u.bwd, gp))
                 continue
-            # conv chain: walk it backwards; gradient w.r.t. each ReLU output is premasked
+            # conv chain: walk it backwards; the gradient w.r.t. each ReLU output is premasked
             g = gsl
             for names, in_i in reversed(info):
                 units = [blk.units[n] for n in names]
-                inp = saved[in_i]
-                if in_i == 0:  # head conv(s) on the block input
+                if in_i == "merged":
+                    continue  # the head's own dgrad is part of the merged G_T GEMM below
+                inp = None if in_i == 0 else inp_of(in_i)
+                into = GT[..., in_i[1]:in_i[1] + in_i[2]] if isinstance(in_i, tuple) else None
+                if in_i == 0:  # unmerged head conv(s) on the block input
                     if len(units) == 2:
                         ua, ub = units
-                        deferred.append((ua, g[..., : ua.cout]))
-                        deferred.append((ub, g[..., ua.cout:]))
+                        deferred.append((ua.bwd, g[..., : ua.cout]))
+                        deferred.append((ub.bwd, g[..., ua.cout:]))
                     elif units[0].stride == 1:
-                        deferred.append((units[0], g))
+                        deferred.append((units[0].bwd, g))
                     else:
                         contribute_tensor(_dgrad_strided(units[0], g, None, (H, W)))
                     continue
-                if len(units) == 2:  # split on an intermediate: sum of two dgrads, masked by inp > 0
+                if len(units) == 2:  # split: sum of two dgrads, masked by inp > 0
                     ua, ub = units
-                    gi = conv2d(g[..., : ua.cout], ua.bwd, stride=1, pad=ua.bwd_pad, relu=False, use_bias=False,
-                                emask=inp)
-                    conv2d(g[..., ua.cout:], ub.bwd, stride=1, pad=ub.bwd_pad, relu=False, use_bias=False,
-                           emask=inp, out=gi, accumulate=True)
+                    gi = dgrad_into(ua, g[..., : ua.cout], inp, out=into)
+                    dgrad_into(ub, g[..., ua.cout:], inp, out=gi, accumulate=True)
                     g = gi
-                    continue
-                u = units[0]
-                if u.stride == 1:
-                    g = conv2d(g, u.bwd, stride=1, pad=u.bwd_pad, relu=False, use_bias=False, emask=inp)
                 else:
-                    g = torch.ops.aten.threshold_backward(
-                        _dgrad_strided(u, g, None, (inp.shape[1], inp.shape[2])), inp, 0)
-        for u, g in deferred:
-            contribute_conv(u, g, emask_x)
+                    g = dgrad_into(units[0], g, inp, out=into)
+        if GT is not None:
+            deferred.append((blk.merge[1], GT))
+        for cw, g in deferred:
+            contribute_conv(cw, g, emask_x)
         if emask_x is not None and not state["masked"]:
             gx = torch.ops.aten.threshold_backward(gx, emask_x, 0)
         return gx, None

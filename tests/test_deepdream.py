@@ -315,14 +315,17 @@ def test_gpu_fused_step_equals_unfused(native_lib):
             ref = DeepDream(net, s, use_graphs=False)
             ref.fused = False
             want = ref.run(x)
+            got = {}
             for graphs in (False, True):
                 dd = DeepDream(net, s, use_graphs=graphs)
                 assert dd.fused
-                got = dd.run(x)
-                if iters == 1:  # one step: equal up to the fp32 rounding of the update
-                    assert (got - want).abs().max() < 1e-4, (max_loss, graphs)
-                else:  # later steps see bf16 inputs that may round differently: compare the dream
-                    assert _cos(got - x, want - x) > 0.99 if max_loss is None else (got - want).abs().max() < 1e-4
+                got[graphs] = dd.run(x)
+                if iters == 1 or max_loss is not None:  # one step: equal up to the fp32 update rounding
+                    assert (got[graphs] - want).abs().max() < 1e-4, (max_loss, graphs)
+                else:  # later steps feed bf16-rounded inputs to a chaotic map: same dream direction
+                    assert _cos(got[graphs] - x, want - x) > 0.95, (max_loss, graphs)
+            # the captured graph replays exactly the eager fused steps
+            assert (got[True] - got[False]).abs().max() < 1e-3, (max_loss, iters)
 
 
 @pytest.mark.gpu

@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from deconv_api_amd import ops  # noqa: E402
 from deconv_api_amd.engine.deepdream import RESNET_LAYERS, DeepDream, DreamSettings  # noqa: E402
 from deconv_api_amd.ops import autograd as ag  # noqa: E402
+from deconv_api_amd.ops import inception as inc  # noqa: E402
 
 
 def main():
@@ -71,6 +72,11 @@ def main():
         return r
 
     ag.conv2d = timed
+    inc.conv2d = timed
+    for blk in getattr(net, "iblocks", []):  # merged head GEMMs
+        if blk.merge is not None:
+            names[id(blk.merge[0])] = (blk.name + ".heads", "fwd")
+            names[id(blk.merge[1])] = (blk.name + ".heads", "bwd")
     per_unit = defaultdict(lambda: [0.0, 0.0])
     grand_t = grand_f = grand_step = 0.0
     for hw in dd.octave_shapes(a.size, a.size):
