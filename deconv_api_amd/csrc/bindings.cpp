@@ -372,6 +372,32 @@ void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_
            "pool");
 }
 
+static int dt_of(const Tensor& t);
+
+// gx [N, H, W, C] <- E [N, OH, OW, C] at every s-th pixel, 0 elsewhere, [masked by emask > 0]
+void subpixel_scatter(Tensor E, c10::optional<Tensor> emask, Tensor gx, int64_t s) {
+  check_cuda(E, "E");
+  check_cuda(gx, "gx");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(E.device());
+  TORCH_CHECK(E.dim() == 4 && gx.dim() == 4 && E.is_contiguous() && gx.is_contiguous() && E.size(0) == gx.size(0) &&
+                  E.size(3) == gx.size(3) && E.size(3) % 8 == 0 && E.scalar_type() == gx.scalar_type() && s >= 1,
+              "subpixel_scatter: E [N,OH,OW,C], gx [N,H,W,C] contiguous, one dtype, C % 8");
+  TORCH_CHECK(E.size(1) == (gx.size(1) + s - 1) / s && E.size(2) == (gx.size(2) + s - 1) / s,
+              "subpixel_scatter: OH = ceil(H / s), OW = ceil(W / s)");
+  const uint16_t* mp = nullptr;
+  if (emask.has_value()) {
+    check_cuda(*emask, "emask");
+    TORCH_CHECK(emask->sizes() == gx.sizes() && emask->is_contiguous() && emask->scalar_type() == gx.scalar_type(),
+                "subpixel_scatter: emask like gx");
+    mp = reinterpret_cast<const uint16_t*>(emask->data_ptr());
+  }
+  check_rc(dv::subpixel_scatter_launch(reinterpret_cast<const uint16_t*>(E.data_ptr()), mp,
+                                       reinterpret_cast<uint16_t*>(gx.data_ptr()), (int)gx.size(0), (int)gx.size(1),
+                                       (int)gx.size(2), (int)gx.size(3), (int)E.size(1), (int)E.size(2), (int)s,
+                                       dt_of(gx), cur_stream()),
+           "subpixel_scatter");
+}
+
 static int dt_of(const Tensor& t) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "expected a bf16 or fp16 tensor");
   return t.scalar_type() == at::kHalf ? dv::DT_F16 : dv::DT_BF16;
@@ -762,6 +788,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "force the LDS-DMA conv tile config / split-K factor (0 = automatic); tuning only");
   m.def("pool", &pool, "k x k max/avg pooling forward/backward", py::arg("in"), py::arg("out"), py::arg("idx"),
         py::arg("kind"), py::arg("dir"), py::arg("geom"), py::arg("bias") = py::none(), py::arg("relu") = false);
+  m.def("subpixel_scatter", &subpixel_scatter, "input gradient of a stride-s 1x1 conv from its GEMM result");
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient");
   m.def("tile_gather", &tile_gather, "tiled DeepDream: rolled tile gather into the 16-bit network input");

@@ -138,6 +138,8 @@ __global__ void __launch_bounds__(256) dream_update_kernel(const uint16_t* __res
 constexpr int TPLAN = 7;
 // elements per unit in a pack (3 channels x tile, rounded to 16 B so the fp32 tail stays aligned)
 __host__ __device__ inline long long tile_ustride(int Th, int Tw) { return ((long long)Th * Tw * 3 + 7) & ~7LL; }
+// per-unit fp32 tail: {loss, sum |g| of pixel block 0 .. TP-1} (the pack kernel runs TP blocks per unit)
+constexpr int TP = 31, TAILF = TP + 1;
 
 // xin[k] (this rank's k-th unit, global unit u = rank + k * world) <- rolled-image tile, 8-channel 16-bit
 template <int DT>
@@ -168,14 +170,15 @@ __global__ void __launch_bounds__(256) tile_pack_kernel(const uint16_t* __restri
                                                         const int* __restrict__ plan, const float* __restrict__ lpart,
                                                         const float* __restrict__ lcoef, int L, int lparts, int units,
                                                         int ucap, int rank, int world, int Th, int Tw) {
-  const int k = blockIdx.x;
+  const int k = blockIdx.y;
   const int* pu = plan + (long long)(rank + k * world) * TPLAN;
   const int y0 = pu[3], y1 = pu[4], x0 = pu[5], x1 = pu[6];
   const int ow = x1 - x0, npix = (y1 - y0) * ow;
   const uint16_t* gk = g + (long long)k * Th * Tw * 8;
   uint16_t* dst = pack + (long long)k * tile_ustride(Th, Tw);
+  float* tail = reinterpret_cast<float*>(pack + (long long)ucap * tile_ustride(Th, Tw)) + (long long)TAILF * k;
   float asum = 0.f;
-  for (int p = threadIdx.x; p < npix; p += 256) {
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < npix; p += TP * 256) {
     const int ty = y0 + p / ow, tx = x0 + p % ow;
     const uint2 v = *reinterpret_cast<const uint2*>(gk + ((long long)ty * Tw + tx) * 8);
     const uint16_t c0 = (uint16_t)(v.x & 0xFFFFu), c1 = (uint16_t)(v.x >> 16), c2 = (uint16_t)(v.y & 0xFFFFu);
@@ -188,18 +191,15 @@ __global__ void __launch_bounds__(256) tile_pack_kernel(const uint16_t* __restri
   asum = wave_sum(asum);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = asum;
   __syncthreads();
-  if (threadIdx.x < 64) {
+  if (threadIdx.x == 0) tail[1 + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
     float ls = 0.f;
     for (int l = 0; l < L; ++l) {
       float t = 0.f;
       for (int p = threadIdx.x; p < lparts; p += 64) t += lpart[((long long)l * units + k) * lparts + p];
       ls += lcoef[l] * wave_sum(t);
     }
-    if (threadIdx.x == 0) {
-      float* tail = reinterpret_cast<float*>(pack + (long long)ucap * tile_ustride(Th, Tw)) + 2 * k;
-      tail[0] = ls;
-      tail[1] = (red[0] + red[1]) + (red[2] + red[3]);
-    }
+    if (threadIdx.x == 0) tail[0] = ls;
   }
 }
 
@@ -222,9 +222,9 @@ __global__ void __launch_bounds__(256) tile_update_kernel(const uint16_t* __rest
       if (plan[(long long)v * TPLAN] != b) continue;
       const float* tail = reinterpret_cast<const float*>(packs + (long long)(v % world) * pack_elems +
                                                          (long long)units_per_rank * tile_ustride(Th, Tw)) +
-                          2 * (v / world);
+                          (long long)TAILF * (v / world);
       ls += tail[0];
-      as += tail[1];
+      for (int q = 0; q < TP; ++q) as += tail[1 + q];
     }
     ls = wave_sum(ls);
     as = wave_sum(as);
@@ -253,7 +253,9 @@ __global__ void __launch_bounds__(256) tile_update_kernel(const uint16_t* __rest
   }
 }
 
-long long tile_pack_elems(int ucap, int Th, int Tw) { return (long long)ucap * (tile_ustride(Th, Tw) + 4); }
+long long tile_pack_elems(int ucap, int Th, int Tw) {
+  return (long long)ucap * (tile_ustride(Th, Tw) + 2 * TAILF + 4);  // + 2 halfs per fp32 tail entry
+}
 
 int tile_gather_launch(const float* x, uint16_t* xin, const int* plan, const int* shift, int units, int rank, int world,
                        int H, int W, int Th, int Tw, int dtype, hipStream_t s) {
@@ -269,12 +271,14 @@ int tile_gather_launch(const float* x, uint16_t* xin, const int* plan, const int
 int tile_pack_launch(const uint16_t* g, uint16_t* pack, const int* plan, const float* lpart, const float* lcoef, int L,
                      int lparts, int units, int ucap, int rank, int world, int Th, int Tw, int dtype, hipStream_t s) {
   if (units < 1 || units > ucap) return -1;
+  if (units > 65535) return -1;
+  const dim3 grid((unsigned)TP, (unsigned)units);
   if (dtype == DT_F16)
-    hipLaunchKernelGGL(tile_pack_kernel<DT_F16>, dim3((unsigned)units), dim3(256), 0, s, g, pack, plan, lpart, lcoef, L,
-                       lparts, units, ucap, rank, world, Th, Tw);
+    hipLaunchKernelGGL(tile_pack_kernel<DT_F16>, grid, dim3(256), 0, s, g, pack, plan, lpart, lcoef, L, lparts, units,
+                       ucap, rank, world, Th, Tw);
   else
-    hipLaunchKernelGGL(tile_pack_kernel<DT_BF16>, dim3((unsigned)units), dim3(256), 0, s, g, pack, plan, lpart, lcoef, L,
-                       lparts, units, ucap, rank, world, Th, Tw);
+    hipLaunchKernelGGL(tile_pack_kernel<DT_BF16>, grid, dim3(256), 0, s, g, pack, plan, lpart, lcoef, L, lparts, units,
+                       ucap, rank, world, Th, Tw);
   return (int)hipGetLastError();
 }
 

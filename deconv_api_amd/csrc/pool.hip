@@ -189,6 +189,43 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __rest
   }
 }
 
+// Input gradient of a stride-s 1x1 conv (pad 0) from its GEMM result E [N, OH, OW, C]:
+// gx[n, h, w] = E[n, h/s, w/s] where h, w are multiples of s, else 0; optionally zeroed where
+// emask[n, h, w] <= 0 (the ReLU of the layer that produced the conv's input). Writes all of gx:
+// replaces a zero fill, a strided copy per sub-pixel class, an add and a mask pass
+// (ops/autograd.py:_BottleneckFn, ResNet-50's stride-2 stage heads).
+template <int DT>
+__global__ void __launch_bounds__(256) subpixel_scatter_kernel(const uint16_t* __restrict__ E,
+                                                               const uint16_t* __restrict__ emask,
+                                                               uint16_t* __restrict__ gx, int N, int H, int W, int C,
+                                                               int OH, int OW, int s) {
+  const int cpp = C >> 3;
+  const long long total = (long long)N * H * W * cpp;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int ch = (int)(t % cpp);
+    const long long pix = t / cpp;
+    const int w = (int)(pix % W);
+    const int h = (int)((pix / W) % H);
+    const long long n = pix / ((long long)W * H);
+    uint4 o = {0u, 0u, 0u, 0u};
+    if (h % s == 0 && w % s == 0 && h / s < OH && w / s < OW) {
+      o = *reinterpret_cast<const uint4*>(E + ((n * OH + h / s) * OW + w / s) * C + ch * 8);
+      if (emask) {
+        const uint4 m = *reinterpret_cast<const uint4*>(emask + pix * C + ch * 8);
+        uint32_t ov[4] = {o.x, o.y, o.z, o.w};
+        const uint32_t mv[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = to_f<DT>(mv[e] & 0xFFFFu), hi = to_f<DT>(mv[e] >> 16);
+          ov[e] = (lo > 0.f ? (ov[e] & 0xFFFFu) : 0u) | (hi > 0.f ? (ov[e] & 0xFFFF0000u) : 0u);
+        }
+        o = uint4{ov[0], ov[1], ov[2], ov[3]};
+      }
+    }
+    *reinterpret_cast<uint4*>(gx + pix * C + ch * 8) = o;
+  }
+}
+
 static unsigned grid_for(long long total) {
   return (unsigned)std::min<long long>((total + 255) / 256, 256LL * 32);
 }
@@ -207,6 +244,17 @@ static int pool_dt(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t
     hipLaunchKernelGGL(avgpool_bwd_kernel<DT>, dim3(grid_for(in_total)), dim3(256), 0, st, in, out, g);
   else
     return -2;
+  return (int)hipGetLastError();
+}
+
+int subpixel_scatter_launch(const uint16_t* E, const uint16_t* emask, uint16_t* gx, int N, int H, int W, int C, int OH,
+                            int OW, int s, int dtype, hipStream_t st) {
+  if (C % 8 != 0 || s < 1) return -1;
+  const unsigned grid = grid_for((long long)N * H * W * (C / 8));
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(subpixel_scatter_kernel<DT_F16>, dim3(grid), dim3(256), 0, st, E, emask, gx, N, H, W, C, OH, OW, s);
+  else
+    hipLaunchKernelGGL(subpixel_scatter_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, E, emask, gx, N, H, W, C, OH, OW, s);
   return (int)hipGetLastError();
 }
 

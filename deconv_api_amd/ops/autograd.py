@@ -367,9 +367,20 @@ class _BottleneckFn(torch.autograd.Function):
         gm = gy if pm else torch.ops.aten.threshold_backward(gy, y, 0)
         g2 = conv2d(gm, c3.bwd, stride=1, pad=c3.bwd_pad, relu=False, use_bias=False, emask=y2 if pm else None)
         g1 = _dgrad(c2, g2, None if pm else y2, (y1.shape[1], y1.shape[2]), emask=y1 if pm else None)
-        gs = gm if sh is None else _dgrad(sh, gm, None, in_hw)
         emask = x if (pm and ctx.x_relu) else None
         a_mask = None if pm else y1
+        if c1.stride > 1 and sh is not None and _pw_strided(c1) and _pw_strided(sh) and sh.stride == c1.stride \
+                and x.is_contiguous():
+            # both stride-s 1x1 convs read x: their input gradients live on the same every-s-th
+            # pixels. E = g1 W1^T + gm Wsh^T (two accumulating GEMMs), then ONE kernel writes gx
+            # (E at the strided pixels, masked by x > 0, zeros elsewhere)
+            E = conv2d(g1, c1.bwd_sub[0][2], stride=1, pad=0, relu=False, mask=a_mask, use_bias=False)
+            conv2d(gm, sh.bwd_sub[0][2], stride=1, pad=0, relu=False, use_bias=False, out=E, accumulate=True)
+            gx = torch.empty_like(x)
+            native.lib().subpixel_scatter(E[..., : x.shape[3]].contiguous() if E.shape[3] != x.shape[3] else E,
+                                          emask, gx, c1.stride)
+            return gx, None
+        gs = gm if sh is None else _dgrad(sh, gm, None, in_hw)
         if c1.stride == 1:
             gx = conv2d(g1, c1.bwd, stride=1, pad=c1.bwd_pad, relu=False, mask=a_mask, use_bias=False, res=gs,
                         emask=emask)
@@ -378,6 +389,12 @@ class _BottleneckFn(torch.autograd.Function):
             if emask is not None:
                 gx = torch.ops.aten.threshold_backward(gx, emask, 0)
         return gx, None
+
+
+def _pw_strided(u: ConvUnit) -> bool:
+    """A 1x1 / pad-0 conv whose sub-pixel decomposition has exactly one non-empty class (0, 0)."""
+    return tuple(u.w.shape[2:]) == (1, 1) and tuple(u.pad) == (0, 0) and len(u.bwd_sub) == u.stride ** 2 and \
+        u.bwd_sub[0][:2] == (0, 0) and u.bwd_sub[0][2] is not None and all(cw is None for _, _, cw, _ in u.bwd_sub[1:])
 
 
 def bottleneck(x: torch.Tensor, c1: ConvUnit, c2: ConvUnit, c3: ConvUnit, short: Optional[ConvUnit]) -> torch.Tensor:
