@@ -749,30 +749,6 @@ void unpool2x2(Tensor p, Tensor code, Tensor out, int64_t code_div, bool relu) {
            "unpool2x2");
 }
 
-void sparse_unpool_conv(Tensor v, Tensor code, Tensor wt, Tensor out, int64_t code_div) {
-  check_cuda(v, "v");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(v.device());
-  TORCH_CHECK(v.dim() == 4 && v.scalar_type() == at::kBFloat16 && v.is_contiguous(), "sparse_unpool_conv: v NHWC bf16");
-  const int64_t NB = v.size(0), PH = v.size(1), PW = v.size(2), C = v.size(3);
-  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.size(0) == NB &&
-                  out.size(1) == 2 * PH && out.size(2) == 2 * PW,
-              "sparse_unpool_conv: out [NB, 2PH, 2PW, Ci] bf16");
-  const int64_t Ci = out.size(3);
-  TORCH_CHECK(C % 16 == 0 && Ci % 128 == 0, "sparse_unpool_conv: needs C % 16 == 0 and Ci % 128 == 0");
-  TORCH_CHECK(code_div >= 1 && NB % code_div == 0, "sparse_unpool_conv: code_div");
-  TORCH_CHECK(code.scalar_type() == at::kByte && code.is_contiguous() && code.numel() == v.numel() / code_div,
-              "sparse_unpool_conv: code");
-  TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.dim() == 4 && wt.size(0) == 4 &&
-                  wt.size(1) == C / 16 && wt.size(2) == Ci && wt.size(3) == 160,
-              "sparse_unpool_conv: wt [4, C/16, Ci, 160] bf16");
-  TORCH_CHECK(code.device() == v.device() && wt.device() == v.device() && out.device() == v.device(),
-              "sparse_unpool_conv: devices");
-  check_rc(dv::sparse_unpool_conv_launch(reinterpret_cast<const uint16_t*>(v.data_ptr()), code.data_ptr<uint8_t>(),
-                                         reinterpret_cast<const uint16_t*>(wt.data_ptr()),
-                                         reinterpret_cast<uint16_t*>(out.data_ptr()), (int)NB, (int)PH, (int)PW,
-                                         (int)C, (int)Ci, (int)code_div, cur_stream()),
-           "sparse_unpool_conv");
-}
 
 }  // namespace
 
@@ -810,6 +786,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("preprocess_u8", &preprocess_u8, "resized RGB u8 -> caffe-preprocessed bf16 network input");
   m.def("maxpool2x2", &maxpool2x2);
   m.def("unpool2x2", &unpool2x2);
-  m.def("sparse_unpool_conv", &sparse_unpool_conv, "2:4 sparse-MFMA conv-down on a max-unpooled input");
   m.attr("ARCH") = "gfx950";
 }

@@ -93,10 +93,6 @@ int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad
 // standalone 2x2/s2 max pool with switch codes, and its inverse (unpool scatter to full res)
 int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C,
                       hipStream_t s);
-// 2:4 sparse-MFMA conv-down on a max-unpooled input, computed from the pooled signal + switch code
-// (conv_sparse.hip); wt = per-phase packed weights [4][C/16][Ci][160] (ops/sparse_unpool.py)
-int sparse_unpool_conv_launch(const uint16_t* v, const uint8_t* code, const uint16_t* wt, uint16_t* out, int NB,
-                              int PH, int PW, int C, int Ci, int code_div, hipStream_t s);
 int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int N, int H, int W,
                      int C, int code_div, int relu, hipStream_t s);
 
