@@ -611,6 +611,32 @@ void topk_pos(Tensor v, Tensor idx, Tensor val, int64_t k) {
            "topk_pos");
 }
 
+// out4 [B, H, W, C] bf16 target activation, idx [B, K] int32 (< C), code u8 [B, H, W, C] or none,
+// S fp32 [B*K, H, W] (or [B*K, 2H, 2W] with code); mode 0 all, 1 max per image, 2 max over the batch
+void seed_map(Tensor out4, Tensor idx, c10::optional<Tensor> code, Tensor S, int64_t mode) {
+  check_cuda(out4, "out4");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(out4.device());
+  TORCH_CHECK(out4.dim() == 4 && out4.is_contiguous() && out4.scalar_type() == at::kBFloat16, "seed_map: out4 bf16 NHWC");
+  TORCH_CHECK(idx.dim() == 2 && idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.size(0) == out4.size(0),
+              "seed_map: idx int32 [B, K]");
+  const int64_t B = out4.size(0), H = out4.size(1), W = out4.size(2), C = out4.size(3), K = idx.size(1);
+  const int64_t up = code.has_value() ? 2 : 1;
+  TORCH_CHECK(S.scalar_type() == at::kFloat && S.is_contiguous() && S.numel() == B * K * H * W * up * up,
+              "seed_map: S fp32 [B*K, H, W] (x4 with code)");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "seed_map: mode");
+  const uint8_t* cp = nullptr;
+  if (code.has_value()) {
+    check_cuda(*code, "code");
+    TORCH_CHECK(code->sizes() == out4.sizes() && code->scalar_type() == at::kByte && code->is_contiguous(),
+                "seed_map: code u8 like out4");
+    cp = code->data_ptr<uint8_t>();
+  }
+  check_rc(dv::seed_map_launch(reinterpret_cast<const uint16_t*>(out4.data_ptr()), idx.data_ptr<int>(), cp,
+                               S.data_ptr<float>(), (int)(B * K), (int)K, (int)H, (int)W, (int)C, (int)mode,
+                               cur_stream()),
+           "seed_map");
+}
+
 void seed_deconv3x3(Tensor S, Tensor f, Tensor wt, Tensor out) {
   check_cuda(S, "S");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
@@ -779,6 +805,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);
   m.def("seed_deconv3x3", &seed_deconv3x3);
+  m.def("seed_map", &seed_map, "deconvnet seed maps (all / max, optional max-unpool for pool targets)");
   m.def("deprocess_mosaic", &deprocess_mosaic, py::arg("recon"), py::arg("out"), py::arg("tiles"), py::arg("reverse"),
         py::arg("stats") = py::none());
   m.def("resize_preprocess", &resize_preprocess);

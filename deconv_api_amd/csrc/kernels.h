@@ -93,6 +93,9 @@ int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad
 // standalone 2x2/s2 max pool with switch codes, and its inverse (unpool scatter to full res)
 int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C,
                       hipStream_t s);
+// seed maps of the deconvnet's B*K chains (all / max mode, optional max-unpool for pool targets)
+int seed_map_launch(const uint16_t* out4, const int* idx, const uint8_t* code, float* S, int BK, int K, int H, int W,
+                    int C, int mode, hipStream_t s);
 int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int N, int H, int W,
                      int C, int code_div, int relu, hipStream_t s);
 

@@ -165,6 +165,66 @@ int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint
   return (int)hipGetLastError();
 }
 
+// Seed maps of the B*K backward chains (reference app/deepdream.py:450-465): S[b*K+k] is channel
+// idx[b,k] of the target activation out4 [B, H, W, C] (16-bit), zero for idx < 0; mode 1 ('max')
+// keeps only the positions equal to the map's max (mode 2: the max over the batch, for global
+// top-k where all images share the filter); idx >= C reads as -1. With `code` (a max-pool target) the map is
+// max-unpooled to [2H, 2W] with that pool's switch codes and clamped at 0 (the seed of the conv
+// below the pool). One workgroup per chain: the 'max' reduction stays in the block.
+__global__ void __launch_bounds__(256) seed_map_kernel(const uint16_t* __restrict__ out4, const int* __restrict__ idx,
+                                                       const uint8_t* __restrict__ code, float* __restrict__ S, int K,
+                                                       int H, int W, int C, int mode) {
+  const int bk = blockIdx.x, b = bk / K;
+  const int f = idx[bk] < C ? idx[bk] : -1;
+  const int HW = H * W;
+  const uint16_t* ob = out4 + (long long)b * HW * C;
+  __shared__ float red[4];
+  float m = -INFINITY;
+  if (mode != 0 && f >= 0) {
+    // mode 2 ('max' with batch-global top-k: every image shares filter f) reduces over the batch
+    const int b0 = mode == 2 ? 0 : b, b1 = mode == 2 ? (int)gridDim.x / K : b + 1;
+    for (int bb = b0; bb < b1; ++bb) {
+      const uint16_t* o2 = out4 + (long long)bb * HW * C;
+      for (int p = threadIdx.x; p < HW; p += 256) m = fmaxf(m, bf2f(o2[(long long)p * C + f]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  }
+  if (code == nullptr) {
+    float* Sb = S + (long long)bk * HW;
+    for (int p = threadIdx.x; p < HW; p += 256) {
+      float v = f >= 0 ? bf2f(ob[(long long)p * C + f]) : 0.f;
+      if (mode != 0 && v != m) v = 0.f;
+      Sb[p] = v;
+    }
+    return;
+  }
+  const int W2 = 2 * W;
+  float* Sb = S + (long long)bk * 4 * HW;
+  const uint8_t* cb = code + (long long)b * HW * C;
+  for (int q = threadIdx.x; q < 4 * HW; q += 256) {
+    const int y = q / W2, x = q - y * W2;
+    const long long p = (long long)(y >> 1) * W + (x >> 1);
+    float v = 0.f;
+    if (f >= 0 && cb[p * C + f] == (uint8_t)(((y & 1) << 1) | (x & 1))) {
+      v = bf2f(ob[p * C + f]);
+      if (mode != 0 && v != m) v = 0.f;
+      v = fmaxf(v, 0.f);
+    }
+    Sb[q] = v;
+  }
+}
+
+int seed_map_launch(const uint16_t* out4, const int* idx, const uint8_t* code, float* S, int BK, int K, int H, int W,
+                    int C, int mode, hipStream_t s) {
+  if (BK <= 0 || K <= 0 || BK % K) return -1;
+  hipLaunchKernelGGL(seed_map_kernel, dim3((unsigned)BK), dim3(256), 0, s, out4, idx, code, S, K, H, W, C, mode);
+  return (int)hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 // Mosaic + deprocess (reference: app/main.py:67-72 + app/deepdream.py:483-498):
 // the `tiles` reconstructions of one image form a 2x2 mosaic that is normalized as a whole:

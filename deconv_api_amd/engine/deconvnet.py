@@ -131,21 +131,11 @@ class DeconvNet:
         return ops.topk_positive(sums, k)
 
     # ------------------------------------------------------------------ backward
-    def _seed_map(self, out4: torch.Tensor, idx: torch.Tensor, mode: str, batch_topk: str) -> torch.Tensor:
-        """One-channel seed maps S [B*K, H, W] fp32 from the target output (app/deepdream.py:450-465)."""
-        B, H, W, C = out4.shape
-        K = idx.shape[1]
-        fi = idx.long().clamp_min(0)  # [B, K]
-        o = out4.float().permute(0, 3, 1, 2)  # [B, C, H, W]
-        S = torch.gather(o, 1, fi.view(B, K, 1, 1).expand(B, K, H, W))  # [B, K, H, W]
-        if mode == "max":
-            if batch_topk == "global":
-                m = S.amax(dim=(0, 2, 3), keepdim=True)
-            else:
-                m = S.amax(dim=(2, 3), keepdim=True)
-            S = S * (S == m)
-        S = S * (idx >= 0).view(B, K, 1, 1)
-        return S.reshape(B * K, H, W).contiguous()
+    def _seed_map(self, out4: torch.Tensor, idx: torch.Tensor, mode: str, batch_topk: str,
+                  code: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One-channel seed maps S [B*K, H, W] fp32 from the target output (app/deepdream.py:450-465);
+        unpooled to [B*K, 2H, 2W] with ``code`` for pool targets (ops.seed_map: one HIP kernel)."""
+        return ops.seed_map(out4, idx, mode, batch_topk, code)
 
     def backward(self, st: ForwardState, idx: torch.Tensor, mode: str = "all",
                  batch_topk: str = "per_image", layer: Optional[str] = None,
@@ -170,14 +160,9 @@ class DeconvNet:
             d = ops.seed_deconv3x3(S, f, self.rt.convs[layer].seed_wt)
             j = li - 1
         elif spec.kind == "pool":
-            # seed at pooled resolution, unpooled with this pool's switches, then the conv below
-            S = self._seed_map(out, idx, mode, batch_topk)  # [BK, PH, PW]
-            code = st.codes[layer]  # [B, PH, PW, C]
-            fi = idx.long().clamp_min(0)
-            cf = torch.gather(code.permute(0, 3, 1, 2), 1,
-                              fi.view(B, K, 1, 1).expand(B, K, *code.shape[1:3]))  # [B, K, PH, PW]
-            cf = cf.reshape(B * K, *code.shape[1:3])
-            Su = ops.unpool_ref(S.unsqueeze(-1), cf.unsqueeze(-1)).squeeze(-1).clamp_min(0).contiguous()
+            # seed at pooled resolution, max-unpooled with this pool's switches (one kernel), then
+            # the conv below
+            Su = self._seed_map(out, idx, mode, batch_topk, code=st.codes[layer])  # [BK, 2PH, 2PW]
             conv_name = self.specs[li - 1].name
             d = ops.seed_deconv3x3(Su, f, self.rt.convs[conv_name].seed_wt)
             j = li - 2

@@ -3,13 +3,13 @@ reference implementations of the same math (used for CPU execution and as test o
 from .conv import (ConvWeights, conv2d, deconv_weights, maxpool_switch_ref, oc_pad, pad_channels_oihw,
                    unpool_ref)
 from .misc import (CAFFE_MEAN, channel_sum, softmax_rows, deprocess_mosaic, maxpool2x2, preprocess_ref, resize_mode,
-                   resize_preprocess, resize_u8_ref, seed_deconv3x3, topk_positive, unpool2x2)
+                   resize_preprocess, resize_u8_ref, seed_deconv3x3, seed_map, topk_positive, unpool2x2)
 from . import native
 
 __all__ = [
     "ConvWeights", "conv2d", "deconv_weights", "maxpool_switch_ref", "oc_pad", "pad_channels_oihw",
     "unpool_ref", "CAFFE_MEAN", "channel_sum", "deprocess_mosaic", "maxpool2x2", "preprocess_ref",
-    "resize_mode", "resize_preprocess", "resize_u8_ref", "seed_deconv3x3", "topk_positive", "unpool2x2",
+    "resize_mode", "resize_preprocess", "resize_u8_ref", "seed_deconv3x3", "seed_map", "topk_positive", "unpool2x2",
     "softmax_rows",
     "native",
 ]

@@ -63,6 +63,37 @@ def topk_positive(v: torch.Tensor, k: int):
     return idx, val
 
 
+def seed_map(out4: torch.Tensor, idx: torch.Tensor, mode: str = "all", batch_topk: str = "per_image",
+             code: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Seed maps of the deconvnet's B*K backward chains (reference app/deepdream.py:450-465).
+
+    out4 [B, H, W, C] target activation, idx [B, K] filter indices (-1: none). Returns fp32
+    [B*K, H, W]: channel idx[b, k] of image b, in 'max' mode only where it equals the map's max (the
+    max over the whole batch with batch_topk='global', where every image shares the filter). With
+    ``code`` (u8 [B, H, W, C] max-pool switches of a pool target) the map is max-unpooled to
+    [B*K, 2H, 2W] and clamped at 0. GPU: one HIP kernel (``seed_map_kernel``, one workgroup per
+    chain) instead of permute/gather/amax/mask/unpool passes."""
+    B, H, W, C = out4.shape
+    K = idx.shape[1]
+    m = {"all": 0, "max": 2 if batch_topk == "global" else 1}[mode]
+    if out4.is_cuda and out4.dtype == torch.bfloat16:
+        up = 1 if code is None else 2
+        S = torch.empty(B * K, H * up, W * up, device=out4.device, dtype=torch.float32)
+        native.lib().seed_map(out4.contiguous(), idx.to(torch.int32).contiguous(),
+                              None if code is None else code.contiguous(), S, m)
+        return S
+    fi = idx.long().clamp_min(0)
+    o = out4.float().permute(0, 3, 1, 2)  # [B, C, H, W]
+    S = torch.gather(o, 1, fi.view(B, K, 1, 1).expand(B, K, H, W))  # [B, K, H, W]
+    if m:
+        S = S * (S == S.amax(dim=(0, 2, 3) if m == 2 else (2, 3), keepdim=True))
+    S = (S * (idx >= 0).view(B, K, 1, 1)).reshape(B * K, H, W)
+    if code is None:
+        return S.contiguous()
+    cf = torch.gather(code.permute(0, 3, 1, 2), 1, fi.view(B, K, 1, 1).expand(B, K, H, W)).reshape(B * K, H, W)
+    return unpool_ref(S.unsqueeze(-1), cf.unsqueeze(-1)).squeeze(-1).clamp_min(0).contiguous()
+
+
 def seed_deconv3x3(S: torch.Tensor, f: torch.Tensor, wt: torch.Tensor) -> torch.Tensor:
     """First deconv step from a one-channel map.
 

@@ -449,6 +449,26 @@ def test_seed_deconv(native_lib):
     assert got[3].abs().sum() == 0
 
 
+@pytest.mark.parametrize("pool", [False, True])
+@pytest.mark.parametrize("mode,batch_topk", [("all", "per_image"), ("max", "per_image"), ("max", "global"),
+                                             ("all", "global")])
+def test_seed_map(native_lib, pool, mode, batch_topk):
+    """HIP seed-map kernel vs the fp32 torch gather/amax/mask(/unpool) reference (exact)."""
+    g = torch.Generator().manual_seed(11)
+    B, H, W, C, K = 3, 7, 9, 64, 4
+    out4 = torch.relu(torch.randint(-2, 5, (B, H, W, C), generator=g).float()).to(torch.bfloat16)  # ties
+    if batch_topk == "global":
+        idx = torch.tensor([[5, 63, 0, -1]], dtype=torch.int32).expand(B, K).contiguous()
+    else:
+        idx = torch.randint(0, C, (B, K), generator=g, dtype=torch.int32)
+        idx[1, 2] = -1
+    code = torch.randint(0, 4, (B, H, W, C), generator=g, dtype=torch.uint8) if pool else None
+    ref = ops.seed_map(out4, idx, mode, batch_topk, code)
+    got = ops.seed_map(out4.to(DEV), idx.to(DEV), mode, batch_topk, None if code is None else code.to(DEV))
+    assert got.shape == ref.shape == (B * K, H * (2 if pool else 1), W * (2 if pool else 1))
+    assert torch.equal(got.cpu(), ref)
+
+
 def test_deprocess_mosaic(native_lib):
     g = torch.Generator().manual_seed(10)
     r = torch.relu(torch.randn(8, 224, 224, 3, generator=g)) * 3
