@@ -47,6 +47,10 @@ class Config:
     host: str = "0.0.0.0"
     port: int = 80                        # Dockerfile:10,15
     hip_graphs: bool = True
+    inception_weights: str = ""          # /deepdream InceptionV3: folded .safetensors or Keras .h5 (empty = random)
+    resnet_weights: str = ""             # /deepdream ResNet-50: same
+    dream_max_batch: int = 8              # /deepdream: same-shape requests run as one DeepDream batch
+    dream_window_ms: float = 20.0         # /deepdream: how long the worker waits to fill a batch
     log_json: bool = True
 
     @classmethod

@@ -1,12 +1,20 @@
 """Service behind the ``POST /deepdream`` extension route (not in the reference): decode ->
 DeepDream (InceptionV3 or ResNet-50) on the GPU worker -> JPEG data URL (same conventions as
-``POST /``)."""
+``POST /``).
+
+Requests are batched: a request joins the pending list after decode + size validation; the GPU
+worker takes the oldest request and every pending one with the same (model, octaves, steps,
+H, W) key (waiting up to ``dream_window_ms`` for more, at most ``dream_max_batch``) and runs them
+as ONE DeepDream batch. Every image's loss, gradient normalisation and max-loss flag are per
+image (engine/deepdream.py), so batching is exact; the batch is padded to a power of two by
+repeating the last image so the per-(B, H, W) hipGraph cache sees few distinct batch sizes."""
 from __future__ import annotations
 
 import asyncio
-import concurrent.futures as cf
 import threading
-from typing import Dict, Optional
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -14,8 +22,35 @@ import torch
 from ..codec import encode_data_url, read_data_url
 from ..config import Config
 from ..engine.deepdream import RESNET_LAYERS, DeepDream, DreamSettings
+from ..utils import metrics as M
 
 MAX_SIDE = 1024
+MODELS = ("inception_v3", "resnet50")
+
+
+@dataclass
+class _Req:
+    img: torch.Tensor  # u8 [H, W, 3], already resized to <= MAX_SIDE
+    key: Tuple[Any, ...]  # (model, octaves, steps, H, W)
+    fut: asyncio.Future
+    loop: asyncio.AbstractEventLoop
+    t0: float = field(default_factory=time.perf_counter)
+
+
+def _bucket(n: int, cap: int) -> int:
+    b = 1
+    while b < n:
+        b *= 2
+    return max(n, min(b, cap))
+
+
+def _resolve(fut: asyncio.Future, value=None, exc: Optional[BaseException] = None) -> None:
+    if fut.done():
+        return
+    if exc is not None:
+        fut.set_exception(exc)
+    else:
+        fut.set_result(value)
 
 
 class DreamService:
@@ -24,46 +59,132 @@ class DreamService:
         self.device = torch.device(self.cfg.resolve_device())
         self._engines: Dict[str, DeepDream] = {}
         self._lock = threading.Lock()
-        self._gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="dv-dream")
+        self._cv = threading.Condition()
+        self._pending: List[_Req] = []
+        self._stop = False
+        self._worker: Optional[threading.Thread] = None
+        self.max_batch = max(1, self.cfg.dream_max_batch)
+        self.window_s = max(0.0, self.cfg.dream_window_ms) / 1e3
+        self.batches: List[int] = []  # real (unpadded) size of every batch run, for tests/metrics
 
-    def engine(self, model: str, octaves: int, steps: int) -> DeepDream:
-        if model not in ("inception_v3", "resnet50"):
+    # ------------------------------------------------------------------ engines
+    @staticmethod
+    def validate(model: str, octaves: int, steps: int) -> None:
+        if model not in MODELS:
             raise ValueError("model must be inception_v3 or resnet50")
         if not (1 <= octaves <= 6 and 1 <= steps <= 100):
             raise ValueError("octaves must be 1..6 and steps 1..100")
+
+    def engine(self, model: str, octaves: int, steps: int) -> DeepDream:
+        self.validate(model, octaves, steps)
         with self._lock:
             if model not in self._engines:
-                if model == "inception_v3":
-                    from ..models.inception_v3 import InceptionV3
+                from ..models.dream_import import load_weights, new_model
 
-                    net = InceptionV3(self.cfg.seed).build(self.device)
-                    self._engines[model] = DeepDream(net, DreamSettings(), use_graphs=self.cfg.hip_graphs)
-                else:
-                    from ..models.resnet50 import ResNet50
-
-                    net = ResNet50(self.cfg.seed).build(self.device)
-                    self._engines[model] = DeepDream(net, DreamSettings(layers=dict(RESNET_LAYERS)),
-                                                     use_graphs=self.cfg.hip_graphs)
+                net = new_model(model, self.cfg.seed)
+                path = self.cfg.inception_weights if model == "inception_v3" else self.cfg.resnet_weights
+                if path:
+                    load_weights(net, path)
+                net.build(self.device)
+                s = DreamSettings() if model == "inception_v3" else DreamSettings(layers=dict(RESNET_LAYERS))
+                self._engines[model] = DeepDream(net, s, use_graphs=self.cfg.hip_graphs)
             e = self._engines[model]
         e.s.octaves, e.s.iterations = octaves, steps
         return e
 
-    def _run(self, img: np.ndarray, model: str, octaves: int, steps: int) -> np.ndarray:
-        e = self.engine(model, octaves, steps)
+    # ------------------------------------------------------------------ request prep (codec pool)
+    def prepare(self, img: np.ndarray, octaves: int) -> torch.Tensor:
+        """Decoded RGB -> u8 [H, W, 3] at most MAX_SIDE per side; rejects images whose smallest
+        octave would be under 75 px (the InceptionV3 minimum)."""
         h, w = img.shape[:2]
         scale = min(1.0, MAX_SIDE / max(h, w))
-        t = torch.from_numpy(img).unsqueeze(0)
+        t = torch.from_numpy(np.ascontiguousarray(img))
         if scale < 1.0:
             from ..engine.deepdream import resize
 
-            t = resize(t.float(), (int(h * scale), int(w * scale))).round().clamp(0, 255).to(torch.uint8)
-        small = min(t.shape[1:3]) / (e.s.octave_scale ** (octaves - 1))
+            t = resize(t.unsqueeze(0).float(), (int(h * scale), int(w * scale)))[0]
+            t = t.round().clamp(0, 255).to(torch.uint8)
+        small = min(t.shape[:2]) / (DreamSettings().octave_scale ** (octaves - 1))
         if small < 75:
             raise ValueError(f"image too small for {octaves} octaves (smallest octave side {small:.0f} < 75)")
-        return e.dream_u8(t)[0].cpu().numpy()
+        return t.contiguous()
 
+    # ------------------------------------------------------------------ batching worker
+    def _ensure_worker(self) -> None:
+        with self._cv:
+            if self._worker is None or not self._worker.is_alive():
+                self._stop = False
+                self._worker = threading.Thread(target=self._loop, name="dv-dream", daemon=True)
+                self._worker.start()
+
+    def _take(self) -> Optional[List[_Req]]:
+        """Oldest pending request plus every same-key one (after up to ``window_s`` of waiting)."""
+        with self._cv:
+            while not self._pending and not self._stop:
+                self._cv.wait()
+            if not self._pending:
+                return None
+            key = self._pending[0].key
+            deadline = time.monotonic() + self.window_s
+            while True:
+                n = sum(1 for r in self._pending if r.key == key)
+                left = deadline - time.monotonic()
+                if n >= self.max_batch or left <= 0 or self._stop:
+                    break
+                self._cv.wait(left)
+            batch = [r for r in self._pending if r.key == key][: self.max_batch]
+            taken = {id(r) for r in batch}
+            self._pending = [r for r in self._pending if id(r) not in taken]
+            M.QUEUE_DEPTH.set(len(self._pending), route="/deepdream")
+            return batch
+
+    def run_batch(self, imgs: List[torch.Tensor], model: str, octaves: int, steps: int) -> np.ndarray:
+        """u8 [H, W, 3] images of one shape -> dreamed u8 [n, H, W, 3] (one engine batch)."""
+        e = self.engine(model, octaves, steps)
+        n = len(imgs)
+        pad = _bucket(n, self.max_batch) - n
+        x = torch.stack(imgs + [imgs[-1]] * pad)
+        t0 = time.perf_counter()
+        out = e.dream_u8(x)[:n].cpu().numpy()
+        M.ENGINE_TIME.observe(time.perf_counter() - t0, stage="deepdream")
+        M.BATCH_SIZE.observe(n, route="/deepdream")
+        M.IMAGES.inc(n, route="/deepdream")
+        return out
+
+    def _loop(self) -> None:
+        while True:
+            batch = self._take()
+            if batch is None:
+                return
+            model, octaves, steps = batch[0].key[:3]
+            self.batches.append(len(batch))
+            try:
+                out = self.run_batch([r.img for r in batch], model, octaves, steps)
+            except Exception as exc:  # noqa: BLE001 - delivered to every request of the batch
+                for r in batch:
+                    r.loop.call_soon_threadsafe(_resolve, r.fut, None, exc)
+                continue
+            for r, o in zip(batch, out):
+                r.loop.call_soon_threadsafe(_resolve, r.fut, o)
+
+    def close(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        if self._worker is not None:
+            self._worker.join(timeout=30)
+
+    # ------------------------------------------------------------------ request entry
     async def dream(self, uri: str, model: str = "inception_v3", octaves: int = 4, steps: int = 20) -> str:
+        self.validate(model, octaves, steps)
         loop = asyncio.get_running_loop()
         img = await loop.run_in_executor(None, read_data_url, uri)
-        out = await loop.run_in_executor(self._gpu, self._run, img, model, octaves, steps)
+        t = await loop.run_in_executor(None, self.prepare, img, octaves)
+        fut = loop.create_future()
+        self._ensure_worker()
+        with self._cv:
+            self._pending.append(_Req(t, (model, octaves, steps, t.shape[0], t.shape[1]), fut, loop))
+            M.QUEUE_DEPTH.set(len(self._pending), route="/deepdream")
+            self._cv.notify_all()
+        out = await fut
         return await loop.run_in_executor(None, encode_data_url, out, self.cfg.jpeg_quality)

@@ -243,3 +243,40 @@ def test_decoded_pixel_cap(client, monkeypatch):
     url = make_data_url(np.zeros((40, 40, 3), np.uint8), "PNG")
     r = client.post("/", data={"file": url, "layer": "block1_conv1"})
     assert r.status_code == 400 and "too large" in r.json()["detail"], r.text
+
+
+def test_deepdream_requests_are_batched():
+    """Concurrent same-shape /deepdream requests run as ONE engine batch (padded to a power of two);
+    a different shape runs in its own batch; batched outputs match single-image runs."""
+    import asyncio
+
+    from deconv_api_amd.codec import encode_data_url, read_data_url
+    from deconv_api_amd.config import Config
+    from deconv_api_amd.serve.dream_service import DreamService
+
+    ds = DreamService(Config.from_env(device="cpu", dream_max_batch=4, dream_window_ms=300.0, hip_graphs=False))
+    rng = np.random.default_rng(0)
+    from urllib.parse import unquote
+
+    shapes = [(80, 80, 3)] * 3 + [(96, 88, 3)]
+    urls = [unquote(encode_data_url(rng.integers(0, 256, s, dtype=np.uint8), 95)) for s in shapes]
+
+    async def go():
+        return await asyncio.gather(*[ds.dream(u, "inception_v3", 1, 1) for u in urls])
+
+    try:
+        outs = asyncio.run(go())
+        assert sorted(ds.batches) == [1, 3]
+        for u, o in zip(urls, outs):
+            assert o.startswith("data:image/")  # the reference labels JPEG bytes as webp
+        # exactness of batching: the engine output of an image inside a batch == alone
+        imgs = [ds.prepare(read_data_url(u), 1) for u in urls[:3]]
+        both = ds.run_batch(imgs, "inception_v3", 1, 1)
+        alone = ds.run_batch(imgs[1:2], "inception_v3", 1, 1)
+        assert both.shape == (3, 80, 80, 3)
+        d = np.abs(both[1].astype(int) - alone[0].astype(int))
+        assert d.max() <= 2 and d.mean() < 0.05
+        with pytest.raises(ValueError):
+            ds.prepare(np.zeros((40, 40, 3), np.uint8), 4)
+    finally:
+        ds.close()
