@@ -83,6 +83,7 @@ def main(argv=None):
             "higher_is_better": True, "scaling": "strong" if a.tile else "weak", "dtype": a.dtype,
             "data": "synthetic uint8 images, seeded random-init weights", "hip_graphs": not a.no_graphs,
             "finite": bool(torch.isfinite(out).all()),
+            "sub_batch_streams": dd.split if dd.fused else 1,
             "config": {"model": a.model, "batch": a.batch, "image_size": a.size, "tile": a.tile,
                        "parallelism": f"{'tiles' if a.tile else 'dp'}{info.world}"},
         }), flush=True)

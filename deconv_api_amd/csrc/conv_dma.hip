@@ -44,6 +44,22 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// vmcnt wait leaving `pend` (<= P) younger K tiles of LO (HI: this wave issues one more B row
+// group) DMAs each in flight; deep rings (STAGES > 4) keep more tiles in flight for the
+// latency-bound small GEMMs
+template <int P, int LO, int HI>
+__device__ __forceinline__ void wait_pend(int pend, bool hi) {
+  if constexpr (P <= 0) {
+    wait_vm<0>();
+  } else {
+    if (pend >= P) {
+      if (hi) wait_vm<P * HI>(); else wait_vm<P * LO>();
+    } else {
+      wait_pend<P - 1, LO, HI>(pend, hi);
+    }
+  }
+}
+
 // swizzle term of LDS row `row` for a BK-wide tile
 template <int BK>
 __device__ __forceinline__ int row_xor(int row) {
@@ -91,7 +107,7 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
   constexpr int B_GROUPS = BN / RPI;        // RPI-row groups of the B tile
   constexpr int B_FULL = B_GROUPS / NW, B_REM = B_GROUPS % NW;
   static_assert(A_I >= 1 && BM % (RPI * NW) == 0, "BM must cover every wave");
-  static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+  static_assert(STAGES >= 2 && STAGES <= 8, "stages");
   __shared__ __attribute__((aligned(16))) uint8_t smem[STAGES * STAGE];
 
   const int tid = threadIdx.x;
@@ -252,14 +268,8 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
   // wait until this wave's DMAs of the current tile landed, leaving `pend` younger tiles in flight
   auto wait_tiles = [&](int pend) {
     constexpr int PT_LO = A_I * (MASK ? 2 : 1) + B_FULL, PT_HI = PT_LO + 1;
-    const bool hi = B_REM && wave < B_REM;
-    if (pend <= 0) {
-      wait_vm<0>();
-    } else if (pend == 1) {
-      if (hi) wait_vm<PT_HI>(); else wait_vm<PT_LO>();
-    } else {
-      if (hi) wait_vm<2 * PT_HI>(); else wait_vm<2 * PT_LO>();
-    }
+    static_assert((STAGES - 2) * PT_HI <= 63, "vmcnt holds at most 63 outstanding DMAs");
+    wait_pend<STAGES - 2, PT_LO, PT_HI>(pend, B_REM && wave < B_REM);
   };
 
   f32x4 acc[FM][FN];
@@ -912,6 +922,11 @@ static int dma_forced(const ConvArgs& a, hipStream_t s, int cfg) {
     case 9: return okn(128) ? dma_cfg<DT, 2, 2, 4, 4, 64, 2, AMODE, EPI>(a, s) : -5;               // 128x128, 4 waves
     case 10: return okn(128) ? dma_cfg<DT, 2, 2, 2, 4, 64, 3, AMODE, EPI>(a, s) : -5;              // 64x128, 4 waves
     case 11: return okn(64) ? dma_cfg<DT, 4, 1, 4, 4, 64, 2, AMODE, EPI>(a, s) : -5;               // 256x64, 4 waves
+    // deep rings for latency-bound small GEMMs (more K tiles in flight per workgroup)
+    case 12: return okn(64) ? dma_cfg<DT, 2, 2, 2, 2, 64, 6, AMODE, EPI>(a, s) : -5;               // 64x64 w4 ST6
+    case 13: return okn(64) ? dma_cfg<DT, 2, 2, 2, 2, 64, 8, AMODE, EPI>(a, s) : -5;               // 64x64 w4 ST8
+    case 14: return okn(64) ? dma_cfg<DT, 4, 1, 2, 4, 64, 6, AMODE, EPI>(a, s) : -5;               // 128x64 w4 ST6
+    case 15: return okn(128) ? dma_cfg<DT, 2, 2, 2, 4, 64, 6, AMODE, EPI>(a, s) : -5;              // 64x128 w4 ST6
     default: return -5;
   }
 }

@@ -178,14 +178,32 @@ __global__ void __launch_bounds__(256) tile_pack_kernel(const uint16_t* __restri
   uint16_t* dst = pack + (long long)k * tile_ustride(Th, Tw);
   float* tail = reinterpret_cast<float*>(pack + (long long)ucap * tile_ustride(Th, Tw)) + (long long)TAILF * k;
   float asum = 0.f;
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < npix; p += TP * 256) {
-    const int ty = y0 + p / ow, tx = x0 + p % ow;
-    const uint2 v = *reinterpret_cast<const uint2*>(gk + ((long long)ty * Tw + tx) * 8);
-    const uint16_t c0 = (uint16_t)(v.x & 0xFFFFu), c1 = (uint16_t)(v.x >> 16), c2 = (uint16_t)(v.y & 0xFFFFu);
-    dst[p * 3 + 0] = c0;
-    dst[p * 3 + 1] = c1;
-    dst[p * 3 + 2] = c2;
-    asum += fabsf(to_f<DT>(c0)) + fabsf(to_f<DT>(c1)) + fabsf(to_f<DT>(c2));
+  // TP blocks per unit (fixed by the tail layout): PU independent loads per thread in flight per
+  // round, else one unit's ~1M owned pixels serialize on load latency (287 us at 1024^2,
+  // profiles/kstats_c5_r2_tiled_fused.txt)
+  constexpr int PU = 8;
+  constexpr int STRIDE = TP * 256;
+  for (int base = blockIdx.x * 256 + threadIdx.x; base < npix; base += STRIDE * PU) {
+    uint2 v[PU];
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int p = base + u * STRIDE;
+      if (p < npix) {
+        const int ty = y0 + p / ow, tx = x0 + p % ow;
+        v[u] = *reinterpret_cast<const uint2*>(gk + ((long long)ty * Tw + tx) * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int p = base + u * STRIDE;
+      if (p < npix) {
+        const uint16_t c0 = (uint16_t)(v[u].x & 0xFFFFu), c1 = (uint16_t)(v[u].x >> 16), c2 = (uint16_t)(v[u].y & 0xFFFFu);
+        dst[p * 3 + 0] = c0;
+        dst[p * 3 + 1] = c1;
+        dst[p * 3 + 2] = c2;
+        asum += fabsf(to_f<DT>(c0)) + fabsf(to_f<DT>(c1)) + fabsf(to_f<DT>(c2));
+      }
+    }
   }
   __shared__ float red[4];
   asum = wave_sum(asum);
@@ -260,7 +278,7 @@ long long tile_pack_elems(int ucap, int Th, int Tw) {
 int tile_gather_launch(const float* x, uint16_t* xin, const int* plan, const int* shift, int units, int rank, int world,
                        int H, int W, int Th, int Tw, int dtype, hipStream_t s) {
   if (units < 1 || units > 65535) return -1;
-  const dim3 grid((unsigned)std::min((Th * Tw + 255) / 256, 128), (unsigned)units);
+  const dim3 grid((unsigned)std::min((Th * Tw + 255) / 256, 512), (unsigned)units);
   if (dtype == DT_F16)
     hipLaunchKernelGGL(tile_gather_kernel<DT_F16>, grid, dim3(256), 0, s, x, xin, plan, shift, rank, world, H, W, Th, Tw);
   else
@@ -286,7 +304,7 @@ int tile_update_launch(const uint16_t* packs, long long pack_elems, int units_pe
                        const int* shift, float* x, uint8_t* done, float* loss, float step, float max_loss, int world,
                        int H, int W, int Th, int Tw, int dtype, hipStream_t s) {
   if (nunits < 1 || nunits > 65535) return -1;
-  const dim3 grid((unsigned)std::min((Th * Tw + 255) / 256, 64), (unsigned)nunits);
+  const dim3 grid((unsigned)std::min((Th * Tw + 255) / 256, 512), (unsigned)nunits);
   hipLaunchKernelGGL(tile_update_kernel, grid, dim3(256), 0, s, packs, pack_elems, units_per_rank, plan, nunits, shift, x,
                      done, loss, step, max_loss, world, H, W, Th, Tw, dtype);
   return (int)hipGetLastError();

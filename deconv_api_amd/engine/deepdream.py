@@ -35,6 +35,16 @@ from ..ops.autograd import premasked_grads, sumsq_core
 # HIP kernels (A/B); DV_DREAM_GRAPHS: hipGraph cache entries (octave shapes) kept, LRU-evicted
 FUSED_STEP = os.environ.get("DV_DREAM_FUSED", "1") != "0"
 GRAPH_CACHE = int(os.environ.get("DV_DREAM_GRAPHS", "8"))
+# DV_DREAM_OCTAVE_GRAPH=0: one graph per step, replayed `iterations` times (A/B). Default: the
+# whole octave (every step) is ONE captured graph - each separate replay costs a ~140 us launch
+# gap on the GPU (profiles/kstats_c3_r2_fused_step.txt: 166 gaps after dream_update_kernel).
+OCTAVE_GRAPH = os.environ.get("DV_DREAM_OCTAVE_GRAPH", "1") != "0"
+# DV_DREAM_SPLIT=n: a batch runs as n independent sub-batches, each on its own HIP stream with its
+# own graphs, so the latency-bound small-octave launches of one sub-batch overlap the other's
+# (images are independent: per-image loss, normalisation and max-loss flag). Measured config 3
+# (B=64, 299^2): 1 -> 327, 2 -> 356, 4 -> 232 img/s (4 side streams + the default stream exceed the
+# 4 hardware queues per process).
+SPLIT = int(os.environ.get("DV_DREAM_SPLIT", "2"))
 LOSS_PARTS = 32
 
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
@@ -79,6 +89,9 @@ class DeepDream:
         self.fused = FUSED_STEP and self.device.type == "cuda"
         self._graphs: "OrderedDict[tuple, object]" = OrderedDict()
         self.graph_cache = GRAPH_CACHE
+        self.split = SPLIT
+        self._slot = 0  # sub-batch index: each concurrent sub-batch owns its graphs/buffers
+        self._streams: List[torch.cuda.Stream] = []
 
     # ------------------------------------------------------------------ one step
     def _net_input(self, x: torch.Tensor) -> torch.Tensor:
@@ -154,7 +167,8 @@ class DeepDream:
                          float(self.s.step), ml)
 
     def _fused_state(self, B: int, hw: Tuple[int, int]):
-        key = (B, tuple(hw))
+        steps = self.s.iterations if OCTAVE_GRAPH else 1
+        key = (B, tuple(hw), steps, self._slot)
         if key in self._graphs:
             self._graphs.move_to_end(key)
             return self._graphs[key]
@@ -168,13 +182,16 @@ class DeepDream:
             torch.cuda.current_stream(self.device).wait_stream(s)
             st.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(st.graph):
-                self._fused_step(st)
+                for _ in range(steps):
+                    self._fused_step(st)
+        st.steps = steps
         self._cache_put(key, st)
         return st
 
     def _cache_put(self, key, val):
         self._graphs[key] = val
-        while len(self._graphs) > max(1, self.graph_cache):  # bounded: request shapes vary
+        # bounded: request shapes vary (each concurrent sub-batch holds its own graph per shape)
+        while len(self._graphs) > max(1, self.graph_cache) * max(1, self.split):
             self._graphs.popitem(last=False)
             torch.cuda.empty_cache()
 
@@ -207,11 +224,12 @@ class DeepDream:
                 st.xin.zero_()
                 st.xin[..., :3].copy_(x)
             st.done.zero_()
-            for _ in range(self.s.iterations):
-                if st.graph is not None:
-                    st.graph.replay()
-                else:
+            if st.graph is None:
+                for _ in range(self.s.iterations):
                     self._fused_step(st)
+            else:
+                for _ in range(self.s.iterations // st.steps):
+                    st.graph.replay()
             return st.x.clone()
         if self.use_graphs:
             g, gx, gdone, gloss = self._graph(B, (H, W))
@@ -235,6 +253,27 @@ class DeepDream:
 
     def run(self, x: torch.Tensor) -> torch.Tensor:
         """x: preprocessed fp32 [B, H, W, 3] on the engine device -> dreamed fp32 image."""
+        n = self.split if (self.fused and x.is_cuda) else 1
+        if n <= 1 or x.shape[0] % n or x.shape[0] < n:
+            return self._run_one(x)
+        cur = torch.cuda.current_stream(self.device)
+        while len(self._streams) < n:
+            self._streams.append(torch.cuda.Stream(self.device))
+        outs = []
+        try:
+            for i, xc in enumerate(x.chunk(n)):
+                st = self._streams[i]
+                st.wait_stream(cur)
+                with torch.cuda.stream(st):
+                    self._slot = i
+                    outs.append(self._run_one(xc))
+        finally:
+            self._slot = 0
+        for st in self._streams[:n]:
+            cur.wait_stream(st)
+        return torch.cat(outs)
+
+    def _run_one(self, x: torch.Tensor) -> torch.Tensor:
         shapes = self.octave_shapes(x.shape[1], x.shape[2])
         original = x
         shrunk = resize(original, shapes[0])

@@ -329,6 +329,26 @@ def test_gpu_fused_step_equals_unfused(native_lib):
 
 
 @pytest.mark.gpu
+def test_gpu_split_batch_streams(native_lib):
+    """A batch run as 2 concurrent sub-batches (own streams, own graphs) == the whole batch."""
+    net = InceptionV3(0).build("cuda")
+    x = (torch.rand(4, 150, 150, 3, generator=torch.Generator().manual_seed(9)) * 2 - 1).cuda()
+    for iters in (1, 3):
+        s = DreamSettings(iterations=iters, octaves=2)
+        one = DeepDream(net, s, use_graphs=True)
+        two = DeepDream(net, s, use_graphs=True)
+        two.split = 2
+        want, got = one.run(x), two.run(x)
+        assert {k[-1] for k in two._graphs} == {0, 1}  # one graph set per sub-batch
+        if iters == 1:
+            assert (got - want).abs().max() < 1e-3
+        else:
+            assert _cos(got - x, want - x) > 0.95
+        again = two.run(x)  # replays of both sub-batches' cached graphs
+        assert (again - got).abs().max() < 1e-3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("max_loss", [None, 1e-9])
 def test_gpu_tiled_fused_equals_torch(native_lib, max_loss):
     """Fused tiled step (HIP rolled gather, owned-pixel packs with loss/|g| tails, pack-driven

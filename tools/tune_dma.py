@@ -23,7 +23,8 @@ from deconv_api_amd.engine.deepdream import RESNET_LAYERS, DeepDream, DreamSetti
 from deconv_api_amd.ops import autograd as ag  # noqa: E402
 
 CFG_NAMES = {0: "auto", 1: "256x256", 2: "128x256", 3: "128x128", 4: "256x128", 5: "256x64", 6: "512x64",
-             7: "128x64w4", 8: "64x64w4", 9: "128x128w4", 10: "64x128w4", 11: "256x64w4"}
+             7: "128x64w4", 8: "64x64w4", 9: "128x128w4", 10: "64x128w4", 11: "256x64w4",
+             12: "64x64w4s6", 13: "64x64w4s8", 14: "128x64w4s6", 15: "64x128w4s6"}
 
 
 def main():
@@ -34,7 +35,7 @@ def main():
     ap.add_argument("--octaves", type=int, default=4)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--cfgs", default="0,1,2,3,4,5,6,7,8,9,10,11")
+    ap.add_argument("--cfgs", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15")
     ap.add_argument("--ks", default="0,1,2,4,8")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
