@@ -1,0 +1,1060 @@
+// LDS-DMA implicit-GEMM convolution for gfx950 (MI355X): the high-throughput path for plain
+// (non-unpool) conv forward and transposed-conv dgrad.
+//
+// Differences from conv_igemm.hip (the register-staged kernel that also handles the
+// unpool-gather and ReLU-mask prologues):
+//   * operands are staged global -> LDS by `buffer_load_dwordx4 ... lds` (LDS-DMA): no VGPR
+//     round trip and no ds_write issue cost. Conv zero padding, the M tail and the K tail come
+//     for free from the buffer descriptor's range check (an out-of-range offset returns 0);
+//   * 8 waves per workgroup, each owning a (16*FM) x (16*FN) C tile (up to 128 x 64, i.e.
+//     256 x 256 per workgroup), so each ds_read_b128 fragment feeds FN (or FM) MFMAs;
+//   * the LDS image is lane-linear per DMA instruction (1 KiB = 1024/(2*BK) rows); the XOR
+//     swizzle is applied to the per-lane SOURCE chunk and to the fragment read address, never
+//     to the DMA destination (cdna_hip_programming.md rule 21). BK=64 rows (128 B): chunk ^
+//     (row & 7). BK=32 rows (64 B): chunk ^ ((4 - ((row >> 2) & 3)) & 3), which puts the 16
+//     rows x 4 chunks of every ds_read_b128 lane group of a 16x16x32 fragment read on distinct
+//     16-B bank slots (derivation in docs/KERNELS.md);
+//   * STAGES-deep LDS ring, one barrier per K tile: the DMA for tile t+STAGES-1 is issued right
+//     after the barrier of tile t and a counted `s_waitcnt vmcnt(N)` leaves the younger tiles in
+//     flight across the barrier (raw s_barrier, never __syncthreads, so nothing drains them).
+// LDS-DMA implicit-GEMM conv: kernel templates, tile configs and per-problem tile choice.
+// Shared by the instantiation units conv_dma_<dtype>_<mode>.hip (one dma_bn<DT, AMODE, EPI>
+// each, compiled in parallel) and conv_dma.hip (dispatch, split-K, masked dgrads, tuning state).
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace dv {
+
+namespace {
+
+constexpr uint32_t kOOB = 0x80000000u;  // any offset >= num_records reads as zero
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, uint8_t* lds_dst, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds_dst, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
+  const uint32_t nrec = bytes > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nrec, 0x00020000);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// vmcnt wait leaving `pend` (<= P) younger K tiles of LO (HI: this wave issues one more B row
+// group) DMAs each in flight; deep rings (STAGES > 4) keep more tiles in flight for the
+// latency-bound small GEMMs
+template <int P, int LO, int HI>
+__device__ __forceinline__ void wait_pend(int pend, bool hi) {
+  if constexpr (P <= 0) {
+    wait_vm<0>();
+  } else {
+    if (pend >= P) {
+      if (hi) wait_vm<P * HI>(); else wait_vm<P * LO>();
+    } else {
+      wait_pend<P - 1, LO, HI>(pend, hi);
+    }
+  }
+}
+
+// swizzle term of LDS row `row` for a BK-wide tile
+template <int BK>
+__device__ __forceinline__ int row_xor(int row) {
+  if constexpr (BK == 64)
+    return row & 7;
+  else
+    return (4 - ((row >> 2) & 3)) & 3;
+}
+
+}  // namespace
+
+template <int DT, int FM, int FN, int EPI, bool accum>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane);
+template <int DT, int FM, int FN>
+__device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw,
+                                             int lane);
+template <int DT, int NT, int BM, int BN, int FM, int FN>
+__device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
+                                             int n0, int wm, int wn, int lane, int tid, bool writer = true);
+
+// DT: 16-bit storage/MFMA dtype of x, w and a 16-bit output (DT_BF16 / DT_F16, common.h)
+// MASK: backward through a ReLU: A elements are kept only where mask (same layout and pixel
+// stride as x) is > 0. The mask tile is DMA'd into LDS next to the A tile with the same offsets
+// and applied to each A fragment in registers right before its MFMAs.
+// KS2: in-workgroup K split. Two groups of WM x WN waves share the C tile; group g computes the
+// 32-deep sub-step g of every BK=64 tile, and group 1's partial sums are added into group 0's
+// through LDS before the epilogue. Each wave then owns a (16*FM) x (16*FN) = 128 x 64 tile where
+// a plain 8-wave layout would own 64 x 64: 12 instead of 16 fragment reads per 32 MFMAs, for the
+// 128- and 64-output-channel layers whose 256 x 128 / 512 x 64 tiles are LDS-read bound.
+template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED,
+          bool MASK = false, bool FRAGPIPE = false, bool KS2 = false>
+__global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(const ConvArgs a, int tiles_n) {
+  constexpr int NW = WM * WN * (KS2 ? 2 : 1);
+  static_assert(!KS2 || (BK == 64 && !MASK), "KS2: BK=64 (one 32-deep sub-step per group), no mask");
+  constexpr int BM = WM * FM * 16;
+  constexpr int BN = WN * FN * 16;
+  constexpr int ROWB = BK * 2;              // LDS bytes per row
+  constexpr int CPR = BK / 8;               // 16-B chunks per row
+  constexpr int RPI = 1024 / ROWB;          // rows per DMA instruction
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int B_BYTES = BN * ROWB;
+  constexpr int M_BYTES = MASK ? A_BYTES : 0;
+  constexpr int STAGE = A_BYTES + M_BYTES + B_BYTES;
+  constexpr int A_I = BM / RPI / NW;        // A DMA instructions per wave per K tile
+  constexpr int B_GROUPS = BN / RPI;        // RPI-row groups of the B tile
+  constexpr int B_FULL = B_GROUPS / NW, B_REM = B_GROUPS % NW;
+  static_assert(A_I >= 1 && BM % (RPI * NW) == 0, "BM must cover every wave");
+  static_assert(STAGES >= 2 && STAGES <= 8, "stages");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = KS2 ? wave / (WM * WN) : 0;  // K group (KS2)
+  const int wl = KS2 ? wave - kg * (WM * WN) : wave;
+  const int wm = wl / WN, wn = wl % WN;
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = wgid % tiles_n;
+  const int tile_m = wgid / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int H = a.H, W = a.W, C = a.C;
+
+  // ---- tile base image: every A source offset is relative to it (32-bit voffsets) ----
+  int n_base;
+  {
+    const int g = m0 < a.M ? m0 : a.M - 1;
+    int pix = g;
+    if constexpr (EPI == CONV_E_POOL) pix = g >> 2;
+    const int per_img = (EPI == CONV_E_POOL) ? (a.OH >> 1) * (a.OW >> 1) : a.OH * a.OW;
+    n_base = pix / per_img;
+  }
+  const long long img_elems = (long long)H * W * a.x_ld;
+  const uint16_t* xb = a.x + (long long)n_base * img_elems;
+  const long long x_total = (long long)a.N * img_elems;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(xb, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
+  __amdgpu_buffer_rsrc_t mr = xr;
+  if constexpr (MASK)
+    mr = make_rsrc(a.mask + (long long)n_base * img_elems, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
+
+  // lane -> (row within its DMA row group, logical 16-B chunk at LDS position lane % CPR)
+  const int lrow = lane / CPR;
+  const int lchunk = (lane % CPR) ^ row_xor<BK>(lrow);  // group bases are multiples of 16 rows
+
+  // ---- per-row A gather state (rows fixed for the whole K loop) ----
+  int r_off[A_I], r_h[A_I], r_w[A_I];
+#pragma unroll
+  for (int j = 0; j < A_I; ++j) {
+    const int row = (j * NW + wave) * RPI + lrow;
+    const int gm = m0 + row;
+    int n, oh, ow;
+    const int g = gm < a.M ? gm : 0;
+    if constexpr (EPI == CONV_E_POOL) {
+      const int PWo = a.OW >> 1, PHo = a.OH >> 1;
+      const int sub = g & 3;
+      int pix = g >> 2;
+      const int pw = pix % PWo;
+      pix /= PWo;
+      const int ph = pix % PHo;
+      n = pix / PHo;
+      oh = 2 * ph + (sub >> 1);
+      ow = 2 * pw + (sub & 1);
+    } else {
+      ow = g % a.OW;
+      const int t = g / a.OW;
+      oh = t % a.OH;
+      n = t / a.OH;
+    }
+    if constexpr (AMODE == CONV_A_TRANSPOSE) {
+      r_h[j] = oh + a.pad_h;
+      r_w[j] = ow + a.pad_w;
+    } else {
+      r_h[j] = oh * a.stride - a.pad_h;
+      r_w[j] = ow * a.stride - a.pad_w;
+    }
+    r_off[j] = (n - n_base) * H * W;  // pixel index of the image's first pixel, relative to base
+    if (gm >= a.M) r_h[j] = -(1 << 28);  // never in bounds
+  }
+  // Fast path (forward convs with <= 32 taps): per row, a tap-validity bitmask and the element
+  // offset of tap (0,0); per K tile the gather is then mask-test + add (the uniform tap delta).
+  // measured: neutral on K>=2304 layers, and its per-row prologue costs 20-40% on K=576 layers
+  // (profiles/layers_r1_fastmask.txt), so it is compiled out
+  constexpr bool FAST = false;
+  const bool fast = FAST && a.KH * a.KW <= 32;
+  uint32_t r_mask[A_I];
+  int r_base[A_I];
+#pragma unroll
+  for (int j = 0; j < A_I; ++j) {
+    uint32_t m = 0;
+    if (fast) {
+      for (int kh = 0; kh < a.KH; ++kh) {
+        const bool okh = (unsigned)(r_h[j] + kh) < (unsigned)H;
+        for (int kw = 0; kw < a.KW; ++kw)
+          if (okh && (unsigned)(r_w[j] + kw) < (unsigned)W) m |= 1u << (kh * a.KW + kw);
+      }
+    }
+    r_mask[j] = m;
+    r_base[j] = m ? (int)(((long long)r_off[j] + (long long)r_h[j] * W + r_w[j]) * a.x_ld) : 0;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    uint8_t* As = smem + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES + M_BYTES;
+    int kh, kw, ch, tap;
+    bool kval;
+    if constexpr (CALIGNED) {
+      const int k0 = kt * BK;
+      tap = k0 / C;  // wave-uniform
+      kh = tap / a.KW;
+      kw = tap - kh * a.KW;
+      ch = k0 - tap * C + lchunk * 8;
+      kval = tap < a.KH * a.KW;
+    } else {
+      const int k = kt * BK + lchunk * 8;
+      tap = k / C;
+      kh = tap / a.KW;
+      kw = tap - kh * a.KW;
+      ch = k - tap * C;
+      kval = k < a.K;
+    }
+    if (FAST && fast) {
+      const int delta = (kh * W + kw) * (int)a.x_ld + ch;
+      const uint32_t tbit = kval ? (1u << tap) : 0u;
+#pragma unroll
+      for (int j = 0; j < A_I; ++j) {
+        const uint32_t voff = (r_mask[j] & tbit) ? (uint32_t)(r_base[j] + delta) * 2u : kOOB;
+        dma16(xr, As + (j * NW + wave) * 1024, voff);
+      }
+    } else {
+#pragma unroll
+    for (int j = 0; j < A_I; ++j) {
+      int ih, iw;
+      bool ok;
+      if constexpr (AMODE == CONV_A_TRANSPOSE) {
+        const int th = r_h[j] - kh, tw = r_w[j] - kw;
+        const int s = a.stride;
+        ih = th / s;
+        iw = tw / s;
+        ok = th >= 0 && tw >= 0 && ih * s == th && iw * s == tw && ih < H && iw < W;
+      } else {
+        ih = r_h[j] + kh;
+        iw = r_w[j] + kw;
+        ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      }
+      ok = ok && kval;
+      ok = ok && DV_BOUNDS((long long)n_base * img_elems + ((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch, 8,
+                           a.x_elems, "conv_dma A gather");
+      const uint32_t voff =
+          ok ? (uint32_t)((((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch) * 2) : kOOB;
+      dma16(xr, As + (j * NW + wave) * 1024, voff);
+      if constexpr (MASK) dma16(mr, As + A_BYTES + (j * NW + wave) * 1024, voff);
+    }
+    }
+#pragma unroll
+    for (int j = 0; j < B_FULL + (B_REM ? 1 : 0); ++j) {
+      const int grp = j * NW + wave;
+      if (grp < B_GROUPS) {
+        const int row = grp * RPI + lrow;
+        const uint32_t voff = (uint32_t)((((long long)(n0 + row)) * a.Kpad + kt * BK + lchunk * 8) * 2);
+        if (DV_BOUNDS((long long)voff / 2, 8, (long long)a.OCpad * a.Kpad, "conv_dma B weights"))
+          dma16(wr, Bs + grp * 1024, voff);
+      }
+    }
+  };
+
+  // wait until this wave's DMAs of the current tile landed, leaving `pend` younger tiles in flight
+  auto wait_tiles = [&](int pend) {
+    constexpr int PT_LO = A_I * (MASK ? 2 : 1) + B_FULL, PT_HI = PT_LO + 1;
+    static_assert((STAGES - 2) * PT_HI <= 63, "vmcnt holds at most 63 outstanding DMAs");
+    wait_pend<STAGES - 2, PT_LO, PT_HI>(pend, B_REM && wave < B_REM);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets: row = 16-aligned base + (lane & 15)
+  const int a_row0 = wm * FM * 16 + (lane & 15);
+  const int b_row0 = wn * FN * 16 + (lane & 15);
+  const int rx = row_xor<BK>(lane & 15);
+  int sw[BK / 32];
+#pragma unroll
+  for (int s = 0; s < BK / 32; ++s) sw[s] = (((s * 4 + (lane >> 4)) ^ rx) << 4);
+
+  // split-K (gridDim.y > 1): this workgroup reduces K tiles [k0, k0 + nk) into a partial sum
+  const int nk_all = a.Kpad / BK;
+  const int k0 = (int)(((long long)nk_all * blockIdx.y) / gridDim.y);
+  const int nk = (int)(((long long)nk_all * (blockIdx.y + 1)) / gridDim.y) - k0;
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nk) issue(k0 + p, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt % STAGES;
+    const int pend = min(STAGES - 2, nk - 1 - kt);
+    wait_tiles(pend);
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < nk) issue(k0 + kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const uint8_t* As = smem + cur * STAGE;
+    const uint8_t* Bs = As + A_BYTES + M_BYTES;
+    if constexpr (KS2) {
+      typedef typename Vec8<DT>::type v8;
+      const int swk = ((kg * 4 + (lane >> 4)) ^ rx) << 4;
+      v8 af[FM], bf[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const v8*>(Bs + (b_row0 + j * 16) * ROWB + swk);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + swk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bf[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      continue;
+    }
+    if constexpr (FRAGPIPE && !MASK) {
+      // all fragments of a 32-K sub-step are read up front, and the next sub-step's reads are
+      // issued before this sub-step's MFMAs (register double buffer), so LDS latency hides
+      // behind FM*FN MFMAs instead of being exposed per A fragment
+      typedef typename Vec8<DT>::type v8;
+      v8 af[2][FM], bf[2][FN];
+      auto ld = [&](int s, int b) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[b][j] = *reinterpret_cast<const v8*>(Bs + (b_row0 + j * 16) * ROWB + sw[s]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[b][i] = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + sw[s]);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int s = 0; s < BK / 32; ++s) {
+        if (s + 1 < BK / 32) ld(s + 1, (s + 1) & 1);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[s & 1][i], bf[s & 1][j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      continue;
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      typedef typename Vec8<DT>::type v8;
+      v8 bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const v8*>(Bs + (b_row0 + j * 16) * ROWB + sw[s]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        v8 af = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + sw[s]);
+        if constexpr (MASK) {
+          uint4 av = __builtin_bit_cast(uint4, af);
+          const uint4 mv = *reinterpret_cast<const uint4*>(As + A_BYTES + (a_row0 + i * 16) * ROWB + sw[s]);
+          av.x = mask_pos_pk(av.x, mv.x);
+          av.y = mask_pos_pk(av.y, mv.y);
+          av.z = mask_pos_pk(av.z, mv.z);
+          av.w = mask_pos_pk(av.w, mv.w);
+          af = __builtin_bit_cast(v8, av);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af, bfr[j], acc[i][j]);
+      }
+    }
+  }
+
+  if constexpr (KS2) {  // group 1's partial sums -> group 0 (lane-linear 16-B slots, conflict-free)
+    static_assert(WM * WN * FM * FN * 64 * 16 <= STAGES * STAGE, "KS2 reduction must fit in the stages");
+    f32x4* red = reinterpret_cast<f32x4*>(smem) + (wl * FM * FN) * 64 + lane;
+    __syncthreads();  // every wave is done reading the operand stages
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) red[(i * FN + j) * 64] = acc[i][j];
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += red[(i * FN + j) * 64];
+    }
+    __syncthreads();  // the epilogue may reuse the stages
+  }
+
+  // ---- epilogue ----
+  if (a.ws != nullptr) {  // split-K partial: raw fp32 sums to ws[split][row][OCpad]
+    if (kg != 0) return;
+    float* ws = a.ws + (long long)blockIdx.y * a.M * a.OCpad;
+    const int row_l = (lane >> 4) * 4, col_l = lane & 15;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wn * FN * 16 + j * 16 + col_l;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * FM * 16 + i * 16 + row_l + r;
+          if (row < a.M) ws[(long long)row * a.OCpad + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  if constexpr (EPI == CONV_E_BF16) {
+    if (a.vec_epi) {
+      static_assert(BM * BN * 2 <= STAGES * STAGE, "C tile must fit in the operand stages");
+      if constexpr (!KS2) __syncthreads();  // every wave is done reading the operand stages
+      epilogue_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid, kg == 0);
+      return;
+    }
+  }
+  if (kg != 0) return;
+  if constexpr (EPI == CONV_E_BF16) {
+    if (a.res || a.emask) {
+      epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+      return;
+    }
+  }
+  if (a.accumulate)
+    epilogue<DT, FM, FN, EPI, true>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+  else
+    epilogue<DT, FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+}
+
+// residual epilogue (ResNet block tail): out = [ReLU](acc + bias + res), then optionally zeroed
+// where emask <= 0 (backward: the input gradient of a block whose input is a ReLU output, with the
+// shortcut gradient as `res`). Each column group's residual/emask values are all loaded before its
+// first store, so the loads overlap each other instead of each waiting behind the previous store.
+template <int DT, int FM, int FN>
+__device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw,
+                                             int lane) {
+  const int row_l = (lane >> 4) * 4;
+  const int col_l = lane & 15;
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = nw + j * 16 + col_l;
+    if (col >= a.OC) continue;
+    const float bias = a.bias ? a.bias[col] : 0.f;
+    uint16_t rv[FM][4], ev[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = min(mw + i * 16 + row_l + r, a.M - 1);
+        rv[i][r] = a.res ? a.res[(long long)row * a.res_ld + col] : (uint16_t)0u;
+        ev[i][r] = a.emask ? a.emask[(long long)row * a.emask_ld + col] : (uint16_t)0x3C00u;  // any > 0
+      }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mw + i * 16 + row_l + r;
+        if (row >= a.M) continue;
+        float v = acc[i][j][r] + bias;
+        if (relu_at(a, col) && !a.res) v = fmaxf(v, 0.f);  // same order as epilogue_lds
+        v += to_f<DT>(rv[i][r]);
+        if (a.accumulate) v += to_f<DT>(out[(long long)row * a.out_ld + col]);
+        if (relu_at(a, col) && a.res) v = fmaxf(v, 0.f);
+        const uint32_t e = ev[i][r];
+        if (e == 0u || (e & 0x8000u)) v = 0.f;
+        if (DV_BOUNDS((long long)row * a.out_ld + col, 1, a.out_elems, "conv_dma epilogue_res out"))
+          out[(long long)row * a.out_ld + col] = from_f<DT>(v);
+      }
+  }
+}
+
+template <int DT, int FM, int FN, int EPI, bool accum>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane) {
+  const int row_l = (lane >> 4) * 4;
+  const int col_l = lane & 15;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = nw + j * 16 + col_l;
+    if (col >= a.OC) continue;
+    const float bias = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int rowb = mw + i * 16 + row_l;
+      if (rowb >= a.M) continue;
+      if constexpr (EPI == CONV_E_POOL) {
+        float best = -INFINITY;
+        int code = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bias;
+          if (a.relu) v = fmaxf(v, 0.f);
+          v = to_f<DT>(from_f<DT>(v));
+          if (v > best) {
+            best = v;
+            code = r;
+          }
+        }
+        const long long prow = rowb >> 2;
+        if (!DV_BOUNDS(prow * a.out_ld + col, 1, a.out_elems, "conv_dma pool epilogue out")) continue;
+        reinterpret_cast<uint16_t*>(a.out)[prow * a.out_ld + col] = from_f<DT>(best);
+        a.out_code[prow * a.OC + col] = (uint8_t)code;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rowb + r;
+          if (row >= a.M) continue;
+          float v = acc[i][j][r] + bias;
+          if (relu_at(a, col)) v = fmaxf(v, 0.f);
+          const long long o = (long long)row * a.out_ld + col;
+          if (!DV_BOUNDS(o, 1, a.out_elems, "conv_dma epilogue out")) continue;
+          if constexpr (EPI == CONV_E_F32) {
+            float* out = reinterpret_cast<float*>(a.out);
+            if (accum) v += out[o];
+            out[o] = v;
+          } else {
+            uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+            if (accum) v += to_f<DT>(out[o]);
+            out[o] = from_f<DT>(v);
+          }
+        }
+      }
+    }
+  }
+}
+
+// LDS-staged 16-bit epilogue. The MFMA C layout gives each lane 4 rows x 1 column per 16x16
+// block, i.e. 2-byte scattered stores; instead the tile is written to LDS (the freed operand
+// stages, 16-B chunks XOR-swizzled by row) and read back as 8-channel chunks: every global
+// store, residual load, emask load and accumulate load is one 16-B access. Semantics as
+// epilogue/epilogue_res: v = acc + bias, [ReLU] (before a += out), + res, [ReLU] (after a res
+// add), zeroed where emask <= 0. Stores of a row's last partial chunk (OC % 8) go per element.
+template <int DT, int NT, int BM, int BN, int FM, int FN>
+__device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
+                                             int n0, int wm, int wn, int lane, int tid, bool writer) {
+  constexpr int CPR = BN / 8;                       // 16-B chunks per C-tile row
+  constexpr int SWZ = (CPR < 8 ? CPR : 8) - 1;
+  const int row_l = (lane >> 4) * 4, col_l = lane & 15;
+  const bool pre_relu = a.relu && a.res == nullptr;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    if (!writer) break;
+    const int col = wn * FN * 16 + j * 16 + col_l;
+    const int gcol = n0 + col;
+    const float bias = (a.bias && gcol < a.OCpad) ? a.bias[gcol] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * FM * 16 + i * 16 + row_l + r;
+        float v = acc[i][j][r] + bias;
+        if (pre_relu && relu_at(a, gcol)) v = fmaxf(v, 0.f);
+        *reinterpret_cast<uint16_t*>(smem + row * (BN * 2) + ((((col >> 3) ^ (row & SWZ))) << 4) + (col & 7) * 2) =
+            from_f<DT>(v);
+      }
+  }
+  __syncthreads();
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+  const bool post = a.accumulate || a.res != nullptr;
+  for (int c = tid; c < BM * CPR; c += NT) {
+    const int row = c / CPR, cc = c % CPR;
+    const int grow = m0 + row, gcol = n0 + cc * 8;
+    if (grow >= a.M || gcol >= a.OC) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((cc ^ (row & SWZ)) << 4));
+    const long long o = (long long)grow * a.out_ld + gcol;
+    if (!a.ucode && !DV_BOUNDS(o, gcol + 8 > a.OC ? a.OC - gcol : 8, a.out_elems, "conv_dma epilogue_lds out")) continue;
+    if (a.res && !DV_BOUNDS((long long)grow * a.res_ld + gcol, gcol + 8 > a.OC ? a.OC - gcol : 8, a.res_elems,
+                            "conv_dma epilogue_lds res"))
+      continue;
+    if (a.emask && !DV_BOUNDS((long long)grow * a.emask_ld + gcol, gcol + 8 > a.OC ? a.OC - gcol : 8, a.emask_elems,
+                              "conv_dma epilogue_lds emask"))
+      continue;
+    if (gcol + 8 > a.OC) {  // a row's last partial chunk: element-wise (no 16-B access past OC)
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      for (int e = 0; e < a.OC - gcol; ++e) {
+        float f = to_f<DT>((vv[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+        if (a.accumulate) f += to_f<DT>(out[o + e]);
+        if (a.res) {
+          f += to_f<DT>(a.res[(long long)grow * a.res_ld + gcol + e]);
+          if (relu_at(a, gcol + e)) f = fmaxf(f, 0.f);
+        }
+        if (a.emask) {
+          const uint32_t m = a.emask[(long long)grow * a.emask_ld + gcol + e];
+          if (m == 0u || (m & 0x8000u)) f = 0.f;
+        }
+        out[o + e] = from_f<DT>(f);
+      }
+      continue;
+    }
+    if (post) {
+      uint4 ad = {0u, 0u, 0u, 0u}, rs = {0u, 0u, 0u, 0u};
+      if (a.accumulate) ad = *reinterpret_cast<const uint4*>(out + o);
+      if (a.res) rs = *reinterpret_cast<const uint4*>(a.res + (long long)grow * a.res_ld + gcol);
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w}, aa[4] = {ad.x, ad.y, ad.z, ad.w}, rr[4] = {rs.x, rs.y, rs.z, rs.w};
+      uint32_t ov[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = to_f<DT>(vv[e] & 0xFFFFu) + to_f<DT>(aa[e] & 0xFFFFu) + to_f<DT>(rr[e] & 0xFFFFu);
+        float hi = to_f<DT>(vv[e] >> 16) + to_f<DT>(aa[e] >> 16) + to_f<DT>(rr[e] >> 16);
+        if (a.relu && a.res) {
+          lo = fmaxf(lo, 0.f);
+          hi = fmaxf(hi, 0.f);
+        }
+        ov[e] = pack2<DT>(lo, hi);
+      }
+      v = uint4{ov[0], ov[1], ov[2], ov[3]};
+    }
+    if (a.emask) {
+      const uint4 em = *reinterpret_cast<const uint4*>(a.emask + (long long)grow * a.emask_ld + gcol);
+      v.x = mask_pos_pk(v.x, em.x);
+      v.y = mask_pos_pk(v.y, em.y);
+      v.z = mask_pos_pk(v.z, em.z);
+      v.w = mask_pos_pk(v.w, em.w);
+    }
+    if (a.ucode) {  // max-unpool: the value goes to the window position its switch code names, 0 elsewhere
+      const int hw = a.OH * a.OW;
+      const int n = grow / hw, rem = grow - n * hw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      const uint2 cd = *reinterpret_cast<const uint2*>(a.ucode + ((long long)(n / a.ucode_div) * hw + rem) * a.OC + gcol);
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      const long long ob = (((long long)n * 2 * a.OH + 2 * oh) * 2 * a.OW + 2 * ow) * a.out_ld + gcol;
+#pragma unroll
+      for (int pos = 0; pos < 4; ++pos) {
+        uint32_t ov[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t cw = e < 2 ? cd.x : cd.y;
+          const uint32_t c0 = (cw >> (16 * (e & 1))) & 0xFFu, c1 = (cw >> (16 * (e & 1) + 8)) & 0xFFu;
+          ov[e] = (c0 == (uint32_t)pos ? vv[e] & 0xFFFFu : 0u) | (c1 == (uint32_t)pos ? vv[e] & 0xFFFF0000u : 0u);
+        }
+        const long long po = ob + ((long long)(pos >> 1) * 2 * a.OW + (pos & 1)) * a.out_ld;
+        if (DV_BOUNDS(po, 8, a.out_elems, "conv_dma unpool-out store"))
+          *reinterpret_cast<uint4*>(out + po) = uint4{ov[0], ov[1], ov[2], ov[3]};
+      }
+      continue;
+    }
+    *reinterpret_cast<uint4*>(out + o) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// KW3: 3x3 / stride 1 / pad 1 forward conv, 256 x 256 tile, where the three kw taps of a kernel row
+// share ONE staged A tile. Output rows are pixels in natural (n, oh, ow) order, so the kw-tap input
+// pixel of output row r is the kw=1 input pixel of output row r + kw - 1: one A tile of 258 rows
+// (output rows m0-1 .. m0+256, each row's kw=1 pixel of input row oh + kh - 1) serves all three
+// taps through a row shift of the fragment reads; the two rows per image row where the shift crosses
+// the image border (ow = 0 for kw = 0, ow = W-1 for kw = 2) are zeroed in registers (the conv's zero
+// padding). A K step is (kernel row kh, 32-channel chunk): A 258 x 64 B + B 3 x 256 x 64 B, i.e.
+// 1.47x fewer staged bytes per FLOP than the plain implicit GEMM (which stages A once per tap), for
+// the 256/512-channel layers whose DMA kernel moves ~9.6 TB/s of staging at 1.1-1.28 PF/s.
+// LDS rows are 64 B with the 16-B chunk XOR-swizzled by bit 2 of the row (q ^ 2((row >> 2) & 1)):
+// conflict-free ds_read_b128 fragment reads for ANY 16-row base (the shifted A reads).
+namespace {
+__device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; }
+}  // namespace
+
+// BN_: 256 (8 waves of 128 x 64) or 128 (8 waves of 64 x 64) output channels per workgroup
+template <int DT, int EPI, bool FP, int BN_ = 256>
+__global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
+  constexpr int BN = BN_, BM = 256, NW = 8;
+  constexpr int WN = BN == 256 ? 4 : 2, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
+  constexpr int A_I = 3;                   // A DMA instructions (16 rows each) per wave: 384 >= 258 rows
+  constexpr int B_I = 3 * BN / 16 / NW;    // B: 3 kw sub-tiles x BN rows (6 / 3 per wave)
+  constexpr int A_BYTES = A_I * NW * 1024, B_BYTES = 3 * BN * 64;
+  constexpr int STAGE = A_BYTES + B_BYTES;  // 72 / 48 KiB
+  static_assert(BM * BN * 2 <= 2 * STAGE, "C tile must fit in the operand stages");
+  typedef typename Vec8<DT>::type v8;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = wgid % tiles_n, tile_m = wgid / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int H = a.H, W = a.W, C = a.C, HW = a.H * a.W;
+
+  const int n_base = (m0 < a.M ? m0 : a.M - 1) / HW;
+  const long long img_elems = (long long)HW * a.x_ld;
+  const long long x_total = (long long)a.N * img_elems;
+  const __amdgpu_buffer_rsrc_t xr =
+      make_rsrc(a.x + (long long)n_base * img_elems, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
+
+  // DMA lanes: 16 rows x 4 chunks per instruction; row group bases are multiples of 16
+  const int lrow = lane >> 2;
+  const int lchunk = (lane & 3) ^ kw3_swz(lrow);
+  int r_pix[A_I], r_oh[A_I];
+#pragma unroll
+  for (int u = 0; u < A_I; ++u) {
+    const int s = (u * NW + wave) * 16 + lrow;  // staged row <-> output row m0 - 1 + s
+    const int m = m0 - 1 + s;
+    const int n = m >= 0 ? m / HW : -1;
+    const bool valid = s < BM + 2 && m >= 0 && m < a.M && n >= n_base;
+    const int rem = m - n * HW;
+    const int oh = rem / W;
+    r_pix[u] = valid ? (n - n_base) * HW + rem : 0;
+    r_oh[u] = valid ? oh : -(1 << 28);
+  }
+  // A-fragment rows whose kw = 0 / kw = 2 neighbour lies in the zero padding
+  uint32_t left = 0, right = 0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ow = (m0 + wm * FM * 16 + i * 16 + (lane & 15)) % W;
+    left |= (ow == 0 ? 1u : 0u) << i;
+    right |= (ow == W - 1 ? 1u : 0u) << i;
+  }
+  const int nch = C / 32;
+  const int nsteps = 3 * nch;
+  auto issue = [&](int step, int buf) {
+    const int kh = step / nch, cc = step - kh * nch;
+    uint8_t* As = smem + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int u = 0; u < A_I; ++u) {
+      const bool ok = (unsigned)(r_oh[u] + kh - 1) < (unsigned)H;
+      const uint32_t voff =
+          ok ? (uint32_t)((((long long)(r_pix[u] + (kh - 1) * W)) * a.x_ld + cc * 32 + lchunk * 8) * 2) : kOOB;
+      dma16(xr, As + (u * NW + wave) * 1024, voff);
+    }
+#pragma unroll
+    for (int u = 0; u < B_I; ++u) {
+      const int v = u * NW + wave;  // kw sub-tile v >> 4, rows (v & 15) * 16 + lrow
+      const int kw = v / (BN / 16), brow = (v % (BN / 16)) * 16 + lrow;
+      const uint32_t voff =
+          (uint32_t)((((long long)(n0 + brow)) * a.Kpad + (kh * 3 + kw) * C + cc * 32 + lchunk * 8) * 2);
+      dma16(wr, Bs + v * 1024, voff);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q = lane >> 4;
+  const int arow0 = wm * FM * 16 + (lane & 15);
+  const int brow0 = wn * FN * 16 + (lane & 15);
+  const int bswz = ((q ^ kw3_swz(brow0)) << 4);  // brow0 + 16 j: same bit 2
+
+  issue(0, 0);
+  for (int k = 0; k < nsteps; ++k) {
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
+    const uint8_t* As = smem + (k & 1) * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+    if constexpr (FP) {
+      // the next kw's B fragments are read before this kw's MFMAs (a full A+B double buffer spills);
+      // each A fragment is read right before its row of MFMAs
+      v8 bf[2][FN];
+      auto ldb = [&](int kw, int b) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bf[b][j] = *reinterpret_cast<const v8*>(Bs + kw * (BN * 64) + (brow0 + j * 16) * 64 + bswz);
+      };
+      ldb(0, 0);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        if (kw < 2) ldb(kw + 1, (kw + 1) & 1);
+        v8 af[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int sr = arow0 + i * 16 + kw;
+          af[i] = *reinterpret_cast<const v8*>(As + sr * 64 + ((q ^ kw3_swz(sr)) << 4));
+          if ((kw == 0 && ((left >> i) & 1)) || (kw == 2 && ((right >> i) & 1)))
+            af[i] = __builtin_bit_cast(v8, make_uint4(0u, 0u, 0u, 0u));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bf[kw & 1][j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      continue;
+    }
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      v8 bf[FN], af[FM];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bf[j] = *reinterpret_cast<const v8*>(Bs + kw * (BN * 64) + (brow0 + j * 16) * 64 + bswz);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int sr = arow0 + i * 16 + kw;
+        af[i] = *reinterpret_cast<const v8*>(As + sr * 64 + ((q ^ kw3_swz(sr)) << 4));
+        if ((kw == 0 && ((left >> i) & 1)) || (kw == 2 && ((right >> i) & 1)))
+          af[i] = __builtin_bit_cast(v8, make_uint4(0u, 0u, 0u, 0u));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bf[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  wait_vm<0>();
+
+  if constexpr (EPI == CONV_E_BF16) {
+    if (a.vec_epi) {
+      __syncthreads();
+      epilogue_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+      return;
+    }
+    if (a.res || a.emask) {
+      epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+      return;
+    }
+  }
+  if (a.accumulate)
+    epilogue<DT, FM, FN, EPI, true>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+  else
+    epilogue<DT, FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+}
+
+// DV_KW3: 0 disables the shared-kw-tap kernel (A/B), 2 forces it for every eligible launch regardless
+// of the grid size (tests: small shapes with many image borders per tile). Read per launch.
+static int kw3_mode() {
+  const char* e = std::getenv("DV_KW3");
+  return e ? std::atoi(e) : 1;
+}
+
+template <int DT, int AMODE, int EPI, int BN = 256>
+static int kw3_try(const ConvArgs& a, hipStream_t s) {
+  if constexpr (AMODE != CONV_A_FWD || EPI == CONV_E_POOL) {
+    return -4;
+  } else {
+    if (kw3_mode() == 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH ||
+        a.W != a.OW || a.C % 32 || a.mask || a.ws || a.OCpad % BN || (long long)a.Kpad < 9LL * a.C)
+      return -4;
+    const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / BN;
+    const long long nwg = (long long)tiles_m * tiles_n;
+    if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
+    // DV_KW3_FP=1: B fragments double-buffered across the kw sub-steps (measured equal to the plain
+    // loop, profiles/layers_r1_kw3_{nofp,on}.txt; a full A+B double buffer spills)
+    const char* fp = std::getenv("DV_KW3_FP");
+    if (fp != nullptr && std::atoi(fp) != 0)
+      hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, true, BN>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
+    else
+      hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, false, BN>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
+    return (int)hipGetLastError();
+  }
+}
+
+template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI, bool MASK = false,
+          bool FP = false, bool KS2 = false>
+static int dma_cfg(const ConvArgs& a, hipStream_t s) {
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  constexpr int NT = WM * WN * (KS2 ? 128 : 64);
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int tiles_n = a.OCpad / BN;
+  const long long nwg = (long long)tiles_m * tiles_n;
+  if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
+  const bool aligned = (a.C % BK) == 0;
+  const dim3 grid((unsigned)nwg, (unsigned)(a.ws ? a.ksplit : 1));
+  if (aligned)
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK, FP, KS2>), grid,
+                       dim3(NT), 0, s, a, tiles_n);
+  else
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP, KS2>), grid,
+                       dim3(NT), 0, s, a, tiles_n);
+  return (int)hipGetLastError();
+}
+
+// DV_DMA_VARIANT: 0 (default) 2-stage BK64 except 256x128 (3-stage); 1: all 2-stage BK64;
+// 2: BK32 x 4-stage rings for 256x256 and 512x64; 3: 128x256 3-stage for OC%256;
+// 4: register double-buffered fragments + s_setprio around MFMA runs (default for 256x256; v1
+// there selects the plain fragment loop) (A/B testing). Measured and removed: 4-wave 256x128 /
+// 128x256 workgroups (BK=32 x 3 stages, 72 KiB -> 2 per CU) on the 256/512-channel layers ran at
+// 0.53-0.72 PF/s vs 0.99-1.28 (profiles/layers_r1_dmav{0,5,6}.txt): 1.5x the staged bytes per FLOP.
+static int dma_variant() {
+  static int v = [] {
+    const char* e = std::getenv("DV_DMA_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+// DV_KS2=1 enables the in-workgroup K split (KS2) on the 256 x 128 and 512 x 64 tiles (A/B only).
+// Measured slower on every VGG16 layer it applies to (profiles/layers_r1_ks2_{off,on}.txt, e.g.
+// block2_conv2.down 0.72 -> 0.68 PF/s): these tiles are bound by the A-operand DMA stream (~9 TB/s
+// L2 -> LDS for both tile shapes), not by LDS fragment reads, so it stays off.
+static bool ks2_on() {
+  static bool v = [] {
+    const char* e = std::getenv("DV_KS2");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, cu = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cu = 256;
+    return cu > 0 ? cu : 256;
+  }();
+  return n;
+}
+
+// Tuning override (tools/tune_dma.py): force tile config `g_cfg` (> 0) and split-K factor
+// `g_ks` (> 0) for every DMA conv launch until reset to 0. Host-side globals, set between launches.
+extern int g_cfg, g_ks;  // tuning override, defined in conv_dma.hip
+
+// every tile config the DMA kernel is instantiated with; -5 = config does not fit this problem
+template <int DT, int AMODE, int EPI>
+static int dma_forced(const ConvArgs& a, hipStream_t s, int cfg) {
+  auto okn = [&](int bn) { return a.OCpad % bn == 0; };
+  switch (cfg) {
+    case 1: return okn(256) ? dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI, false, true>(a, s) : -5;  // 256x256
+    case 2: return okn(256) ? dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s) : -5;               // 128x256
+    case 3: return okn(128) ? dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s) : -5;               // 128x128
+    case 4: return okn(128) ? dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s) : -5;               // 256x128
+    case 5: return okn(64) ? dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, EPI>(a, s) : -5;                // 256x64
+    case 6: return okn(64) ? dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s) : -5;                // 512x64
+    case 7: return okn(64) ? dma_cfg<DT, 4, 1, 2, 4, 64, 3, AMODE, EPI>(a, s) : -5;                // 128x64, 4 waves
+    case 8: return okn(64) ? dma_cfg<DT, 2, 2, 2, 2, 64, 3, AMODE, EPI>(a, s) : -5;                // 64x64, 4 waves
+    case 9: return okn(128) ? dma_cfg<DT, 2, 2, 4, 4, 64, 2, AMODE, EPI>(a, s) : -5;               // 128x128, 4 waves
+    case 10: return okn(128) ? dma_cfg<DT, 2, 2, 2, 4, 64, 3, AMODE, EPI>(a, s) : -5;              // 64x128, 4 waves
+    case 11: return okn(64) ? dma_cfg<DT, 4, 1, 4, 4, 64, 2, AMODE, EPI>(a, s) : -5;               // 256x64, 4 waves
+    // deep rings for latency-bound small GEMMs (more K tiles in flight per workgroup)
+    case 12: return okn(64) ? dma_cfg<DT, 2, 2, 2, 2, 64, 6, AMODE, EPI>(a, s) : -5;               // 64x64 w4 ST6
+    case 13: return okn(64) ? dma_cfg<DT, 2, 2, 2, 2, 64, 8, AMODE, EPI>(a, s) : -5;               // 64x64 w4 ST8
+    case 14: return okn(64) ? dma_cfg<DT, 4, 1, 2, 4, 64, 6, AMODE, EPI>(a, s) : -5;               // 128x64 w4 ST6
+    case 15: return okn(128) ? dma_cfg<DT, 2, 2, 2, 4, 64, 6, AMODE, EPI>(a, s) : -5;              // 64x128 w4 ST6
+    default: return -5;
+  }
+}
+
+// Measured override of the size-based choice below for small and narrow-K problems (the DeepDream
+// nets' 1x1 / 1x7 / 5x5 convs and dgrads; tools/tune_dma.py sweep of every launch of configs 3 and 5,
+// profiles/tune_dma_c{3,5}.txt): conv time 9.80 -> 8.52 ms (InceptionV3, 4 octaves) and 6.45 -> 6.07
+// ms (ResNet-50 512^2 x 32). Small problems are bound by per-K-step latency, not MFMA rate: a 64x64
+// 4-wave tile with a 3-stage ring and no split-K; mid-size / short-K ones by the epilogue and DMA
+// issue of one big tile per CU: 128x128. The big-K VGG16 layers keep the large tiles.
+static int auto_cfg(const ConvArgs& a) {
+  static const bool off = std::getenv("DV_NO_AUTO_CFG") != nullptr;  // A/B: the size-based choice only
+  if (a.mask != nullptr || off) return 0;
+  const long long mn = (long long)a.M * a.OCpad;
+  if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= 256) return 8;
+  if (a.OCpad % 128 == 0 && a.OC > 64 && a.Kpad < 4096 && (a.Kpad < 1024 || mn < 50000000LL)) return 3;
+  return 0;
+}
+
+// Tile choice: the largest tile (best MFMA:LDS ratio) unless it leaves CUs idle. A problem with
+// fewer big tiles than the chip has CUs (deep layers at small batch, strong-scaled tiles) drops to
+// the next smaller tile, which doubles the workgroup count and fits 2 workgroups per CU in LDS.
+template <int DT, int AMODE, int EPI>
+static int dma_bn(const ConvArgs& a, hipStream_t s) {
+  if (g_cfg > 0) return dma_forced<DT, AMODE, EPI>(a, s, g_cfg);
+  if (const int c = auto_cfg(a)) return dma_forced<DT, AMODE, EPI>(a, s, c);
+  // measured (profiles/layers_r1_pipeline.txt): BK=32 x 4-stage rings lose to 2-stage BK=64 on the
+  // 256x256 and 512x64 tiles; the 3-stage BK=64 ring wins slightly on 256x128.
+  const int v = DT == DT_BF16 ? dma_variant() : 0;  // A/B variants are bf16-only
+  const long long cus = num_cus();
+  auto nwg = [&](int BM, int BN) { return (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN); };
+  if (a.OCpad % 256 == 0 && a.OC > 128) {
+    if (kw3_mode() == 2) {
+      const int rc = kw3_try<DT, AMODE, EPI>(a, s);
+      if (rc != -4) return rc;
+    }
+    if constexpr (DT == DT_BF16) {
+      if (v == 2) return dma_cfg<DT, 2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
+      if (v == 1 && nwg(256, 256) >= cus) return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);
+    }
+    if (v == 3 || (nwg(256, 256) < cus && nwg(128, 256) >= cus))
+      return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
+    if (nwg(256, 256) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
+    {  // 3x3 s1 p1 forward: the three kw taps share one staged A tile
+      const int rc = kw3_try<DT, AMODE, EPI>(a, s);
+      if (rc != -4) return rc;
+    }
+    // 256 x 256 with register double-buffered fragments: +3% on the big VGG layers (profiles/)
+    return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI, false, true>(a, s);
+  }
+  if (a.OCpad % 128 == 0 && a.OC > 64) {
+    if constexpr (DT == DT_BF16) {
+      if (v == 1) return dma_cfg<DT, 4, 2, 4, 4, 64, 2, AMODE, EPI>(a, s);
+      if (v == 4 && nwg(256, 128) >= cus) return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI, false, true>(a, s);
+    }
+    if (kw3_mode() == 2 || nwg(256, 128) >= cus) {  // 3x3 s1 p1 forward: shared-kw-tap 256 x 128 tile
+      const int rc = kw3_try<DT, AMODE, EPI, 128>(a, s);
+      if (rc != -4) return rc;
+    }
+    if (nwg(256, 128) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
+    if (ks2_on()) return dma_cfg<DT, 2, 2, 8, 4, 64, 3, AMODE, EPI, false, false, true>(a, s);  // 256 x 128, KS2
+    return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 256 x 128
+  }
+  if (a.OCpad % 64 == 0 && a.OC > 16) {
+    if constexpr (DT == DT_BF16) {
+      if (v == 2) return dma_cfg<DT, 8, 1, 4, 4, 32, 4, AMODE, EPI>(a, s);
+      if (v == 4 && nwg(512, 64) >= cus) return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI, false, true>(a, s);
+    }
+    if (nwg(512, 64) < cus) return dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 64
+    if (ks2_on()) return dma_cfg<DT, 4, 1, 8, 4, 64, 2, AMODE, EPI, false, false, true>(a, s);  // 512 x 64, KS2
+    return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s);  // 512 x 64
+  }
+  if (a.OCpad % 16 == 0) {
+    if (nwg(512, 16) < cus) return dma_cfg<DT, 8, 1, 2, 1, 64, 2, AMODE, EPI>(a, s);  // 256 x 16
+    return dma_cfg<DT, 8, 1, 4, 1, 64, 2, AMODE, EPI>(a, s);  // 512 x 16
+  }
+  return -3;
+}
+
+// ReLU-masked dgrad: the mask tile doubles A's LDS footprint, so smaller tiles than dma_bn
+// (<= 128 KiB of LDS per workgroup at 2 stages)
+template <int DT, int AMODE>
+static int dma_mask_bn(const ConvArgs& a, hipStream_t s) {
+  if (a.OCpad % 256 == 0 && a.OC > 128) return dma_cfg<DT, 2, 4, 4, 4, 64, 2, AMODE, CONV_E_BF16, true>(a, s);  // 128x256
+  if (a.OCpad % 128 == 0 && a.OC > 64) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, CONV_E_BF16, true>(a, s);   // 128x128
+  if (a.OCpad % 64 == 0 && a.OC > 16) return dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, CONV_E_BF16, true>(a, s);    // 256x64
+  if (a.OCpad % 16 == 0) return dma_cfg<DT, 8, 1, 2, 1, 64, 2, AMODE, CONV_E_BF16, true>(a, s);                // 256x16
+  return -3;
+}
+
+// Tile dims the default (DV_DMA_VARIANT=0) selection above picks, for split-K planning.
+static void dma_tile_dims(const ConvArgs& a, bool mask, int& BM, int& BN) {
+  const long long cus = num_cus();
+  auto nwg = [&](int bm, int bn) { return (long long)((a.M + bm - 1) / bm) * (a.OCpad / bn); };
+  BM = 256;
+  BN = 16;
+  if (!mask) {
+    const int c = auto_cfg(a);
+    if (c == 8) { BM = 64; BN = 64; return; }
+    if (c == 3) { BM = 128; BN = 128; return; }
+  }
+  if (mask) {
+    if (a.OCpad % 256 == 0 && a.OC > 128) { BM = 128; BN = 256; }
+    else if (a.OCpad % 128 == 0 && a.OC > 64) { BM = 128; BN = 128; }
+    else if (a.OCpad % 64 == 0 && a.OC > 16) { BM = 256; BN = 64; }
+    return;
+  }
+  if (a.OCpad % 256 == 0 && a.OC > 128) {
+    if (nwg(256, 256) >= cus) { BM = 256; BN = 256; }
+    else if (nwg(128, 256) >= cus) { BM = 128; BN = 256; }
+    else { BM = 128; BN = 128; }
+  } else if (a.OCpad % 128 == 0 && a.OC > 64) {
+    BM = nwg(256, 128) < cus ? 128 : 256;
+    BN = 128;
+  } else if (a.OCpad % 64 == 0 && a.OC > 16) {
+    BM = nwg(512, 64) < cus ? 256 : 512;
+    BN = 64;
+  } else {
+    BM = nwg(512, 16) < cus ? 256 : 512;
+  }
+}
+
+// one dma_bn<DT, AMODE, EPI> per instantiation unit (conv_dma_*.hip)
+int dma_run_bf16_fwd(const ConvArgs& a, hipStream_t s);
+int dma_run_bf16_fwd_pool(const ConvArgs& a, hipStream_t s);
+int dma_run_bf16_fwd_f32(const ConvArgs& a, hipStream_t s);
+int dma_run_bf16_tr(const ConvArgs& a, hipStream_t s);
+int dma_run_f16_fwd(const ConvArgs& a, hipStream_t s);
+int dma_run_f16_tr(const ConvArgs& a, hipStream_t s);
+
+}  // namespace dv

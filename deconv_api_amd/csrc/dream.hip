@@ -38,6 +38,7 @@ __global__ void __launch_bounds__(256) sumsq_core_kernel(const uint16_t* __restr
 template <int DT>
 __global__ void __launch_bounds__(256) sumsq_core_bwd_kernel(const uint16_t* __restrict__ x,
                                                              const float* __restrict__ scale,
+                                                             const uint16_t* __restrict__ addend,
                                                              uint16_t* __restrict__ gx, int N, int H, int W, int C,
                                                              int b) {
   const int cpp = C >> 3;
@@ -47,14 +48,19 @@ __global__ void __launch_bounds__(256) sumsq_core_bwd_kernel(const uint16_t* __r
     const int ww = (int)(pix % W);
     const int hh = (int)((pix / W) % H);
     const int n = (int)(pix / ((long long)W * H));
-    uint4 o = {0u, 0u, 0u, 0u};
-    if (hh >= b && hh < H - b && ww >= b && ww < W - b) {
+    const bool core = hh >= b && hh < H - b && ww >= b && ww < W - b;
+    // addend (the gradient flowing back from the layers above a loss tap): gx = addend + loss grad
+    uint4 o = addend ? *reinterpret_cast<const uint4*>(addend + t * 8) : uint4{0u, 0u, 0u, 0u};
+    if (core) {
       const float s2 = 2.f * scale[n];
       const uint4 v = *reinterpret_cast<const uint4*>(x + t * 8);
-      o.x = pack2<DT>(s2 * to_f<DT>(v.x & 0xFFFFu), s2 * to_f<DT>(v.x >> 16));
-      o.y = pack2<DT>(s2 * to_f<DT>(v.y & 0xFFFFu), s2 * to_f<DT>(v.y >> 16));
-      o.z = pack2<DT>(s2 * to_f<DT>(v.z & 0xFFFFu), s2 * to_f<DT>(v.z >> 16));
-      o.w = pack2<DT>(s2 * to_f<DT>(v.w & 0xFFFFu), s2 * to_f<DT>(v.w >> 16));
+      const uint32_t vi[4] = {v.x, v.y, v.z, v.w};
+      uint32_t oi[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        oi[e] = pack2<DT>(s2 * to_f<DT>(vi[e] & 0xFFFFu) + to_f<DT>(oi[e] & 0xFFFFu),
+                          s2 * to_f<DT>(vi[e] >> 16) + to_f<DT>(oi[e] >> 16));
+      o = uint4{oi[0], oi[1], oi[2], oi[3]};
     }
     *reinterpret_cast<uint4*>(gx + t * 8) = o;
   }
@@ -340,15 +346,15 @@ int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, i
   return (int)hipGetLastError();
 }
 
-int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, uint16_t* gx, int N, int H, int W, int C, int b,
-                          int dtype, hipStream_t s) {
+int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, const uint16_t* addend, uint16_t* gx, int N, int H,
+                          int W, int C, int b, int dtype, hipStream_t s) {
   if (C % 8 != 0) return -1;
   const long long total = (long long)N * H * W * (C / 8);
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 256LL * 32);
   if (dtype == DT_F16)
-    hipLaunchKernelGGL(sumsq_core_bwd_kernel<DT_F16>, dim3(grid), dim3(256), 0, s, x, scale, gx, N, H, W, C, b);
+    hipLaunchKernelGGL(sumsq_core_bwd_kernel<DT_F16>, dim3(grid), dim3(256), 0, s, x, scale, addend, gx, N, H, W, C, b);
   else
-    hipLaunchKernelGGL(sumsq_core_bwd_kernel<DT_BF16>, dim3(grid), dim3(256), 0, s, x, scale, gx, N, H, W, C, b);
+    hipLaunchKernelGGL(sumsq_core_bwd_kernel<DT_BF16>, dim3(grid), dim3(256), 0, s, x, scale, addend, gx, N, H, W, C, b);
   return (int)hipGetLastError();
 }
 

@@ -128,7 +128,7 @@ int tile_update_launch(const uint16_t* packs, long long pack_elems, int units_pe
                        int H, int W, int Th, int Tw, int dtype, hipStream_t s);
 int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, int W, int C, int b, int dtype,
                       hipStream_t s);
-int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, uint16_t* gx, int N, int H, int W, int C, int b,
+int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, const uint16_t* addend, uint16_t* gx, int N, int H, int W, int C, int b,
                           int dtype, hipStream_t s);
 // col2im of a strided conv's input gradient for <= 8 input channels (output padded to 8 channels)
 struct Col2ImGeom {

@@ -29,7 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from ..ops import native
-from ..ops.autograd import premasked_grads, sumsq_core
+from ..ops.autograd import loss_tap, premasked_grads, sumsq_core
 
 # DV_DREAM_FUSED=0: the step tail (loss, normalization, update) as torch ops instead of the fused
 # HIP kernels (A/B); DV_DREAM_GRAPHS: hipGraph cache entries (octave shapes) kept, LRU-evicted
@@ -45,6 +45,9 @@ OCTAVE_GRAPH = os.environ.get("DV_DREAM_OCTAVE_GRAPH", "1") != "0"
 # (B=64, 299^2): 1 -> 327, 2 -> 356, 4 -> 232 img/s (4 side streams + the default stream exceed the
 # 4 hardware queues per process).
 SPLIT = int(os.environ.get("DV_DREAM_SPLIT", "2"))
+# DV_DREAM_TAPS=0: intermediate loss layers get their loss gradient through autograd's sum (A/B);
+# default: a loss tap adds it into the gradient from above in the loss-gradient kernel itself
+TAPS = os.environ.get("DV_DREAM_TAPS", "1") != "0"
 LOSS_PARTS = 32
 
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
@@ -142,26 +145,51 @@ class DeepDream:
         st.graph = None
         return st
 
-    def _fused_step(self, st) -> None:
-        """forward -> per-layer sumsq partials + loss gradients (HIP) -> autograd backward of the
-        network only -> one fused normalize/update kernel that also writes the next xin."""
+    def _loss_grad(self, st, xin: torch.Tensor) -> torch.Tensor:
+        """Fused-path forward + loss partials (into st.lpart) + gradient w.r.t. ``xin``. Every loss
+        layer but the deepest is a loss tap (ops.autograd.loss_tap): its loss gradient joins the
+        gradient from above inside one kernel, so autograd starts from the deepest layer only."""
         lib = native.lib()
         names = list(self.s.layers.keys())
         b = self.s.border
+        if st.scales is None:
+            st.scales = {}
+        tapped = set()
+
+        def scale(name, a):
+            if name not in st.scales:
+                st.scales[name] = torch.full((a.shape[0],), self.s.layers[name] / float(a[0].numel()),
+                                             dtype=torch.float32, device=self.device)
+            return st.scales[name]
+
+        def tap(name, a):
+            a = a.contiguous()
+            tapped.add(name)
+            return loss_tap(a, scale(name, a), b)
+
         with premasked_grads():  # the loss gradient 2*act/numel vanishes where act does
-            acts = self.net.forward(st.xin, names)
+            acts = self.net.forward(xin, names, tap=tap if TAPS else None)
         outs = [acts[n].contiguous() for n in names]
         if st.lcoef is None:
             coef = [self.s.layers[n] / float(a[0].numel()) for n, a in zip(names, outs)]
             st.lcoef = torch.tensor(coef, dtype=torch.float32, device=self.device)
-            st.scales = [torch.full((outs[0].shape[0],), c, dtype=torch.float32, device=self.device) for c in coef]
-        gacts = []
-        for i, a in enumerate(outs):
+        roots, gacts = [], []
+        for i, (n, a) in enumerate(zip(names, outs)):
             lib.sumsq_core(a, st.lpart[i], b)
+            if n in tapped:
+                continue
             ga = torch.empty_like(a)
-            lib.sumsq_core_bwd(a, st.scales[i], ga, b)
+            lib.sumsq_core_bwd(a, scale(n, a), ga, b)
+            roots.append(a)
             gacts.append(ga)
-        (g,) = torch.autograd.grad(outs, st.xin, gacts)
+        (g,) = torch.autograd.grad(roots, xin, gacts)
+        return g
+
+    def _fused_step(self, st) -> None:
+        """forward -> per-layer sumsq partials + loss gradients (HIP) -> autograd backward of the
+        network only -> one fused normalize/update kernel that also writes the next xin."""
+        lib = native.lib()
+        g = self._loss_grad(st, st.xin)
         ml = -1.0 if self.s.max_loss is None else float(self.s.max_loss)
         lib.dream_update(g.contiguous(), st.x, st.xin, st.gpart, st.lpart, st.lcoef, st.done, st.loss,
                          float(self.s.step), ml)
@@ -473,22 +501,8 @@ class TiledDeepDream(DeepDream):
         lib = native.lib()
         if st.mine == 0:
             return
-        names = list(self.s.layers.keys())
         lib.tile_gather(st.x, st.xin, st.plan, st.shifts[it], st.rank, st.world)
-        with premasked_grads():
-            acts = self.net.forward(st.xin, names)
-        outs = [acts[n].contiguous() for n in names]
-        if st.lcoef is None:
-            coef = [self.s.layers[n] / float(a[0].numel()) for n, a in zip(names, outs)]
-            st.lcoef = torch.tensor(coef, dtype=torch.float32, device=self.device)
-            st.scales = [torch.full((st.mine,), c, dtype=torch.float32, device=self.device) for c in coef]
-        gacts = []
-        for i, a in enumerate(outs):
-            lib.sumsq_core(a, st.lpart[i], self.s.border)
-            ga = torch.empty_like(a)
-            lib.sumsq_core_bwd(a, st.scales[i], ga, self.s.border)
-            gacts.append(ga)
-        (g,) = torch.autograd.grad(outs, st.xin, gacts)
+        g = self._loss_grad(st, st.xin)
         lib.tile_pack(g.contiguous(), st.pack, st.plan, st.lpart, st.lcoef, st.ucap, st.rank, st.world)
 
     def _tile_apply(self, st, it: int) -> None:

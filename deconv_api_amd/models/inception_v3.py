@@ -117,8 +117,9 @@ class InceptionV3:
                 x = self.units[op](x)
         return x
 
-    def forward(self, x: torch.Tensor, outputs: Iterable[str] = ("mixed10",)) -> Dict[str, torch.Tensor]:
-        """x: [N, H, W, 8] (RGB in slots 0..2, inception preprocessing x/127.5 - 1)."""
+    def forward(self, x: torch.Tensor, outputs: Iterable[str] = ("mixed10",), tap=None) -> Dict[str, torch.Tensor]:
+        """x: [N, H, W, 8] (RGB in slots 0..2, inception preprocessing x/127.5 - 1). ``tap(name, t)``
+        (optional) replaces every requested output except the deepest before deeper layers use it."""
         want = set(outputs)
         last = max(MIXED.index(o) for o in want)
         for op in self.stem:
@@ -134,5 +135,7 @@ class InceptionV3:
             else:
                 x = cat_channels([self._branch(x, br[k]) for k in order])
             if name in want:
+                if tap is not None and bi < last:
+                    x = tap(name, x)
                 out[name] = x
         return out

@@ -62,7 +62,10 @@ class ResNet50:
     def num_params(self) -> int:
         return sum(u.w.numel() + u.b.numel() for u in self.units.values())
 
-    def forward(self, x: torch.Tensor, outputs: Iterable[str] = ("conv5_block3_out",)) -> Dict[str, torch.Tensor]:
+    def forward(self, x: torch.Tensor, outputs: Iterable[str] = ("conv5_block3_out",),
+                tap=None) -> Dict[str, torch.Tensor]:
+        """``tap(name, t)`` (optional) replaces every requested output except the deepest before
+        deeper blocks use it (the DeepDream loss taps)."""
         want = set(outputs)
         names = self.block_names
         last = max(names.index(o) for o in want)
@@ -77,5 +80,7 @@ class ResNet50:
             # elementwise kernels in the backward; see ops.autograd._BottleneckFn)
             x = bottleneck(x, u[c1], u[c2], u[c3], u[short] if short is not None else None)
             if name in want:
+                if tap is not None and i < last:
+                    x = tap(name, x)
                 out[name] = x
         return out

@@ -322,6 +322,33 @@ class _SumSqCoreFn(torch.autograd.Function):
         return gx, None
 
 
+class _LossTapFn(torch.autograd.Function):
+    """Identity on an intermediate DeepDream loss layer whose output also feeds deeper layers. Its
+    backward adds the layer's own loss gradient (2 * scale[n] * a on the border-b core) to the
+    gradient arriving from above in ONE kernel (sumsq_core_bwd with an addend), instead of autograd
+    summing two separately materialized gradients (an extra elementwise add per tap and step)."""
+
+    @staticmethod
+    def forward(ctx, a, scale, b: int):
+        ctx.save_for_backward(a, scale)
+        ctx.b = b
+        return a.view_as(a)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, scale = ctx.saved_tensors
+        gx = torch.empty_like(a)
+        native.lib().sumsq_core_bwd(a, scale, gx, ctx.b, g.contiguous())
+        return gx, None, None
+
+
+def loss_tap(a: torch.Tensor, scale: torch.Tensor, b: int) -> torch.Tensor:
+    """``a`` unchanged; its gradient gains the DeepDream loss term of ``a`` (GPU, contiguous a). The
+    ReLU-output tag carries over: the consumer's backward relies on it to hand back a gradient
+    already masked by a > 0 (the premasked contract)."""
+    return _tag(_LossTapFn.apply(a, scale, b), _is_relu_out(a))
+
+
 def sumsq_core(x: torch.Tensor, b: int) -> torch.Tensor:
     """sum(x[:, b:-b, b:-b, :]^2) per image, fp32 [N] (the DeepDream activation loss term)."""
     if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.shape[3] % 8 == 0:

@@ -29,5 +29,5 @@ def test_debug_macro_is_a_constant_in_release():
     src = open(os.path.join(CSRC, "common.h")).read()
     assert "#define DV_BOUNDS(off, n, extent, what) true" in src
     assert src.count("DV_BOUNDS") >= 3
-    for f in ("conv_dma.hip", "conv_halo_stream.hip", "conv_smalln.hip"):
+    for f in ("conv_dma_impl.h", "conv_halo_stream.hip", "conv_smalln.hip"):
         assert "DV_BOUNDS" in open(os.path.join(CSRC, f)).read(), f

@@ -2,7 +2,7 @@
 """Summarize ``hipcc -Rpass-analysis=kernel-resource-usage`` remarks (VGPRs, AGPRs, spills, occupancy,
 LDS) per demangled kernel, optionally filtered by a substring of the demangled name.
 
-  hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only -c deconv_api_amd/csrc/conv_dma.hip \\
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only -c deconv_api_amd/csrc/conv_dma_bf16_fwd.hip \\
       -o /tmp/x.o -Rpass-analysis=kernel-resource-usage 2> /tmp/ru.txt
   python tools/resource_usage.py /tmp/ru.txt --filter conv_dma_kw3
 """
