@@ -165,6 +165,32 @@ def _dgrad(unit: ConvUnit, gy, mask, in_hw, emask=None):
     return gx if emask is None else torch.ops.aten.threshold_backward(gx, emask, 0)
 
 
+# strided-conv input gradients below this many (full transposed-GEMM) FLOPs run as ONE transposed
+# conv written straight into its destination (accumulate / x-mask epilogue) instead of s^2
+# sub-pixel GEMMs + copies: small maps are launch-latency bound, not MFMA bound
+STRIDED_DIRECT_FLOPS = float(os.environ.get("DV_STRIDED_DIRECT_GFLOP", "60")) * 1e9
+
+
+def strided_direct(unit: ConvUnit, gy, in_hw) -> bool:
+    kh, kw = unit.w.shape[2:]
+    fl = 2.0 * gy.shape[0] * in_hw[0] * in_hw[1] * unit.cin * unit.cout * kh * kw
+    return unit.col_w is None and fl <= STRIDED_DIRECT_FLOPS
+
+
+def dgrad_strided_into(unit: ConvUnit, gy, in_hw, out: torch.Tensor, accumulate: bool = False,
+                       emask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``out`` (=|+=) input gradient of a strided conv, zeroed where ``emask`` <= 0: one transposed
+    conv on the LDS-DMA kernel when small (``strided_direct``), else the sub-pixel / col2im path
+    plus one elementwise pass."""
+    if strided_direct(unit, gy, in_hw):
+        return conv2d(gy, unit.bwd, stride=unit.stride, pad=unit.pad, relu=False, in_mode="transpose",
+                      out_hw=in_hw, use_bias=False, out=out, accumulate=accumulate, emask=emask)
+    r = _dgrad_strided(unit, gy, None, in_hw)
+    if emask is not None:
+        r = torch.ops.aten.threshold_backward(r, emask, 0)
+    return out.add_(r) if accumulate else out.copy_(r)
+
+
 def _dgrad_strided(unit: ConvUnit, gy, mask, in_hw):
     if unit.col_w is not None and COL2IM:
         return _col2im_dgrad(gy, mask, unit, in_hw)

@@ -35,7 +35,7 @@ import torch
 import torch.nn.functional as F
 
 from . import native
-from .autograd import _PREMASKED, ConvUnit, _dgrad_strided, _is_relu_out, _tag
+from .autograd import _PREMASKED, ConvUnit, _is_relu_out, _tag, dgrad_strided_into
 from .conv import conv2d
 
 
@@ -247,10 +247,9 @@ class _InceptionFn(torch.autograd.Function):
             if u.stride == 1:
                 return conv2d(g, u.bwd, stride=1, pad=u.bwd_pad, relu=False, use_bias=False, emask=inp, out=out,
                               accumulate=accumulate)
-            r = torch.ops.aten.threshold_backward(_dgrad_strided(u, g, None, (inp.shape[1], inp.shape[2])), inp, 0)
             if out is None:
-                return r
-            return out.add_(r) if accumulate else out.copy_(r)
+                out = torch.empty_like(inp)
+            return dgrad_strided_into(u, g, (inp.shape[1], inp.shape[2]), out, accumulate, emask=inp)
 
         deferred = []  # head-conv contributions on x go last: their epilogue applies the x mask
         for off, wdt, kind, info in ctx.plan:
@@ -290,8 +289,10 @@ class _InceptionFn(torch.autograd.Function):
                         deferred.append((ub.bwd, g[..., ua.cout:]))
                     elif units[0].stride == 1:
                         deferred.append((units[0].bwd, g))
-                    else:
-                        contribute_tensor(_dgrad_strided(units[0], g, None, (H, W)))
+                    else:  # strided head on x: straight into gx (written / accumulated)
+                        dgrad_strided_into(units[0], g, (H, W), gx, accumulate=state["written"])
+                        state["written"] = True
+                        state["masked"] = False
                     continue
                 if len(units) == 2:  # split: sum of two dgrads, masked by inp > 0
                     ua, ub = units

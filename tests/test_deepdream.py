@@ -275,12 +275,15 @@ def test_gpu_bottleneck_block_grad(native_lib, stride, proj, premasked):
 @pytest.mark.gpu
 @pytest.mark.parametrize("bi,hw", [(0, 11), (3, 11), (4, 9), (8, 9), (9, 5)])
 @pytest.mark.parametrize("premasked", [False, True])
-def test_gpu_inception_block_grad(native_lib, bi, hw, premasked):
+@pytest.mark.parametrize("strided_direct", [True, False])
+def test_gpu_inception_block_grad(native_lib, bi, hw, premasked, strided_direct, monkeypatch):
     """One-node InceptionV3 mixed block (direct concat-slice writes, commuted avg-pool branch,
     accumulate/emask epilogues) vs CPU autograd of the unfused block: mixed0 (A), mixed3 (B),
-    mixed4 (C), mixed8 (D, strided + max), mixed9 (E, split convs)."""
+    mixed4 (C), mixed8 (D, strided + max), mixed9 (E, split convs). Strided-conv gradients both as
+    one transposed conv into gx (small maps) and as sub-pixel GEMMs (large maps)."""
     from deconv_api_amd.ops import autograd as AG
 
+    monkeypatch.setattr(AG, "STRIDED_DIRECT_FLOPS", 1e30 if strided_direct else 0.0)
     cpu, gpu = InceptionV3(0).build("cpu"), InceptionV3(0).build("cuda")
     cin = [192, 256, 288, 288, 768, 768, 768, 768, 768, 1280, 2048][bi]
     g = torch.Generator().manual_seed(bi + 17 * premasked)

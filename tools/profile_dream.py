@@ -68,7 +68,14 @@ def main():
         oh, ow = (y.shape[1], y.shape[2]) if out is None else (out.shape[1], out.shape[2])
         M = xx.shape[0] * oh * ow
         fl = 2.0 * M * cw.cout * cw.KH * cw.KW * cw.cin
-        records.append((names.get(id(cw), ("?", "?")), M, cw.cout, cw.K, fl, st, en))
+        # compulsory HBM bytes: input + output (+ residual / output-mask / accumulate reads)
+        by = xx.numel() * xx.element_size() + M * cw.cout * y.element_size()
+        for k in ("res", "emask"):
+            if kw.get(k) is not None:
+                by += kw[k].numel() * kw[k].element_size()
+        if kw.get("accumulate"):
+            by += M * cw.cout * y.element_size()
+        records.append((names.get(id(cw), ("?", "?")), M, cw.cout, cw.K, fl, by, st, en))
         return r
 
     ag.conv2d = timed
@@ -92,11 +99,11 @@ def main():
         step_ms = s0.elapsed_time(s1)
         tot_t = tot_f = 0.0
         rows = []
-        for (n, kind), M, N, K, fl, st, en in records:
+        for (n, kind), M, N, K, fl, by, st, en in records:
             ms = st.elapsed_time(en)
             tot_t += ms
             tot_f += fl
-            rows.append((ms, n, kind, M, N, K, fl))
+            rows.append((ms, n, kind, M, N, K, fl, by))
             per_unit[(n, kind)][0] += ms
             per_unit[(n, kind)][1] += fl
         grand_t += tot_t
@@ -106,9 +113,9 @@ def main():
               f"in {len(rows)} launches, {tot_f / 1e12:.3f} TFLOP, {tot_f / tot_t / 1e9:.0f} TF/s on conv time, "
               f"{tot_f / step_ms / 1e9:.0f} TF/s on step time")
         rows.sort(reverse=True)
-        print(f"  {'unit':22s} {'kind':9s} {'M':>9s} {'N':>5s} {'K':>6s} {'ms':>7s} {'TF/s':>7s}")
-        for ms, n, kind, M, N, K, fl in rows[: a.top]:
-            print(f"  {n:22s} {kind:9s} {M:9d} {N:5d} {K:6d} {ms:7.3f} {fl / ms / 1e9:7.0f}")
+        print(f"  {'unit':22s} {'kind':9s} {'M':>9s} {'N':>5s} {'K':>6s} {'ms':>7s} {'TF/s':>7s} {'GB/s':>7s}")
+        for ms, n, kind, M, N, K, fl, by in rows[: a.top]:
+            print(f"  {n:22s} {kind:9s} {M:9d} {N:5d} {K:6d} {ms:7.3f} {fl / ms / 1e9:7.0f} {by / ms / 1e6:7.0f}")
     print(f"=== all octaves: step {grand_step:.2f} ms, conv {grand_t:.2f} ms, {grand_f / 1e12:.3f} TFLOP "
           f"({grand_f / grand_step / 1e9:.0f} TF/s on step time)")
     print("per unit (summed over octaves):")
