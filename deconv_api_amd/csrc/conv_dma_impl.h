@@ -540,33 +540,6 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
   constexpr int SWZ = (CPR < 8 ? CPR : 8) - 1;
   const int row_l = (lane >> 4) * 4, col_l = lane & 15;
   const bool pre_relu = a.relu && a.res == nullptr;
-  // Residual / accumulate / output-mask operands of this thread's (<= 4) chunks are loaded BEFORE
-  // the C tile goes through LDS, so their HBM latency overlaps the LDS staging instead of
-  // serializing once per chunk after it: the short-K GEMMs with a residual (ResNet c3 convs,
-  // K = 64..256) are epilogue-latency bound (~3 TB/s, profiles/tune_dma_c5.txt).
-  constexpr int ITER = (BM * CPR + NT - 1) / NT;
-  constexpr bool PF = ITER <= 4;
-  const bool prefetch = PF && a.ucode == nullptr && (a.res || a.accumulate || a.emask);
-  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
-  uint4 pre_r[PF ? ITER : 1], pre_a[PF ? ITER : 1], pre_m[PF ? ITER : 1];
-  if constexpr (PF) {
-#pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-      pre_r[it] = pre_a[it] = pre_m[it] = uint4{0u, 0u, 0u, 0u};
-      const int c = tid + it * NT;
-      const int row = c / CPR, cc = c % CPR;
-      const int grow = m0 + row, gcol = n0 + cc * 8;
-      if (!prefetch || c >= BM * CPR || grow >= a.M || gcol + 8 > a.OC) continue;
-      const long long o = (long long)grow * a.out_ld + gcol;
-      if (a.accumulate && DV_BOUNDS(o, 8, a.out_elems, "conv_dma epilogue_lds acc prefetch"))
-        pre_a[it] = *reinterpret_cast<const uint4*>(out + o);
-      if (a.res && DV_BOUNDS((long long)grow * a.res_ld + gcol, 8, a.res_elems, "conv_dma epilogue_lds res prefetch"))
-        pre_r[it] = *reinterpret_cast<const uint4*>(a.res + (long long)grow * a.res_ld + gcol);
-      if (a.emask &&
-          DV_BOUNDS((long long)grow * a.emask_ld + gcol, 8, a.emask_elems, "conv_dma epilogue_lds emask prefetch"))
-        pre_m[it] = *reinterpret_cast<const uint4*>(a.emask + (long long)grow * a.emask_ld + gcol);
-    }
-  }
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     if (!writer) break;
@@ -585,21 +558,21 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
       }
   }
   __syncthreads();
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
   const bool post = a.accumulate || a.res != nullptr;
-  // one 16-B output chunk; `have`: its res / accumulate / emask operands are the prefetched ones
-  auto chunk = [&](int c, bool have, const uint4& rpre, const uint4& apre, const uint4& mpre) {
+  for (int c = tid; c < BM * CPR; c += NT) {
     const int row = c / CPR, cc = c % CPR;
     const int grow = m0 + row, gcol = n0 + cc * 8;
-    if (grow >= a.M || gcol >= a.OC) return;
+    if (grow >= a.M || gcol >= a.OC) continue;
     uint4 v = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((cc ^ (row & SWZ)) << 4));
     const long long o = (long long)grow * a.out_ld + gcol;
-    if (!a.ucode && !DV_BOUNDS(o, gcol + 8 > a.OC ? a.OC - gcol : 8, a.out_elems, "conv_dma epilogue_lds out")) return;
+    if (!a.ucode && !DV_BOUNDS(o, gcol + 8 > a.OC ? a.OC - gcol : 8, a.out_elems, "conv_dma epilogue_lds out")) continue;
     if (a.res && !DV_BOUNDS((long long)grow * a.res_ld + gcol, gcol + 8 > a.OC ? a.OC - gcol : 8, a.res_elems,
                             "conv_dma epilogue_lds res"))
-      return;
+      continue;
     if (a.emask && !DV_BOUNDS((long long)grow * a.emask_ld + gcol, gcol + 8 > a.OC ? a.OC - gcol : 8, a.emask_elems,
                               "conv_dma epilogue_lds emask"))
-      return;
+      continue;
     if (gcol + 8 > a.OC) {  // a row's last partial chunk: element-wise (no 16-B access past OC)
       const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
       for (int e = 0; e < a.OC - gcol; ++e) {
@@ -615,12 +588,12 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
         }
         out[o + e] = from_f<DT>(f);
       }
-      return;
+      continue;
     }
     if (post) {
       uint4 ad = {0u, 0u, 0u, 0u}, rs = {0u, 0u, 0u, 0u};
-      if (a.accumulate) ad = have ? apre : *reinterpret_cast<const uint4*>(out + o);
-      if (a.res) rs = have ? rpre : *reinterpret_cast<const uint4*>(a.res + (long long)grow * a.res_ld + gcol);
+      if (a.accumulate) ad = *reinterpret_cast<const uint4*>(out + o);
+      if (a.res) rs = *reinterpret_cast<const uint4*>(a.res + (long long)grow * a.res_ld + gcol);
       const uint32_t vv[4] = {v.x, v.y, v.z, v.w}, aa[4] = {ad.x, ad.y, ad.z, ad.w}, rr[4] = {rs.x, rs.y, rs.z, rs.w};
       uint32_t ov[4];
 #pragma unroll
@@ -636,7 +609,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
       v = uint4{ov[0], ov[1], ov[2], ov[3]};
     }
     if (a.emask) {
-      const uint4 em = have ? mpre : *reinterpret_cast<const uint4*>(a.emask + (long long)grow * a.emask_ld + gcol);
+      const uint4 em = *reinterpret_cast<const uint4*>(a.emask + (long long)grow * a.emask_ld + gcol);
       v.x = mask_pos_pk(v.x, em.x);
       v.y = mask_pos_pk(v.y, em.y);
       v.z = mask_pos_pk(v.z, em.z);
@@ -662,17 +635,9 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
         if (DV_BOUNDS(po, 8, a.out_elems, "conv_dma unpool-out store"))
           *reinterpret_cast<uint4*>(out + po) = uint4{ov[0], ov[1], ov[2], ov[3]};
       }
-      return;
+      continue;
     }
     *reinterpret_cast<uint4*>(out + o) = v;
-  };
-  if constexpr (PF) {
-#pragma unroll
-    for (int it = 0; it < ITER; ++it)
-      if (tid + it * NT < BM * CPR) chunk(tid + it * NT, prefetch, pre_r[it], pre_a[it], pre_m[it]);
-  } else {
-    const uint4 z = {0u, 0u, 0u, 0u};
-    for (int c = tid; c < BM * CPR; c += NT) chunk(c, false, z, z, z);
   }
 }
 
