@@ -159,6 +159,8 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     auto al = [](const void* p, int64_t ld) { return reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 8 == 0; };
     a.vec_epi = epi == dv::CONV_E_BF16 && al(a.out, a.out_ld) && (!a.res || al(a.res, a.res_ld)) &&
                 (!a.emask || al(a.emask, a.emask_ld)) && std::getenv("DV_NO_VEC_EPI") == nullptr;
+    static const bool no_batch = std::getenv("DV_NO_EPI_BATCH") != nullptr;
+    a.epi_batch = !no_batch;
   }
   if (ucode.has_value()) {  // max-unpooled output (the consumer of this conv reads the full-res map)
     check_cuda(*ucode, "ucode");

@@ -527,6 +527,45 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[F
   }
 }
 
+// one 16-bit output chunk's v (+ accumulate operand ad) (+ residual rs) [ReLU after a residual]
+template <int DT>
+__device__ __forceinline__ uint4 epi_combine(const ConvArgs& a, uint4 v, uint4 ad, uint4 rs) {
+  const uint32_t vv[4] = {v.x, v.y, v.z, v.w}, aa[4] = {ad.x, ad.y, ad.z, ad.w}, rr[4] = {rs.x, rs.y, rs.z, rs.w};
+  uint32_t ov[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float lo = to_f<DT>(vv[e] & 0xFFFFu) + to_f<DT>(aa[e] & 0xFFFFu) + to_f<DT>(rr[e] & 0xFFFFu);
+    float hi = to_f<DT>(vv[e] >> 16) + to_f<DT>(aa[e] >> 16) + to_f<DT>(rr[e] >> 16);
+    if (a.relu && a.res) {
+      lo = fmaxf(lo, 0.f);
+      hi = fmaxf(hi, 0.f);
+    }
+    ov[e] = pack2<DT>(lo, hi);
+  }
+  return uint4{ov[0], ov[1], ov[2], ov[3]};
+}
+
+// a row's last partial chunk (OC % 8): element-wise, no 16-B access past OC
+template <int DT>
+__device__ __forceinline__ void epi_tail(const ConvArgs& a, uint4 v, int grow, int gcol, long long o) {
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+  if (!DV_BOUNDS(o, a.OC - gcol, a.out_elems, "conv_dma epilogue tail out")) return;
+  const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+  for (int e = 0; e < a.OC - gcol; ++e) {
+    float f = to_f<DT>((vv[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+    if (a.accumulate) f += to_f<DT>(out[o + e]);
+    if (a.res) {
+      f += to_f<DT>(a.res[(long long)grow * a.res_ld + gcol + e]);
+      if (relu_at(a, gcol + e)) f = fmaxf(f, 0.f);
+    }
+    if (a.emask) {
+      const uint32_t m = a.emask[(long long)grow * a.emask_ld + gcol + e];
+      if (m == 0u || (m & 0x8000u)) f = 0.f;
+    }
+    out[o + e] = from_f<DT>(f);
+  }
+}
+
 // LDS-staged 16-bit epilogue. The MFMA C layout gives each lane 4 rows x 1 column per 16x16
 // block, i.e. 2-byte scattered stores; instead the tile is written to LDS (the freed operand
 // stages, 16-B chunks XOR-swizzled by row) and read back as 8-channel chunks: every global
@@ -560,6 +599,57 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
   __syncthreads();
   uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
   const bool post = a.accumulate || a.res != nullptr;
+  // Batched operand loads: with residual / accumulate / output-mask operands, each thread first
+  // issues the loads of ALL its (<= 8) chunks, then combines and stores, so the chunks' HBM round
+  // trips overlap instead of serializing once per loop iteration. Fully unrolled with constant
+  // indices (the operand arrays stay in VGPRs; the C tile is already in LDS, acc is dead here).
+  // The short-K GEMMs with such epilogues (ResNet block convs and dgrads, K = 64..576) are
+  // epilogue-latency bound. DV_NO_EPI_BATCH=1 (host) falls back to the per-chunk loop (A/B).
+  constexpr int ITER = (BM * CPR + NT - 1) / NT;
+  if constexpr (ITER <= 8) {
+    if (a.epi_batch && a.ucode == nullptr && (post || a.emask != nullptr)) {
+      uint4 rv[ITER], av[ITER], mv[ITER];
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        rv[it] = av[it] = mv[it] = uint4{0u, 0u, 0u, 0u};
+        const int c = tid + it * NT;
+        const int row = c / CPR, cc = c % CPR;
+        const int grow = m0 + row, gcol = n0 + cc * 8;
+        if (c >= BM * CPR || grow >= a.M || gcol + 8 > a.OC) continue;
+        const long long o = (long long)grow * a.out_ld + gcol;
+        if (a.accumulate && DV_BOUNDS(o, 8, a.out_elems, "conv_dma epilogue_lds acc load"))
+          av[it] = *reinterpret_cast<const uint4*>(out + o);
+        if (a.res && DV_BOUNDS((long long)grow * a.res_ld + gcol, 8, a.res_elems, "conv_dma epilogue_lds res load"))
+          rv[it] = *reinterpret_cast<const uint4*>(a.res + (long long)grow * a.res_ld + gcol);
+        if (a.emask &&
+            DV_BOUNDS((long long)grow * a.emask_ld + gcol, 8, a.emask_elems, "conv_dma epilogue_lds emask load"))
+          mv[it] = *reinterpret_cast<const uint4*>(a.emask + (long long)grow * a.emask_ld + gcol);
+      }
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int c = tid + it * NT;
+        const int row = c / CPR, cc = c % CPR;
+        const int grow = m0 + row, gcol = n0 + cc * 8;
+        if (c >= BM * CPR || grow >= a.M || gcol >= a.OC) continue;
+        uint4 v = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((cc ^ (row & SWZ)) << 4));
+        const long long o = (long long)grow * a.out_ld + gcol;
+        if (gcol + 8 > a.OC) {
+          epi_tail<DT>(a, v, grow, gcol, o);
+          continue;
+        }
+        if (!DV_BOUNDS(o, 8, a.out_elems, "conv_dma epilogue_lds out")) continue;
+        if (post) v = epi_combine<DT>(a, v, av[it], rv[it]);
+        if (a.emask) {
+          v.x = mask_pos_pk(v.x, mv[it].x);
+          v.y = mask_pos_pk(v.y, mv[it].y);
+          v.z = mask_pos_pk(v.z, mv[it].z);
+          v.w = mask_pos_pk(v.w, mv[it].w);
+        }
+        *reinterpret_cast<uint4*>(out + o) = v;
+      }
+      return;
+    }
+  }
   for (int c = tid; c < BM * CPR; c += NT) {
     const int row = c / CPR, cc = c % CPR;
     const int grow = m0 + row, gcol = n0 + cc * 8;

@@ -46,6 +46,7 @@ struct ConvArgs {
   const uint16_t* emask;  // optional (16-bit out): out = 0 where emask <= 0 (same layout as out)
   long long emask_ld;
   int vec_epi;            // host-checked: 16-bit out/res/emask rows 16-B aligned -> LDS-staged epilogue
+  int epi_batch;          // LDS-staged epilogue: load every chunk's res/acc/emask operands up front
   float* ws;              // split-K: fp32 partials [ksplit][M][OCpad] (LDS-DMA kernel), else nullptr
   int ksplit;
   double* stats;          // optional (row-streaming kernel): stats[n / stats_div] += {sum out, sum out^2}
