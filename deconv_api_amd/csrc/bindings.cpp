@@ -222,7 +222,8 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   }
   // first layer (8-channel padded RGB image -> 64 channels): row-streaming, output-write bound
   if (epi == dv::CONV_E_BF16 && amode == dv::CONV_A_FWD && (impl == 0 || impl == 3) && a.C == 8 && !a.ucode &&
-      a.H * a.W >= 56 * 56 && !mask.has_value() && std::getenv("DV_NO_C8_STREAM") == nullptr) {
+      !a.res && !a.emask && a.relu_cols <= 0 && a.H * a.W >= 56 * 56 && !mask.has_value() &&
+      std::getenv("DV_NO_C8_STREAM") == nullptr) {
     const int rc = dv::conv3x3_c8_stream_launch(a, cur_stream());
     if (rc >= 0) {
       check_rc(rc, "conv_c8_stream");
@@ -286,11 +287,15 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       a.x_ld = a.C;
       a.relu_in = 0;
     }
-    // 3x3 s1 p1 convs with 64/128 output channels at large maps: halo-stream kernel (every input
-    // pixel fetched once per 32-channel chunk instead of once per tap)
+    // A/B switches: DV_HS_EMASK_OFF (masked dgrads back on the DMA kernel), DV_HS_PAD_OFF (pad != 1)
+    static const bool hs_emask_off = std::getenv("DV_HS_EMASK_OFF") != nullptr;
+    static const bool hs_pad_off = std::getenv("DV_HS_PAD_OFF") != nullptr;
+    // 3x3 s1 convs (pad 0..2) with 64/128 padded output channels at large maps: halo-stream kernel
+    // (every input pixel fetched once per 32-channel chunk instead of once per tap); also the ReLU-
+    // masked (emask) input gradients of such convs (InceptionV3 stem / ResNet 3x3 dgrads)
     if (impl == 0 && amode == dv::CONV_A_FWD && (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_POOL) &&
-        !mask.has_value() && !a.res && !a.emask && !a.ucode && !a.accumulate && (int64_t)a.H * a.W >= 64 * 64 &&
-        a.W >= 64) {
+        !mask.has_value() && !a.res && !a.ucode && !a.accumulate && a.relu_cols <= 0 &&
+        (int64_t)a.H * a.W >= 64 * 64 && a.W >= 64 && (!a.emask || !hs_emask_off) && (a.pad_h == 1 || !hs_pad_off)) {
       const int rc = dv::conv3x3_hs_launch(a, (int)epi, cur_stream());
       if (rc >= 0) {
         check_rc(rc, "conv_halo_stream");

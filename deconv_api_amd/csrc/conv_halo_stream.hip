@@ -87,9 +87,14 @@ __device__ __forceinline__ f32x16 hs_mfma(const typename Vec8<DT>::type& a, cons
 
 }  // namespace
 
-// OCT: output channels per workgroup (= OCpad, 64 or 128); POOL: fused 2x2 max-pool + switch epilogue
-template <int DT, int OCT, bool POOL, int RING>
-__global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+// OCT: output channels per workgroup (= OCpad, 64 or 128); POOL: fused 2x2 max-pool + switch epilogue.
+// Any symmetric pad (0: 'valid', 1: 'same', 2: the full-pad input gradient of a 'valid' conv): the
+// halo of output tile (ty0, tx0) starts at input (ty0 - pad, tx0 - pad); output OH x OW.
+// NB1 (one 32-channel chunk, C == 32): ONE halo buffer (72 KiB of LDS -> 2 workgroups per CU; with a
+// single chunk there is no next-chunk prefetch to double-buffer).
+// emask (non-pool): the output is zeroed where emask <= 0 (an input gradient masked by its ReLU).
+template <int DT, int OCT, bool POOL, int RING, bool NB1 = false>
+__global__ void __launch_bounds__(512, NB1 && OCT == 64 ? 4 : 1) conv3x3_hs_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
   constexpr int FN = OCT / 32;  // 32-channel A blocks per wave
   // weights of one step: OCT rows x 80 B. OCT = 128: 10 KiB = one 1-KiB dwordx4 DMA + one 256-B dword
   // DMA per wave (exact); OCT = 64: 5 KiB in one dwordx4 DMA per wave, 3 of them out-of-range dummies
@@ -98,9 +103,10 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
   constexpr int LA = RING - 1;                    // B(k + RING - 1) is issued at step k
   constexpr int STEPS_PER_CHUNK = 9;
   typedef typename Vec8<DT>::type v8;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * HS_HBUF + RING * BSLOT];
+  constexpr int NHB = NB1 ? 1 : 2;  // halo buffers
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NHB * HS_HBUF + RING * BSLOT];
   uint8_t* halo = smem;
-  uint8_t* ring = smem + 2 * HS_HBUF;
+  uint8_t* ring = smem + NHB * HS_HBUF;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -123,7 +129,7 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
     const int s = (u * 8 + wave) * 64 + lane;
     const int p = s / 5, q = s - 5 * (s / 5);
     const int hy = p / HS_HW, hx = p - HS_HW * (p / HS_HW);
-    const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+    const int y = ty0 - a.pad_h + hy, x = tx0 - a.pad_w + hx;
     const bool ok = q < 4 && p < HS_HH * HS_HW && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
     hoff[u] = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + q * 8) * 2) : HS_OOB;
   }
@@ -172,16 +178,16 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
 #pragma unroll
   for (int p = 0; p < LA; ++p) issue_w(p);
   for (int c = 0; c < nch; ++c) {
-    const uint8_t* hb = halo + (c & 1) * HS_HBUF + prow;
+    const uint8_t* hb = halo + (NB1 ? 0 : (c & 1)) * HS_HBUF + prow;
 #pragma unroll
     for (int t = 0; t < STEPS_PER_CHUNK; ++t) {
       const int k = c * STEPS_PER_CHUNK + t;
-      // younger than B(k): the B's of steps k-LA+1 .. k-1 (or of the prologue), plus halo(c) when
-      // step 9c lies in that window (1 <= t <= LA-1)
-      if (t >= 1 && t <= LA - 1) hs_wait<(LA - 1) * BI + HS_HI>();
+      // younger than B(k): the B's of steps k-LA+1 .. k-1 (or of the prologue), plus halo(c+1) when
+      // step 9c lies in that window (1 <= t <= LA-1; NB1 issues no next-chunk halo)
+      if (!NB1 && t >= 1 && t <= LA - 1) hs_wait<(LA - 1) * BI + HS_HI>();
       else hs_wait<(LA - 1) * BI>();
       __builtin_amdgcn_s_barrier();
-      if (t == 0) issue_halo(c + 1, (c + 1) & 1);
+      if (!NB1 && t == 0) issue_halo(c + 1, (c + 1) & 1);
       issue_w(k + LA);
       const uint8_t* wb = ring + (k % RING) * BSLOT + wrow;
       const int kh = t / 3, kw = t % 3;
@@ -205,7 +211,7 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
   // epilogue: lane = pixel (tile row 2*wave + i, column px); register r of block j = output channel
   // 32j + 8(r >> 2) + 4h + (r & 3): 4 consecutive channels -> one 8-B store
   const int ox = tx0 + px;
-  if (ox >= W) return;
+  if (ox >= a.OW) return;
   // the lane's bias values (the same for both pixel rows), all loads in flight together
   float4 bv[FN][4];
 #pragma unroll
@@ -268,8 +274,21 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int oy = ty0 + 2 * wave + i;
-    if (oy >= H) continue;
-    uint16_t* orow = out + (((long long)n * H + oy) * W + ox) * a.out_ld;
+    if (oy >= a.OH) continue;
+    const long long pix = ((long long)n * a.OH + oy) * a.OW + ox;
+    uint16_t* orow = out + pix * a.out_ld;
+    // output mask of this pixel row: every 8-B quad loaded before the row's first store
+    uint2 em[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int oc = 32 * j + 8 * g + 4 * h;
+        em[j][g] = make_uint2(0x3C003C00u, 0x3C003C00u);  // any > 0
+        if (a.emask && oc + 4 <= a.OC &&
+            DV_BOUNDS(pix * a.emask_ld + oc, 4, a.emask_elems, "halo-stream emask"))
+          em[j][g] = *reinterpret_cast<const uint2*>(a.emask + pix * a.emask_ld + oc);
+      }
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -280,10 +299,19 @@ __global__ void __launch_bounds__(512) conv3x3_hs_kernel(const ConvArgs a, int t
         const float v2 = fmaxf(acc[i][j][4 * g + 2] + bv[j][g].z, lo);
         const float v3 = fmaxf(acc[i][j][4 * g + 3] + bv[j][g].w, lo);
         if (oc + 4 <= a.OC) {
-          *reinterpret_cast<uint2*>(orow + oc) = make_uint2(pack2<DT>(v0, v1), pack2<DT>(v2, v3));
+          if (DV_BOUNDS(pix * a.out_ld + oc, 4, a.out_elems, "halo-stream out"))
+            *reinterpret_cast<uint2*>(orow + oc) = make_uint2(mask_pos_pk(pack2<DT>(v0, v1), em[j][g].x),
+                                                              mask_pos_pk(pack2<DT>(v2, v3), em[j][g].y));
         } else if (oc < a.OC) {  // OC % 4 tail (never for VGG16)
           const float v[4] = {v0, v1, v2, v3};
-          for (int r = 0; r < a.OC - oc; ++r) orow[oc + r] = from_f<DT>(v[r]);
+          for (int r = 0; r < a.OC - oc; ++r) {
+            float f = v[r];
+            if (a.emask) {
+              const uint32_t m = a.emask[pix * a.emask_ld + oc + r];
+              if (m == 0u || (m & 0x8000u)) f = 0.f;
+            }
+            orow[oc + r] = from_f<DT>(f);
+          }
         }
       }
   }
@@ -375,7 +403,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
       const int s = (u * 4 + wave) * 64 + lane;
       const int p = s >> 2, ch = (s & 3) ^ h16_swz(s >> 2);
       const int hy = p / H16_HW, hx = p - H16_HW * (p / H16_HW);
-      const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+      const int y = ty0 - a.pad_h + hy, x = tx0 - a.pad_w + hx;
       const bool ok = p < H16_HW * H16_HW && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
       hoff[u] = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + ch * 8) * 2) : HS_OOB;
     }
@@ -553,15 +581,26 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int oy = ty0 + 4 * wave + i;
-    uint16_t* orow = out + (((long long)n * H + oy) * W + ox) * a.out_ld;
+    const long long pix = ((long long)n * a.OH + oy) * a.OW + ox;
+    uint16_t* orow = out + pix * a.out_ld;
+    // output mask (emask: an input gradient zeroed where its ReLU input was <= 0), row loaded up front
+    uint2 em[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int oc = 16 * j + 4 * q;
+      em[j] = make_uint2(0x3C003C00u, 0x3C003C00u);  // any > 0
+      if (a.emask && oc < a.OC && DV_BOUNDS(pix * a.emask_ld + oc, 4, a.emask_elems, "hs16 emask"))
+        em[j] = *reinterpret_cast<const uint2*>(a.emask + pix * a.emask_ld + oc);
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int oc = 16 * j + 4 * q;
       if (oc >= a.OC) continue;
       const float v0 = fmaxf(acc[i][j][0] + bv[j].x, lo), v1 = fmaxf(acc[i][j][1] + bv[j].y, lo);
       const float v2 = fmaxf(acc[i][j][2] + bv[j].z, lo), v3 = fmaxf(acc[i][j][3] + bv[j].w, lo);
-      if (DV_BOUNDS((((long long)n * H + oy) * W + ox) * a.out_ld + oc, 4, a.out_elems, "hs16 out"))
-        *reinterpret_cast<uint2*>(orow + oc) = make_uint2(pack2<DT>(v0, v1), pack2<DT>(v2, v3));
+      if (DV_BOUNDS(pix * a.out_ld + oc, 4, a.out_elems, "hs16 out"))
+        *reinterpret_cast<uint2*>(orow + oc) =
+            make_uint2(mask_pos_pk(pack2<DT>(v0, v1), em[j].x), mask_pos_pk(pack2<DT>(v2, v3), em[j].y));
     }
   }
 }
@@ -588,21 +627,24 @@ static int hs_ring() {
 
 int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
   if (std::getenv("DV_NO_HS") != nullptr) return -4;
-  if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH || a.W != a.OW ||
-      a.C % 32 != 0 || a.x_ld % 8 != 0 || (a.OCpad != 64 && a.OCpad != 128) || a.relu_in || a.accumulate ||
-      a.mask || a.code || a.res || a.emask || a.ws || a.stats || a.out_ld % 4 != 0 ||
+  // 3x3 / stride 1, symmetric pad 0..2 (output = input + 2 pad - 2)
+  const bool geom = a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad_h == a.pad_w && a.pad_h >= 0 && a.pad_h <= 2 &&
+                    a.OH == a.H + 2 * a.pad_h - 2 && a.OW == a.W + 2 * a.pad_w - 2 && a.OH > 0 && a.OW > 0;
+  if (!geom || a.C % 32 != 0 || a.x_ld % 8 != 0 || (a.OCpad != 64 && a.OCpad != 128) || a.relu_in || a.accumulate ||
+      a.mask || a.code || a.res || a.ws || a.stats || a.ucode || a.relu_cols > 0 || a.out_ld % 4 != 0 ||
       (reinterpret_cast<uintptr_t>(a.out) & 7) || (reinterpret_cast<uintptr_t>(a.x) & 15) ||
       (reinterpret_cast<uintptr_t>(a.bias) & 15) ||
+      (a.emask && (a.emask_ld % 4 != 0 || (reinterpret_cast<uintptr_t>(a.emask) & 7))) ||
       (long long)a.Kpad < 9LL * a.C || (long long)a.H * a.W * a.x_ld * 2 > 0x7FFFFFF0LL)
     return -4;
   const bool pool = epi == CONV_E_POOL;
   if (!pool && epi != CONV_E_BF16) return -4;
-  if (pool && (a.H % 2 || a.W % 2 || a.out_code == nullptr || a.OC % 4 || a.dtype != DT_BF16 ||
-               (reinterpret_cast<uintptr_t>(a.out_code) & 3)))
+  if (pool && (a.pad_h != 1 || a.emask || a.H % 2 || a.W % 2 || a.out_code == nullptr || a.OC % 4 ||
+               a.dtype != DT_BF16 || (reinterpret_cast<uintptr_t>(a.out_code) & 3)))
     return -4;
-  // exact 16 x 16 tiling (OC % 4 == 0: whole 8-B channel quads) -> hs16
-  if (a.H % 16 == 0 && a.W % 16 == 0 && a.OC % 4 == 0 && std::getenv("DV_NO_HS16") == nullptr) {
-    const int t16x = a.W / 16, t16y = a.H / 16;
+  // exact 16 x 16 tiling of the output (OC % 4 == 0: whole 8-B channel quads) -> hs16
+  if (a.OH % 16 == 0 && a.OW % 16 == 0 && a.OC % 4 == 0 && std::getenv("DV_NO_HS16") == nullptr) {
+    const int t16x = a.OW / 16, t16y = a.OH / 16;
     const long long n16 = (long long)a.N * t16x * t16y;
     if (n16 <= 0 || n16 > 0x7fffffffLL) return -2;
     const dim3 g16((unsigned)n16), b16(256);
@@ -620,7 +662,7 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
 #undef HS16
     return (int)hipGetLastError();
   }
-  const int tx = (a.W + HS_TW - 1) / HS_TW, ty = (a.H + HS_TH - 1) / HS_TH;
+  const int tx = (a.OW + HS_TW - 1) / HS_TW, ty = (a.OH + HS_TH - 1) / HS_TH;
   const long long nwg = (long long)a.N * tx * ty;
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
   const dim3 grid((unsigned)nwg), block(512);
@@ -628,6 +670,9 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
   if (pool) {
     if (a.OCpad == 128) HS_LAUNCH(DT_BF16, 128, true);
     else HS_LAUNCH(DT_BF16, 64, true);
+  } else if (a.C == 32 && a.OCpad == 64) {  // one channel chunk: single halo buffer, 2 workgroups per CU
+    if (a.dtype == DT_F16) hipLaunchKernelGGL((conv3x3_hs_kernel<DT_F16, 64, false, 3, true>), grid, block, 0, s, a, tx, ty);
+    else hipLaunchKernelGGL((conv3x3_hs_kernel<DT_BF16, 64, false, 3, true>), grid, block, 0, s, a, tx, ty);
   } else if (a.dtype == DT_F16) {
     if (a.OCpad == 128) HS_LAUNCH(DT_F16, 128, false);
     else HS_LAUNCH(DT_F16, 64, false);

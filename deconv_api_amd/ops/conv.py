@@ -354,7 +354,10 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
     geom = [N, H, W, C, OH, OW, OC, cw.OCpad, cw.KH, cw.KW, stride, pad[0], pad[1], cw.K, cw.Kpad, M,
             int(relu), int(relu_in), int(accumulate), int(code_div), x_ld, mask_ld, out_ld]
     bias = cw.bias_pad if use_bias else None
-    dma_only = res is not None or emask is not None or unpool_out is not None or relu_cols > 0
+    # res / unpool_out / relu_cols exist on the LDS-DMA kernel only; emask also on the halo-stream
+    # kernels (the binding routes by shape under 'auto')
+    dma_only = res is not None or unpool_out is not None or relu_cols > 0 or \
+        (emask is not None and _policy["impl"] not in ("auto",))
     lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
              IMPL["dma"] if dma_only else IMPL[_policy["impl"]],  # DMA-only epilogue features
              res, emask, stats, stats_div, unpool_out, unpool_div, relu_cols)

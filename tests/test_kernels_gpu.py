@@ -711,3 +711,37 @@ def test_dense_layers_as_mfma_gemm(native_lib):
         rg, rc = gpu.backward(sg, idx).cpu(), cpu.backward(sc, idx.cpu())
         a, b = rg.double().flatten(), rc.double().flatten()
         assert float(a @ b / (a.norm() * b.norm() + 1e-30)) > 0.98, layer
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C,OC,H,W,pad,use_emask", [
+    (32, 32, 75, 75, 0, False),   # InceptionV3 conv2d_2 forward ('valid'), one channel chunk (NB1)
+    (32, 32, 73, 73, 2, True),    # its input gradient: full pad, ReLU-masked output
+    (64, 32, 73, 71, 1, True),    # conv2d_3 input gradient (64 -> 32), ragged tiles
+    (32, 64, 73, 73, 1, False),   # conv2d_3 forward
+    (64, 64, 64, 64, 1, True),    # hs16 (16-multiple output) with an output mask
+    (64, 128, 66, 66, 0, False),  # hs16, 'valid' (64 x 64 output)
+    (96, 96, 70, 67, 1, True),    # OC 96 -> 128-channel tile, 3 chunks, ragged
+])
+def test_conv_halo_stream_pad_emask(native_lib, monkeypatch, dt, C, OC, H, W, pad, use_emask):
+    """Halo-stream 3x3 kernels with pad 0/1/2 (output H + 2 pad - 2), ragged tiles and the emask
+    epilogue (ReLU-masked input gradients) against the fp32 reference and the LDS-DMA kernel."""
+    g = torch.Generator().manual_seed(C * 3 + OC + H + pad)
+    r = lambda t: t.to(dt).float()  # noqa: E731
+    N = 2
+    x = r(torch.randn(N, H, W, C, generator=g))
+    cw = ConvWeights(r(torch.randn(OC, C, 3, 3, generator=g) / np.sqrt(9 * C)), r(torch.randn(OC, generator=g)), "fwd")
+    OH, OW = H + 2 * pad - 2, W + 2 * pad - 2
+    em = r(torch.randn(N, OH, OW, OC, generator=g)) if use_emask else None
+    relu = not use_emask
+    ref = ops.conv2d(x, cw, pad=pad, relu=relu, emask=em)
+    assert ref.shape == (N, OH, OW, OC)
+    dw = cw.to_device(DEV, dt)
+    emd = em.to(dt).to(DEV) if use_emask else None
+    got = ops.conv2d(x.to(dt).to(DEV), dw, pad=pad, relu=relu, emask=emd)
+    assert got.dtype == dt and _rel(got, ref) < 1e-2
+    if use_emask:
+        assert bool(((got.float().cpu() != 0) & (em <= 0)).sum() == 0)
+    monkeypatch.setenv("DV_NO_HS", "1")
+    dma = ops.conv2d(x.to(dt).to(DEV), dw, pad=pad, relu=relu, emask=emd)
+    assert _rel(dma, ref) < 1e-2

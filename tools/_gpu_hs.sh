@@ -1,6 +1,9 @@
+# halo-stream pad/emask generalization: kernel tests, deepdream tests, configs 2/3/5 with A/B
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "halo_stream or relu_in or large_m or unpool" -x -q --timeout 120 --timeout-method thread > gpurun_out/t_hs.log 2>&1 || exit 1
-DV_NO_HSU=1 timeout -k 10 120 python tools/profile_layers.py > gpurun_out/layers_hsu_off.txt 2>&1 || exit 1
-timeout -k 10 120 python tools/profile_layers.py > gpurun_out/layers_hsu_on.txt 2>&1 || exit 1
-timeout -k 10 100 python bench.py > gpurun_out/bench_hs.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_deepdream.py -m gpu > gpurun_out/hs_tests.log 2>&1 || exit 1
+timeout -k 10 200 python -u bench_dream.py --model inception_v3 --batch 64 --size 299 > gpurun_out/hs_c3_on.log 2>&1 || exit 1
+DV_HS_EMASK_OFF=1 DV_HS_PAD_OFF=1 timeout -k 10 200 python -u bench_dream.py --model inception_v3 --batch 64 --size 299 > gpurun_out/hs_c3_off.log 2>&1 || exit 1
+timeout -k 10 200 python -u bench_dream.py --model resnet50 --size 1024 --tile 512 --dtype fp16 --batch 8 > gpurun_out/hs_c5_on.log 2>&1 || exit 1
+DV_HS_EMASK_OFF=1 timeout -k 10 200 python -u bench_dream.py --model resnet50 --size 1024 --tile 512 --dtype fp16 --batch 8 > gpurun_out/hs_c5_off.log 2>&1 || exit 1
+timeout -k 10 120 python -u bench.py > gpurun_out/hs_c2.log 2>&1
