@@ -307,8 +307,8 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     const int64_t imgs_per_tile = 512 / std::max(1, a.OH * a.OW) + 2;
     TORCH_CHECK((int64_t)a.H * a.W * a.x_ld * 2 * imgs_per_tile < 0x7FFFFFF0LL, "conv dma: image too large");
     // split-K when the tile grid would leave most CUs idle (plain epilogues only)
-    const bool plain_epi =
-        (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && !a.accumulate && !a.res && !a.emask && !a.ucode;
+    // (the reduce kernel applies bias / ReLU / accumulate / residual / emask; not the unpool scatter)
+    const bool plain_epi = (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && !a.ucode;
     const int ks = plain_epi ? dv::conv_dma_splitk(a) : 1;
     Tensor ws;
     if (ks > 1) {

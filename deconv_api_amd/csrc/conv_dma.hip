@@ -15,14 +15,27 @@ void conv_dma_tune(int cfg, int ks) {
 
 // Split-K factor for a launch that would leave most CUs idle: small M (batch-1 serving, deep
 // layers of strong-scaled DeepDream tiles, dense layers) with a long K. 1 = no split.
+// The small-problem 64x64 tiles (auto_cfg 8: DeepDream's small octaves, replayed from hipGraphs)
+// split a long K into 2 / 4 parts: in a graph the extra reduce launch costs ~2 us while each K
+// tile of the serial K loop costs ~0.4 us (tools/small_conv_latency.py: M 1600 x N 160 x K 1440
+// 14.8 -> 11.4 us, M 4096 x N 96 x K 2592 23.3 -> 15.2 us; K <= 768 gains nothing).
 int conv_dma_splitk(const ConvArgs& a) {
   if (g_ks > 0) return std::min(g_ks, a.Kpad / 64);
-  if (std::getenv("DV_NO_SPLITK")) return 1;
-  if (g_cfg == 0 && auto_cfg(a) == 8) return 1;
+  static const bool off = std::getenv("DV_NO_SPLITK") != nullptr;
+  static const bool small_off = std::getenv("DV_NO_SMALL_SPLITK") != nullptr;
+  if (off) return 1;
+  const int nk = a.Kpad / 64;
+  if (g_cfg == 0 && auto_cfg(a) == 8) {
+    // only the smallest problems: the reduce pass re-reads ks x M x OCpad fp32 partials, which
+    // outweighs the shorter K loop once M x OCpad grows (full-model A/B, docs/KERNELS.md)
+    static const long long mn_max =
+        std::getenv("DV_SMALL_SPLITK_MN") ? std::atoll(std::getenv("DV_SMALL_SPLITK_MN")) : 300000LL;
+    if (small_off || (long long)a.M * a.OCpad > mn_max) return 1;
+    return nk >= 20 ? 4 : (nk >= 16 ? 2 : 1);
+  }
   int BM, BN;
   dma_tile_dims(a, a.mask != nullptr, BM, BN);
   const long long nwg = (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN);
-  const int nk = a.Kpad / 64;
   const long long cus = num_cus();
   if (nwg * 2 > cus || nk < 8) return 1;
   long long k = (cus + nwg - 1) / nwg;  // about one workgroup per CU
@@ -31,7 +44,9 @@ int conv_dma_splitk(const ConvArgs& a) {
   return k < 2 ? 1 : (int)k;
 }
 
-// out = act(sum_s ws[s] + bias): the split-K epilogue (16-bit or fp32 output, row stride out_ld)
+// The split-K epilogue: out = act(sum_s ws[s] + bias) with the kernel epilogue's full semantics
+// (16-bit or fp32 output of row stride out_ld): v = sum + bias, [ReLU] (before an accumulate /
+// residual add), += out (accumulate), += res then [ReLU], zeroed where emask <= 0.
 template <int DT>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a, int epi) {
   const long long total = (long long)a.M * a.OC;
@@ -41,13 +56,26 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a, in
     const float* w = a.ws + (long long)row * a.OCpad + col;
     float v = a.bias ? a.bias[col] : 0.f;
     for (int k = 0; k < a.ksplit; ++k) v += w[k * plane];
-    if (relu_at(a, col)) v = fmaxf(v, 0.f);
+    if (relu_at(a, col) && !a.res) v = fmaxf(v, 0.f);
     const long long o = (long long)row * a.out_ld + col;
     if (!DV_BOUNDS(o, 1, a.out_elems, "splitk_reduce out")) continue;
-    if (epi == CONV_E_F32)
-      reinterpret_cast<float*>(a.out)[o] = v;
-    else
-      reinterpret_cast<uint16_t*>(a.out)[o] = from_f<DT>(v);
+    if (epi == CONV_E_F32) {
+      float* out = reinterpret_cast<float*>(a.out);
+      if (a.accumulate) v += out[o];
+      out[o] = v;
+      continue;
+    }
+    uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+    if (a.accumulate) v += to_f<DT>(out[o]);
+    if (a.res) {
+      v += to_f<DT>(a.res[(long long)row * a.res_ld + col]);
+      if (relu_at(a, col)) v = fmaxf(v, 0.f);
+    }
+    if (a.emask) {
+      const uint32_t m = a.emask[(long long)row * a.emask_ld + col];
+      if (m == 0u || (m & 0x8000u)) v = 0.f;
+    }
+    out[o] = from_f<DT>(v);
   }
 }
 

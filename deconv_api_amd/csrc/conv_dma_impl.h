@@ -204,25 +204,34 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
     r_base[j] = m ? (int)(((long long)r_off[j] + (long long)r_h[j] * W + r_w[j]) * a.x_ld) : 0;
   }
 
+  // K decomposition (tap = (kh, kw), channel) of the NEXT tile to issue, advanced incrementally:
+  // issue() runs for kt = k_first, k_first + 1, ... in order, so one division pair up front replaces
+  // the two integer divisions per K tile (~40 scalar/vector instructions of a ~150-instruction K step
+  // that bounds the latency of the small, few-workgroup GEMMs). CALIGNED: wave-uniform tile base;
+  // otherwise per lane (its 8-channel chunk may sit in a later tap than the tile's first element).
+  int nk_tap, nk_kh, nk_kw, nk_ch, nk_k;
+  auto k_init = [&](int kt) {
+    nk_k = kt * BK + (CALIGNED ? 0 : lchunk * 8);
+    nk_tap = nk_k / C;
+    nk_kh = nk_tap / a.KW;
+    nk_kw = nk_tap - nk_kh * a.KW;
+    nk_ch = nk_k - nk_tap * C;
+  };
   auto issue = [&](int kt, int buf) {
     uint8_t* As = smem + buf * STAGE;
     uint8_t* Bs = As + A_BYTES + M_BYTES;
-    int kh, kw, ch, tap;
-    bool kval;
-    if constexpr (CALIGNED) {
-      const int k0 = kt * BK;
-      tap = k0 / C;  // wave-uniform
-      kh = tap / a.KW;
-      kw = tap - kh * a.KW;
-      ch = k0 - tap * C + lchunk * 8;
-      kval = tap < a.KH * a.KW;
-    } else {
-      const int k = kt * BK + lchunk * 8;
-      tap = k / C;
-      kh = tap / a.KW;
-      kw = tap - kh * a.KW;
-      ch = k - tap * C;
-      kval = k < a.K;
+    const int tap = nk_tap, kh = nk_kh, kw = nk_kw;
+    const int ch = nk_ch + (CALIGNED ? lchunk * 8 : 0);
+    const bool kval = CALIGNED ? tap < a.KH * a.KW : nk_k < a.K;
+    nk_k += BK;
+    nk_ch += BK;
+    while (nk_ch >= C) {  // CALIGNED: exactly one wrap per C / BK tiles; else <= BK / C + 1 wraps
+      nk_ch -= C;
+      ++nk_tap;
+      if (++nk_kw == a.KW) {
+        nk_kw = 0;
+        ++nk_kh;
+      }
     }
     if (FAST && fast) {
       const int delta = (kh * W + kw) * (int)a.x_ld + ch;
@@ -294,6 +303,7 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
   const int nk_all = a.Kpad / BK;
   const int k0 = (int)(((long long)nk_all * blockIdx.y) / gridDim.y);
   const int nk = (int)(((long long)nk_all * (blockIdx.y + 1)) / gridDim.y) - k0;
+  k_init(k0);
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
     if (p < nk) issue(k0 + p, p);
@@ -1031,7 +1041,10 @@ static int auto_cfg(const ConvArgs& a) {
   static const bool off = std::getenv("DV_NO_AUTO_CFG") != nullptr;  // A/B: the size-based choice only
   if (a.mask != nullptr || off) return 0;
   const long long mn = (long long)a.M * a.OCpad;
-  if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= 256) return 8;
+  // (short K too: M 1600 x N 64 x K 64 4.2 vs 6.0 us for the size-based 256 x 64 tile in a graph,
+  // tools/small_conv_latency.py; DV_SMALL_TILE_KMIN=256 restores the round-1 rule)
+  static const int kmin = std::getenv("DV_SMALL_TILE_KMIN") ? std::atoi(std::getenv("DV_SMALL_TILE_KMIN")) : 0;
+  if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= kmin) return 8;
   if (a.OCpad % 128 == 0 && a.OC > 64 && a.Kpad < 4096 && (a.Kpad < 1024 || mn < 50000000LL)) return 3;
   return 0;
 }

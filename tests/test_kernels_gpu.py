@@ -745,3 +745,38 @@ def test_conv_halo_stream_pad_emask(native_lib, monkeypatch, dt, C, OC, H, W, pa
     monkeypatch.setenv("DV_NO_HS", "1")
     dma = ops.conv2d(x.to(dt).to(DEV), dw, pad=pad, relu=relu, emask=emd)
     assert _rel(dma, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mode", ["emask", "accumulate", "res", "relu"])
+def test_conv_splitk_full_epilogue(native_lib, dt, mode):
+    """Split-K partials + the reduce kernel with the full epilogue (emask / accumulate / residual /
+    ReLU), forced on the small-problem 64x64 tile (as DeepDream's small octaves run it)."""
+    g = torch.Generator().manual_seed(len(mode))
+    r = lambda t: t.to(dt).float()  # noqa: E731
+    N, H, C, OC = 4, 9, 160, 96
+    x = r(torch.randn(N, H, H, C, generator=g))
+    cw = ConvWeights(r(torch.randn(OC, C, 3, 3, generator=g) / np.sqrt(9 * C)), r(torch.randn(OC, generator=g)), "fwd")
+    em = r(torch.randn(N, H, H, OC, generator=g))
+    base = r(torch.randn(N, H, H, OC, generator=g))
+    kw = {"emask": dict(relu=False, emask=em), "accumulate": dict(relu=True), "res": dict(relu=True, res=base),
+          "relu": dict(relu=True)}[mode]
+    if mode == "accumulate":
+        ref = ops.conv2d(x, cw, relu=True) + base
+    else:
+        ref = ops.conv2d(x, cw, **kw)
+    dev_kw = {k: (v.to(dt).to(DEV) if torch.is_tensor(v) else v) for k, v in kw.items()}
+    lib = native_lib
+    for ks in (1, 2, 4):
+        lib.dma_tune(8, ks)
+        try:
+            if mode == "accumulate":
+                out = base.to(dt).to(DEV)
+                got = ops.conv2d(x.to(dt).to(DEV), cw.to_device(DEV, dt), out=out, accumulate=True, **dev_kw)
+            else:
+                got = ops.conv2d(x.to(dt).to(DEV), cw.to_device(DEV, dt), **dev_kw)
+        finally:
+            lib.dma_tune(0, 0)
+        assert _rel(got, ref) < 1e-2, (mode, ks)
+        if mode == "emask":
+            assert bool(((got.float().cpu() != 0) & (em <= 0)).sum() == 0)

@@ -1,0 +1,8 @@
+# incremental K decomposition: kernel tests, microbench, configs 3/5/2
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_deepdream.py -m gpu > gpurun_out/ki_tests.log 2>&1 || exit 1
+timeout -k 10 200 python -u tools/small_conv_latency.py > gpurun_out/ki_lat.log 2>&1 || exit 1
+timeout -k 10 200 python -u bench_dream.py --model inception_v3 --batch 64 --size 299 > gpurun_out/ki_c3.log 2>&1 || exit 1
+timeout -k 10 200 python -u bench_dream.py --model resnet50 --size 1024 --tile 512 --dtype fp16 --batch 8 > gpurun_out/ki_c5.log 2>&1 || exit 1
+timeout -k 10 120 python -u bench.py > gpurun_out/ki_c2.log 2>&1
