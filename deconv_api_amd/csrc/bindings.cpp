@@ -316,6 +316,14 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       a.ws = ws.data_ptr<float>();
       a.ksplit = ks;
     }
+    if (ks == 1 && (impl == 0 || impl == 2) && amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16 && !mask.has_value()) {
+      const int rc = dv::conv_pw_launch(a, cur_stream());  // large-M 1x1 convs: persistent pipeline
+      if (rc >= 0) {
+        check_rc(rc, "conv_pw");
+        finish_stats();
+        return;
+      }
+    }
     check_rc(dv::conv_dma_launch(a, (int)amode, (int)epi, cur_stream()), "conv_dma");
     if (ks > 1) check_rc(dv::splitk_reduce_launch(a, (int)epi, cur_stream()), "splitk_reduce");
   } else {

@@ -68,6 +68,9 @@ int conv_dma_splitk(const ConvArgs& a);
 // tuning override: force DMA tile config cfg (> 0, conv_dma.hip:dma_forced) and split-K ks (> 0); 0 = auto
 void conv_dma_tune(int cfg, int ks);
 int splitk_reduce_launch(const ConvArgs& a, int epi, hipStream_t stream);
+// persistent pointwise (1x1 / s1 / p0) conv at large M, 16-bit LDS-staged epilogue (conv_pw.hip);
+// < 0: unsupported shape / mode (use conv_dma_launch)
+int conv_pw_launch(const ConvArgs& a, hipStream_t stream);
 
 // ---- misc kernels (misc.hip) ----
 // per-(image, channel) sums of a NHWC bf16 tensor: sums[n][c] = sum_{hw} x[n][hw][c]

@@ -780,3 +780,46 @@ def test_conv_splitk_full_epilogue(native_lib, dt, mode):
         assert _rel(got, ref) < 1e-2, (mode, ks)
         if mode == "emask":
             assert bool(((got.float().cpu() != 0) & (em <= 0)).sum() == 0)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C,OC,mode", [(64, 256, "res"), (256, 64, "relu"), (64, 256, "emask"), (128, 512, "res_emask"),
+                                       (64, 96, "accumulate"), (192, 64, "relu_slice")])
+def test_conv_pointwise_persistent(native_lib, monkeypatch, dt, C, OC, mode):
+    """Persistent pointwise kernel (large-M 1x1 convs; tile sequence through one 2-stage LDS ring):
+    every epilogue mode against the fp32 reference and the one-tile-per-workgroup DMA kernel, with
+    an M tail (M % tile != 0) and a channel-slice input (x_ld > C)."""
+    g = torch.Generator().manual_seed(C + OC + len(mode))
+    r = lambda t: t.to(dt).float()  # noqa: E731
+    N, H, W = 2, 181, 183  # M = 66246: > 4 x 256 tiles of 128 x 128, ragged tail
+    ld = C + 64 if mode == "relu_slice" else C
+    xb = r(torch.randn(N, H, W, ld, generator=g))
+    x = xb[..., :C]
+    cw = ConvWeights(r(torch.randn(OC, C, 1, 1, generator=g) / np.sqrt(C)), r(torch.randn(OC, generator=g)), "fwd")
+    res = r(torch.randn(N, H, W, OC, generator=g))
+    em = r(torch.randn(N, H, W, OC, generator=g))
+    kw = {"res": dict(relu=True, res=res), "relu": dict(relu=True), "emask": dict(relu=False, emask=em),
+          "res_emask": dict(relu=True, res=res, emask=em), "accumulate": dict(relu=True),
+          "relu_slice": dict(relu=True)}[mode]
+    ref = ops.conv2d(x, cw, pad=0, **kw)
+    if mode == "accumulate":
+        ref = ref + res
+    dw = cw.to_device(DEV, dt)
+    xd = xb.to(dt).to(DEV)[..., :C]
+    dkw = {k: (v.to(dt).to(DEV) if torch.is_tensor(v) else v) for k, v in kw.items()}
+
+    def run():
+        if mode == "accumulate":
+            out = res.to(dt).to(DEV)
+            return ops.conv2d(xd, dw, pad=0, out=out, accumulate=True, **dkw)
+        return ops.conv2d(xd, dw, pad=0, **dkw)
+
+    got = run()
+    assert got.dtype == dt and _rel(got, ref) < 1e-2, mode
+    monkeypatch.setenv("DV_NO_PW", "1")  # read once per process: compare with a forced-tile DMA launch
+    native_lib.dma_tune(3 if OC > 64 else 5, 1)
+    try:
+        dma = run()
+    finally:
+        native_lib.dma_tune(0, 0)
+    assert _rel(got, dma) < 1e-2, mode
