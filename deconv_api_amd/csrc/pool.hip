@@ -17,17 +17,19 @@ struct PoolGeom {
   int relu;              // avgpool fwd: ReLU on the output
 };
 
-template <int DT>
+template <int DT, int KC, typename IT>
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeom g) {
   const int cpp = g.C >> 3;
-  const long long total = (long long)g.N * g.OH * g.OW * cpp;
-  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+  const int k = KC ? KC : g.k;
+  const IT total = (IT)g.N * g.OH * g.OW * cpp;
+  for (IT t = (IT)blockIdx.x * 256 + threadIdx.x; t < total; t += (IT)gridDim.x * 256) {
     const int ch = (int)(t % cpp);
-    const long long pix = t / cpp;
+    const IT pix = t / cpp;
     const int ow = (int)(pix % g.OW);
-    const int oh = (int)((pix / g.OW) % g.OH);
-    const long long n = pix / ((long long)g.OW * g.OH);
+    const IT pq = pix / g.OW;
+    const int oh = (int)(pq % g.OH);
+    const long long n = (long long)(pq / g.OH);
     float best[8];
     int bi[8];
 #pragma unroll
@@ -35,15 +37,22 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
       best[e] = -INFINITY;
       bi[e] = 0;
     }
-    for (int kh = 0; kh < g.k; ++kh) {
+    // every tap loads from a clamped (in-bounds) pixel and out-of-window taps are skipped in the
+    // reduction only, so an unrolled 3x3 window issues all 9 loads before the first use
+#pragma unroll
+    for (int kh = 0; kh < k; ++kh) {
       const int ih = oh * g.s - g.pad + kh;
-      if ((unsigned)ih >= (unsigned)g.H) continue;
-      for (int kw = 0; kw < g.k; ++kw) {
+      const bool vh = (unsigned)ih < (unsigned)g.H;
+      const int ihc = vh ? ih : (ih < 0 ? 0 : g.H - 1);
+#pragma unroll
+      for (int kw = 0; kw < k; ++kw) {
         const int iw = ow * g.s - g.pad + kw;
-        if ((unsigned)iw >= (unsigned)g.W) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.x_ld + ch * 8);
+        const bool vw = (unsigned)iw < (unsigned)g.W;
+        const int iwc = vw ? iw : (iw < 0 ? 0 : g.W - 1);
+        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ihc) * g.W + iwc) * g.x_ld + ch * 8);
+        if (!(vh && vw)) continue;
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-        const int pos = kh * g.k + kw;
+        const int pos = kh * k + kw;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float f = to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
@@ -59,36 +68,38 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const uint16_t* __rest
     o.y = pack2<DT>(best[2], best[3]);
     o.z = pack2<DT>(best[4], best[5]);
     o.w = pack2<DT>(best[6], best[7]);
-    *reinterpret_cast<uint4*>(y + pix * g.y_ld + ch * 8) = o;
+    *reinterpret_cast<uint4*>(y + (long long)pix * g.y_ld + ch * 8) = o;
     uint2 ix;
     ix.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
     ix.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
-    *reinterpret_cast<uint2*>(idx + pix * g.C + ch * 8) = ix;
+    *reinterpret_cast<uint2*>(idx + (long long)pix * g.C + ch * 8) = ix;
   }
 }
 
-template <int DT>
+template <int DT, int KC, typename IT>
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __restrict__ gy, const uint8_t* __restrict__ idx,
                                                           uint16_t* __restrict__ gx, PoolGeom g) {
   const int cpp = g.C >> 3;
-  const long long total = (long long)g.N * g.H * g.W * cpp;
-  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+  const int k = KC ? KC : g.k;
+  const IT total = (IT)g.N * g.H * g.W * cpp;
+  for (IT t = (IT)blockIdx.x * 256 + threadIdx.x; t < total; t += (IT)gridDim.x * 256) {
     const int ch = (int)(t % cpp);
-    const long long pix = t / cpp;
+    const IT pix = t / cpp;
     const int w = (int)(pix % g.W);
-    const int h = (int)((pix / g.W) % g.H);
-    const long long n = pix / ((long long)g.W * g.H);
+    const IT pq = pix / g.W;
+    const int h = (int)(pq % g.H);
+    const long long n = (long long)(pq / g.H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // windows containing (h, w): oh*s - pad <= h <= oh*s - pad + k - 1
-    const int oh_lo = max(0, (h + g.pad - g.k + g.s) / g.s), oh_hi = min(g.OH - 1, (h + g.pad) / g.s);
-    const int ow_lo = max(0, (w + g.pad - g.k + g.s) / g.s), ow_hi = min(g.OW - 1, (w + g.pad) / g.s);
+    const int oh_lo = max(0, (h + g.pad - k + g.s) / g.s), oh_hi = min(g.OH - 1, (h + g.pad) / g.s);
+    const int ow_lo = max(0, (w + g.pad - k + g.s) / g.s), ow_hi = min(g.OW - 1, (w + g.pad) / g.s);
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
       const int kh = h + g.pad - oh * g.s;
-      if (kh < 0 || kh >= g.k) continue;
+      if (kh < 0 || kh >= k) continue;
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
         const int kw = w + g.pad - ow * g.s;
-        if (kw < 0 || kw >= g.k) continue;
-        const uint32_t pos = (uint32_t)(kh * g.k + kw);
+        if (kw < 0 || kw >= k) continue;
+        const uint32_t pos = (uint32_t)(kh * k + kw);
         const long long op = (n * g.OH + oh) * g.OW + ow;
         const uint4 v = *reinterpret_cast<const uint4*>(gy + op * g.y_ld + ch * 8);
         const uint2 ix = *reinterpret_cast<const uint2*>(idx + op * g.C + ch * 8);
@@ -105,7 +116,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
     o.y = pack2<DT>(acc[2], acc[3]);
     o.z = pack2<DT>(acc[4], acc[5]);
     o.w = pack2<DT>(acc[6], acc[7]);
-    *reinterpret_cast<uint4*>(gx + pix * g.x_ld + ch * 8) = o;
+    *reinterpret_cast<uint4*>(gx + (long long)pix * g.x_ld + ch * 8) = o;
   }
 }
 
@@ -114,31 +125,38 @@ __device__ __forceinline__ int win_count(int o, int s, int pad, int k, int L) {
   return hi - lo + 1;
 }
 
-template <int DT>
+template <int DT, int KC, typename IT>
 __global__ void __launch_bounds__(256) avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           PoolGeom g) {
   const int cpp = g.C >> 3;
-  const long long total = (long long)g.N * g.OH * g.OW * cpp;
-  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+  const int k = KC ? KC : g.k;
+  const IT total = (IT)g.N * g.OH * g.OW * cpp;
+  for (IT t = (IT)blockIdx.x * 256 + threadIdx.x; t < total; t += (IT)gridDim.x * 256) {
     const int ch = (int)(t % cpp);
-    const long long pix = t / cpp;
+    const IT pix = t / cpp;
     const int ow = (int)(pix % g.OW);
-    const int oh = (int)((pix / g.OW) % g.OH);
-    const long long n = pix / ((long long)g.OW * g.OH);
+    const IT pq = pix / g.OW;
+    const int oh = (int)(pq % g.OH);
+    const long long n = (long long)(pq / g.OH);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int kh = 0; kh < g.k; ++kh) {
+#pragma unroll
+    for (int kh = 0; kh < k; ++kh) {
       const int ih = oh * g.s - g.pad + kh;
-      if ((unsigned)ih >= (unsigned)g.H) continue;
-      for (int kw = 0; kw < g.k; ++kw) {
+      const bool vh = (unsigned)ih < (unsigned)g.H;
+      const int ihc = vh ? ih : (ih < 0 ? 0 : g.H - 1);
+#pragma unroll
+      for (int kw = 0; kw < k; ++kw) {
         const int iw = ow * g.s - g.pad + kw;
-        if ((unsigned)iw >= (unsigned)g.W) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ih) * g.W + iw) * g.x_ld + ch * 8);
+        const bool vw = (unsigned)iw < (unsigned)g.W;
+        const int iwc = vw ? iw : (iw < 0 ? 0 : g.W - 1);
+        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + ihc) * g.W + iwc) * g.x_ld + ch * 8);
+        if (!(vh && vw)) continue;  // clamped load above: all loads of the window issue up front
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
       }
     }
-    const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, g.k, g.H) * win_count(ow, g.s, g.pad, g.k, g.W));
+    const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, k, g.H) * win_count(ow, g.s, g.pad, k, g.W));
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       acc[e] = acc[e] * inv + (g.bias ? g.bias[ch * 8 + e] : 0.f);
@@ -149,31 +167,33 @@ __global__ void __launch_bounds__(256) avgpool_fwd_kernel(const uint16_t* __rest
     o.y = pack2<DT>(acc[2], acc[3]);
     o.z = pack2<DT>(acc[4], acc[5]);
     o.w = pack2<DT>(acc[6], acc[7]);
-    *reinterpret_cast<uint4*>(y + pix * g.y_ld + ch * 8) = o;
+    *reinterpret_cast<uint4*>(y + (long long)pix * g.y_ld + ch * 8) = o;
   }
 }
 
-template <int DT>
+template <int DT, int KC, typename IT>
 __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __restrict__ gy, uint16_t* __restrict__ gx,
                                                           PoolGeom g) {
   const int cpp = g.C >> 3;
-  const long long total = (long long)g.N * g.H * g.W * cpp;
-  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+  const int k = KC ? KC : g.k;
+  const IT total = (IT)g.N * g.H * g.W * cpp;
+  for (IT t = (IT)blockIdx.x * 256 + threadIdx.x; t < total; t += (IT)gridDim.x * 256) {
     const int ch = (int)(t % cpp);
-    const long long pix = t / cpp;
+    const IT pix = t / cpp;
     const int w = (int)(pix % g.W);
-    const int h = (int)((pix / g.W) % g.H);
-    const long long n = pix / ((long long)g.W * g.H);
+    const IT pq = pix / g.W;
+    const int h = (int)(pq % g.H);
+    const long long n = (long long)(pq / g.H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int oh_lo = max(0, (h + g.pad - g.k + g.s) / g.s), oh_hi = min(g.OH - 1, (h + g.pad) / g.s);
-    const int ow_lo = max(0, (w + g.pad - g.k + g.s) / g.s), ow_hi = min(g.OW - 1, (w + g.pad) / g.s);
+    const int oh_lo = max(0, (h + g.pad - k + g.s) / g.s), oh_hi = min(g.OH - 1, (h + g.pad) / g.s);
+    const int ow_lo = max(0, (w + g.pad - k + g.s) / g.s), ow_hi = min(g.OW - 1, (w + g.pad) / g.s);
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
       const int kh = h + g.pad - oh * g.s;
-      if (kh < 0 || kh >= g.k) continue;
+      if (kh < 0 || kh >= k) continue;
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
         const int kw = w + g.pad - ow * g.s;
-        if (kw < 0 || kw >= g.k) continue;
-        const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, g.k, g.H) * win_count(ow, g.s, g.pad, g.k, g.W));
+        if (kw < 0 || kw >= k) continue;
+        const float inv = 1.f / (float)(win_count(oh, g.s, g.pad, k, g.H) * win_count(ow, g.s, g.pad, k, g.W));
         const uint4 v = *reinterpret_cast<const uint4*>(gy + ((n * g.OH + oh) * g.OW + ow) * g.y_ld + ch * 8);
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -185,7 +205,7 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __rest
     o.y = pack2<DT>(acc[2], acc[3]);
     o.z = pack2<DT>(acc[4], acc[5]);
     o.w = pack2<DT>(acc[6], acc[7]);
-    *reinterpret_cast<uint4*>(gx + pix * g.x_ld + ch * 8) = o;
+    *reinterpret_cast<uint4*>(gx + (long long)pix * g.x_ld + ch * 8) = o;
   }
 }
 
@@ -230,21 +250,33 @@ static unsigned grid_for(long long total) {
   return (unsigned)std::min<long long>((total + 255) / 256, 256LL * 32);
 }
 
-template <int DT>
-static int pool_dt(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, const PoolGeom& g,
-                   hipStream_t st) {
+template <int DT, int KC, typename IT>
+static int pool_dt_k(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, const PoolGeom& g,
+                     hipStream_t st) {
   const long long out_total = (long long)g.N * g.OH * g.OW * (g.C / 8), in_total = (long long)g.N * g.H * g.W * (g.C / 8);
   if (kind == 0 && dir == 0)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<DT>, dim3(grid_for(out_total)), dim3(256), 0, st, in, out, idx, g);
+    hipLaunchKernelGGL((maxpool_fwd_kernel<DT, KC, IT>), dim3(grid_for(out_total)), dim3(256), 0, st, in, out, idx, g);
   else if (kind == 0 && dir == 1)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<DT>, dim3(grid_for(in_total)), dim3(256), 0, st, in, idx, out, g);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<DT, KC, IT>), dim3(grid_for(in_total)), dim3(256), 0, st, in, idx, out, g);
   else if (kind == 1 && dir == 0)
-    hipLaunchKernelGGL(avgpool_fwd_kernel<DT>, dim3(grid_for(out_total)), dim3(256), 0, st, in, out, g);
+    hipLaunchKernelGGL((avgpool_fwd_kernel<DT, KC, IT>), dim3(grid_for(out_total)), dim3(256), 0, st, in, out, g);
   else if (kind == 1 && dir == 1)
-    hipLaunchKernelGGL(avgpool_bwd_kernel<DT>, dim3(grid_for(in_total)), dim3(256), 0, st, in, out, g);
+    hipLaunchKernelGGL((avgpool_bwd_kernel<DT, KC, IT>), dim3(grid_for(in_total)), dim3(256), 0, st, in, out, g);
   else
     return -2;
   return (int)hipGetLastError();
+}
+
+// 3x3 windows (every pool of InceptionV3 / ResNet-50) unroll with all loads in flight; 32-bit index
+// math whenever the thread count fits (64-bit divisions cost ~100 instructions each per thread)
+template <int DT>
+static int pool_dt(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, const PoolGeom& g,
+                   hipStream_t st) {
+  const long long big = std::max((long long)g.N * g.OH * g.OW, (long long)g.N * g.H * g.W) * (g.C / 8) + 256LL * 32 * 256;
+  const bool i32 = big < 0x7FFFFFFFLL;
+  if (g.k == 3 && i32) return pool_dt_k<DT, 3, int>(kind, dir, in, out, idx, g, st);
+  if (i32) return pool_dt_k<DT, 0, int>(kind, dir, in, out, idx, g, st);
+  return pool_dt_k<DT, 0, long long>(kind, dir, in, out, idx, g, st);
 }
 
 int subpixel_scatter_launch(const uint16_t* E, const uint16_t* emask, uint16_t* gx, int N, int H, int W, int C, int OH,

@@ -111,7 +111,7 @@ def test_gpu_pool_kernels(native_lib):
     from deconv_api_amd.ops.autograd import avg_pool, max_pool
 
     g = torch.Generator().manual_seed(1)
-    for k, s, p in [(3, 2, 0), (3, 1, 1), (3, 2, 1)]:
+    for k, s, p in [(3, 2, 0), (3, 1, 1), (3, 2, 1), (2, 2, 0), (5, 1, 2)]:  # 3x3: unrolled kernels
         x = torch.randn(2, 13, 11, 24, generator=g).to(torch.bfloat16).float()
         for fn in (max_pool, avg_pool):
             xc = x.clone().requires_grad_(True)
