@@ -433,7 +433,8 @@ void sumsq_core(Tensor x, Tensor part, int64_t b) {
 }
 
 // gx = 2 * scale[n] * x on the border-b core (0 elsewhere), plus `addend` (same layout) when given
-void sumsq_core_bwd(Tensor x, Tensor scale, Tensor gx, int64_t b, c10::optional<Tensor> addend) {
+void sumsq_core_bwd(Tensor x, Tensor scale, Tensor gx, int64_t b, c10::optional<Tensor> addend,
+                    c10::optional<Tensor> part) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.size(3) % 8 == 0, "sumsq_bwd: x contiguous NHWC, C % 8");
@@ -446,6 +447,18 @@ void sumsq_core_bwd(Tensor x, Tensor scale, Tensor gx, int64_t b, c10::optional<
     TORCH_CHECK(addend->sizes() == x.sizes() && addend->scalar_type() == x.scalar_type() && addend->is_contiguous(),
                 "sumsq_bwd: addend like x");
     ap = reinterpret_cast<const uint16_t*>(addend->data_ptr());
+  }
+  if (part.has_value()) {  // + the loss partials of x (the forward sumsq_core, fused)
+    check_cuda(*part, "part");
+    TORCH_CHECK(part->dim() == 2 && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->size(0) == x.size(0),
+                "sumsq_bwd: part [N, P] fp32");
+    check_rc(dv::sumsq_core_fused_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()), scale.data_ptr<float>(), ap,
+                                         reinterpret_cast<uint16_t*>(gx.data_ptr()), part->data_ptr<float>(),
+                                         (int)part->size(1), (int)x.size(0), (int)x.size(1), (int)x.size(2),
+                                         (int)x.size(3), (int)b, dt_of(x), cur_stream()),
+             "sumsq_core_fused");
+    return;
   }
   check_rc(dv::sumsq_core_bwd_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()), scale.data_ptr<float>(), ap,
                                      reinterpret_cast<uint16_t*>(gx.data_ptr()), (int)x.size(0), (int)x.size(1),
@@ -816,7 +829,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("subpixel_scatter", &subpixel_scatter, "input gradient of a stride-s 1x1 conv from its GEMM result");
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient (+ optional addend)", py::arg("x"),
-        py::arg("scale"), py::arg("gx"), py::arg("b"), py::arg("addend") = py::none());
+        py::arg("scale"), py::arg("gx"), py::arg("b"), py::arg("addend") = py::none(), py::arg("part") = py::none());
   m.def("tile_gather", &tile_gather, "tiled DeepDream: rolled tile gather into the 16-bit network input");
   m.def("tile_pack", &tile_pack, "tiled DeepDream: owned-pixel gradient pack + unit loss / sum|g| tail");
   m.def("tile_update", &tile_update, "tiled DeepDream: normalize + update the image from every rank's packs");

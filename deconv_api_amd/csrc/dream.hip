@@ -66,6 +66,48 @@ __global__ void __launch_bounds__(256) sumsq_core_bwd_kernel(const uint16_t* __r
   }
 }
 
+// The same gradient fused with the loss itself: block (p, n) of a (parts, N) grid walks image n's
+// elements, writes gx = addend + 2 scale[n] x (core) / addend (border), and its fp32 partial sum of
+// x^2 over the core to part[n][p] - the forward sumsq_core launch of every loss layer disappears
+// (the loss is consumed only by the update after the backward). Same partial layout as sumsq_core.
+template <int DT>
+__global__ void __launch_bounds__(256) sumsq_core_fused_kernel(const uint16_t* __restrict__ x,
+                                                               const float* __restrict__ scale,
+                                                               const uint16_t* __restrict__ addend,
+                                                               uint16_t* __restrict__ gx, float* __restrict__ part,
+                                                               int H, int W, int C, int b) {
+  const int n = blockIdx.y;
+  const int cpp = C >> 3;
+  const int total = H * W * cpp;
+  const long long base = (long long)n * total;
+  const float s2 = 2.f * scale[n];
+  float acc = 0.f;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    const int pix = t / cpp;
+    const int ww = pix % W, hh = pix / W;
+    const bool core = hh >= b && hh < H - b && ww >= b && ww < W - b;
+    uint4 o = addend ? *reinterpret_cast<const uint4*>(addend + (base + t) * 8) : uint4{0u, 0u, 0u, 0u};
+    if (core) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (base + t) * 8);
+      const uint32_t vi[4] = {v.x, v.y, v.z, v.w};
+      uint32_t oi[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = to_f<DT>(vi[e] & 0xFFFFu), hi = to_f<DT>(vi[e] >> 16);
+        acc += lo * lo + hi * hi;
+        oi[e] = pack2<DT>(s2 * lo + to_f<DT>(oi[e] & 0xFFFFu), s2 * hi + to_f<DT>(oi[e] >> 16));
+      }
+      o = uint4{oi[0], oi[1], oi[2], oi[3]};
+    }
+    *reinterpret_cast<uint4*>(gx + (base + t) * 8) = o;
+  }
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[(long long)n * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // ---- fused DeepDream step tail (engine/deepdream.py:DeepDream._fused_step) ----
 // part[n][p] = sum of |g| over channels 0..2 of the network-input gradient g [N, H, W, 8]
 template <int DT>
@@ -343,6 +385,17 @@ int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, i
     hipLaunchKernelGGL(sumsq_core_kernel<DT_F16>, grid, dim3(256), 0, s, x, part, H, W, C, b);
   else
     hipLaunchKernelGGL(sumsq_core_kernel<DT_BF16>, grid, dim3(256), 0, s, x, part, H, W, C, b);
+  return (int)hipGetLastError();
+}
+
+int sumsq_core_fused_launch(const uint16_t* x, const float* scale, const uint16_t* addend, uint16_t* gx, float* part,
+                            int parts, int N, int H, int W, int C, int b, int dtype, hipStream_t s) {
+  if (C % 8 != 0 || H <= 2 * b || W <= 2 * b || parts < 1 || (long long)H * W * (C / 8) > 0x7FFFFFFFLL) return -1;
+  const dim3 grid((unsigned)parts, (unsigned)N);
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(sumsq_core_fused_kernel<DT_F16>, grid, dim3(256), 0, s, x, scale, addend, gx, part, H, W, C, b);
+  else
+    hipLaunchKernelGGL(sumsq_core_fused_kernel<DT_BF16>, grid, dim3(256), 0, s, x, scale, addend, gx, part, H, W, C, b);
   return (int)hipGetLastError();
 }
 

@@ -134,6 +134,9 @@ int sumsq_core_launch(const uint16_t* x, float* part, int parts, int N, int H, i
                       hipStream_t s);
 int sumsq_core_bwd_launch(const uint16_t* x, const float* scale, const uint16_t* addend, uint16_t* gx, int N, int H, int W, int C, int b,
                           int dtype, hipStream_t s);
+// sumsq_core_bwd + the forward partials (part [N][parts], as sumsq_core) in one pass
+int sumsq_core_fused_launch(const uint16_t* x, const float* scale, const uint16_t* addend, uint16_t* gx, float* part,
+                            int parts, int N, int H, int W, int C, int b, int dtype, hipStream_t s);
 // col2im of a strided conv's input gradient for <= 8 input channels (output padded to 8 channels)
 struct Col2ImGeom {
   int N, H, W, OH, OW, KH, KW, stride, pad_h, pad_w, Cr, J_ld;

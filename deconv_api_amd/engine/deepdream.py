@@ -48,6 +48,9 @@ SPLIT = int(os.environ.get("DV_DREAM_SPLIT", "2"))
 # DV_DREAM_TAPS=0: intermediate loss layers get their loss gradient through autograd's sum (A/B);
 # default: a loss tap adds it into the gradient from above in the loss-gradient kernel itself
 TAPS = os.environ.get("DV_DREAM_TAPS", "1") != "0"
+# DV_DREAM_FUSED_LOSS=0: separate forward loss-partial launches (A/B); default: every loss layer's
+# partial sums of squares come out of its loss-gradient kernel (one launch per loss layer, not two)
+FUSED_LOSS = os.environ.get("DV_DREAM_FUSED_LOSS", "1") != "0"
 LOSS_PARTS = 32
 
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
@@ -165,7 +168,7 @@ class DeepDream:
         def tap(name, a):
             a = a.contiguous()
             tapped.add(name)
-            return loss_tap(a, scale(name, a), b)
+            return loss_tap(a, scale(name, a), b, st.lpart[names.index(name)] if FUSED_LOSS else None)
 
         with premasked_grads():  # the loss gradient 2*act/numel vanishes where act does
             acts = self.net.forward(xin, names, tap=tap if TAPS else None)
@@ -175,11 +178,16 @@ class DeepDream:
             st.lcoef = torch.tensor(coef, dtype=torch.float32, device=self.device)
         roots, gacts = [], []
         for i, (n, a) in enumerate(zip(names, outs)):
-            lib.sumsq_core(a, st.lpart[i], b)
-            if n in tapped:
+            if n in tapped:  # its loss partials come from the tap's backward kernel (FUSED_LOSS)
+                if not FUSED_LOSS:
+                    lib.sumsq_core(a, st.lpart[i], b)
                 continue
             ga = torch.empty_like(a)
-            lib.sumsq_core_bwd(a, scale(n, a), ga, b)
+            if FUSED_LOSS:
+                lib.sumsq_core_bwd(a, scale(n, a), ga, b, None, st.lpart[i])
+            else:
+                lib.sumsq_core(a, st.lpart[i], b)
+                lib.sumsq_core_bwd(a, scale(n, a), ga, b)
             roots.append(a)
             gacts.append(ga)
         (g,) = torch.autograd.grad(roots, xin, gacts)

@@ -355,24 +355,26 @@ class _LossTapFn(torch.autograd.Function):
     summing two separately materialized gradients (an extra elementwise add per tap and step)."""
 
     @staticmethod
-    def forward(ctx, a, scale, b: int):
+    def forward(ctx, a, scale, b: int, part=None):
         ctx.save_for_backward(a, scale)
         ctx.b = b
+        ctx.part = part
         return a.view_as(a)
 
     @staticmethod
     def backward(ctx, g):
         a, scale = ctx.saved_tensors
         gx = torch.empty_like(a)
-        native.lib().sumsq_core_bwd(a, scale, gx, ctx.b, g.contiguous())
-        return gx, None, None
+        native.lib().sumsq_core_bwd(a, scale, gx, ctx.b, g.contiguous(), ctx.part)
+        return gx, None, None, None
 
 
-def loss_tap(a: torch.Tensor, scale: torch.Tensor, b: int) -> torch.Tensor:
+def loss_tap(a: torch.Tensor, scale: torch.Tensor, b: int, part: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``a`` unchanged; its gradient gains the DeepDream loss term of ``a`` (GPU, contiguous a). The
     ReLU-output tag carries over: the consumer's backward relies on it to hand back a gradient
-    already masked by a > 0 (the premasked contract)."""
-    return _tag(_LossTapFn.apply(a, scale, b), _is_relu_out(a))
+    already masked by a > 0 (the premasked contract). ``part`` ([N, P] fp32): the backward kernel
+    also writes the layer's loss partials there (no separate forward loss launch)."""
+    return _tag(_LossTapFn.apply(a, scale, b, part), _is_relu_out(a))
 
 
 def sumsq_core(x: torch.Tensor, b: int) -> torch.Tensor:
