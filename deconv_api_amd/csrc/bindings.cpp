@@ -418,6 +418,53 @@ static int dt_of(const Tensor& t) {
   return t.scalar_type() == at::kHalf ? dv::DT_F16 : dv::DT_BF16;
 }
 
+// strided few-channel stem conv (InceptionV3 conv2d_1) on the direct VALU kernels; w: fp32
+// [KH][KW][cr][cout]. g = {N, H, W, OH, OW, C, cr, cout, k, stride, pad, relu}. dir 0: x [N,H,W,C] ->
+// out [N,OH,OW,cout] (+bias, ReLU); dir 1: x = gy [N,OH,OW,cout] -> out = gx [N,H,W,C]. Returns false
+// when the geometry is not covered (the caller takes the GEMM path).
+bool stem_conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, std::vector<int64_t> g, int64_t dir) {
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  check_cuda(w, "w");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(g.size() == 12, "stem_conv: geometry");
+  const int N = (int)g[0], H = (int)g[1], W = (int)g[2], OH = (int)g[3], OW = (int)g[4], C = (int)g[5];
+  const int cr = (int)g[6], cout = (int)g[7], k = (int)g[8], st = (int)g[9], pad = (int)g[10], relu = (int)g[11];
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == (int64_t)k * k * cr * cout,
+              "stem_conv: w fp32 [k][k][cr][cout]");
+  TORCH_CHECK(x.scalar_type() == out.scalar_type() && x.dim() == 4 && out.dim() == 4 && x.stride(3) == 1 &&
+                  out.stride(3) == 1 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "stem_conv: 16-bit NHWC, 16-B aligned");
+  const Tensor& full = dir == 0 ? x : out;
+  const Tensor& red = dir == 0 ? out : x;
+  TORCH_CHECK(full.size(0) == N && full.size(1) == H && full.size(2) == W && full.size(3) >= C &&
+                  red.size(0) == N && red.size(1) == OH && red.size(2) == OW && red.size(3) >= cout,
+              "stem_conv: shapes");
+  TORCH_CHECK(full.stride(1) == W * full.stride(2) && full.stride(0) == (int64_t)H * W * full.stride(2) &&
+                  red.stride(1) == OW * red.stride(2) && red.stride(0) == (int64_t)OH * OW * red.stride(2),
+              "stem_conv: dense pixels");
+  int rc;
+  if (dir == 0) {
+    const float* bp = nullptr;
+    if (bias.has_value()) {
+      check_cuda(*bias, "bias");
+      TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= cout, "stem_conv: bias fp32");
+      bp = bias->data_ptr<float>();
+    }
+    rc = dv::stem_conv_fwd_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()), w.data_ptr<float>(), bp,
+                                  reinterpret_cast<uint16_t*>(out.data_ptr()), N, H, W, OH, OW, C, cr, cout, k, st, pad,
+                                  relu, x.stride(2), out.stride(2), dt_of(x), cur_stream());
+  } else {
+    rc = dv::stem_conv_dgrad_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()), w.data_ptr<float>(),
+                                    reinterpret_cast<uint16_t*>(out.data_ptr()), N, H, W, OH, OW, C, cr, cout, k, st,
+                                    pad, x.stride(2), out.stride(2), dt_of(x), cur_stream());
+  }
+  if (rc == -4) return false;
+  check_rc(rc, "stem_conv");
+  return true;
+}
+
 // DeepDream loss core: part [N, P] fp32 partial sums of x^2 over x[:, b:H-b, b:W-b, :]
 void sumsq_core(Tensor x, Tensor part, int64_t b) {
   check_cuda(x, "x");
@@ -828,6 +875,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("kind"), py::arg("dir"), py::arg("geom"), py::arg("bias") = py::none(), py::arg("relu") = false);
   m.def("subpixel_scatter", &subpixel_scatter, "input gradient of a stride-s 1x1 conv from its GEMM result");
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
+  m.def("stem_conv", &stem_conv, "strided few-channel stem conv (direct VALU kernels), fwd (dir 0) / dgrad (dir 1)");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient (+ optional addend)", py::arg("x"),
         py::arg("scale"), py::arg("gx"), py::arg("b"), py::arg("addend") = py::none(), py::arg("part") = py::none());
   m.def("tile_gather", &tile_gather, "tiled DeepDream: rolled tile gather into the 16-bit network input");

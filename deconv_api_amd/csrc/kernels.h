@@ -68,6 +68,14 @@ int conv_dma_splitk(const ConvArgs& a);
 // tuning override: force DMA tile config cfg (> 0, conv_dma.hip:dma_forced) and split-K ks (> 0); 0 = auto
 void conv_dma_tune(int cfg, int ks);
 int splitk_reduce_launch(const ConvArgs& a, int epi, hipStream_t stream);
+// direct VALU kernels for InceptionV3's conv2d_1 (8-ch padded RGB -> 32, 3x3 / stride 2): forward and
+// input gradient (conv_stem.hip); < 0: unsupported geometry
+int stem_conv_fwd_launch(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,
+                         int OH, int OW, int C, int cr, int cout, int k, int stride, int pad, int relu, long long x_ld,
+                         long long y_ld, int dtype, hipStream_t s);
+int stem_conv_dgrad_launch(const uint16_t* gy, const float* w, uint16_t* gx, int N, int H, int W, int OH, int OW,
+                           int C, int cr, int cout, int k, int stride, int pad, long long gy_ld, long long gx_ld,
+                           int dtype, hipStream_t s);
 // persistent pointwise (1x1 / s1 / p0) conv at large M, 16-bit LDS-staged epilogue (conv_pw.hip);
 // < 0: unsupported shape / mode (use conv_dma_launch)
 int conv_pw_launch(const ConvArgs& a, hipStream_t stream);

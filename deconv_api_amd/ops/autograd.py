@@ -25,6 +25,8 @@ from .conv import ConvWeights, conv2d, pad_channels_oihw, transpose_subpixel
 SUBPIXEL = os.environ.get("DV_SUBPIXEL", "1") != "0"
 # DV_COL2IM=0 disables the GEMM + col2im input gradient of few-channel strided convs (A/B testing)
 COL2IM = os.environ.get("DV_COL2IM", "1") != "0"
+# DV_STEM_DIRECT=0: InceptionV3's conv2d_1 (3 -> 32, 3x3 / 2) on the GEMM (+ col2im) path (A/B)
+STEM_DIRECT = os.environ.get("DV_STEM_DIRECT", "1") != "0"
 
 
 _PREMASKED = [False]
@@ -112,6 +114,12 @@ class ConvUnit:
                     wc = self.w.permute(2, 3, 1, 0).reshape(kh * kw * cr, self.cout, 1, 1)  # [(kh,kw,c), oc]
                     self.col_w = ConvWeights(wc.contiguous(), None, "fwd").to_device(self.device, dtype)
                     self.col_ld = -(-kh * kw * cr // 8) * 8
+                # few-channel strided stem conv (InceptionV3 conv2d_1): direct VALU kernels for the
+                # forward and the input gradient (csrc/conv_stem.hip), fp32 [kh][kw][c][co] weights
+                self.stem_w = None
+                if STEM_DIRECT and cr == 3 and kh == kw == 3 and self.stride == 2 and self.cout == 32 and \
+                        w8.shape[1] == 8:
+                    self.stem_w = self.w.permute(2, 3, 1, 0).contiguous().to(self.device)
                 # sub-pixel classes: s^2 stride-1 convs instead of one s^2-times-wasteful gather
                 self.bwd_sub = []
                 for rh, rw, ws, pd in transpose_subpixel(w8, self.stride, self.pad):
@@ -128,10 +136,24 @@ class ConvUnit:
         return y.relu() if self.relu else y
 
 
+def _stem_fwd(x, unit: ConvUnit):
+    """conv2d_1-style strided few-channel conv on the direct kernel, or None (geometry not covered)."""
+    if getattr(unit, "stem_w", None) is None or unit.pad[0] != unit.pad[1]:
+        return None
+    N, H, W, C = x.shape
+    OH = (H + 2 * unit.pad[0] - 3) // unit.stride + 1
+    OW = (W + 2 * unit.pad[1] - 3) // unit.stride + 1
+    y = torch.empty(N, OH, OW, unit.cout, dtype=x.dtype, device=x.device)
+    g = [N, H, W, OH, OW, C, 3, unit.cout, 3, unit.stride, unit.pad[0], int(unit.relu)]
+    return y if native.lib().stem_conv(x, unit.stem_w, unit.fwd.bias_pad, y, g, 0) else None
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, unit: ConvUnit):
-        y = conv2d(x, unit.fwd, stride=unit.stride, pad=unit.pad, relu=unit.relu)
+        y = _stem_fwd(x, unit)
+        if y is None:
+            y = conv2d(x, unit.fwd, stride=unit.stride, pad=unit.pad, relu=unit.relu)
         ctx.unit = unit
         ctx.in_hw = (x.shape[1], x.shape[2])
         ctx.premasked = _PREMASKED[0]
@@ -192,6 +214,13 @@ def dgrad_strided_into(unit: ConvUnit, gy, in_hw, out: torch.Tensor, accumulate:
 
 
 def _dgrad_strided(unit: ConvUnit, gy, mask, in_hw):
+    if mask is None and getattr(unit, "stem_w", None) is not None and unit.pad[0] == unit.pad[1]:
+        N, OH, OW, _ = gy.shape
+        H, W = in_hw
+        gx = torch.empty(N, H, W, unit.fwd.cin, dtype=gy.dtype, device=gy.device)
+        g = [N, H, W, OH, OW, unit.fwd.cin, 3, unit.cout, 3, unit.stride, unit.pad[0], 0]
+        if native.lib().stem_conv(gy.contiguous(), unit.stem_w, None, gx, g, 1):
+            return gx
     if unit.col_w is not None and COL2IM:
         return _col2im_dgrad(gy, mask, unit, in_hw)
     if SUBPIXEL:

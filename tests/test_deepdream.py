@@ -402,3 +402,39 @@ def test_gpu_tiled_whole_octave_graph_1024(native_lib):
     assert all(st.graph is not None for st in dd._tgraphs.values())
     assert torch.isfinite(graph).all() and _cos(graph - x, eager - x) > 0.99
     assert torch.isfinite(dd.run(x)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p,H,W", [(0, 37, 41), (0, 40, 38), (1, 33, 36)])
+def test_gpu_stem_conv_direct(native_lib, p, H, W):
+    """InceptionV3 conv2d_1 geometry (3 -> 32, 3x3 / stride 2) on the direct VALU kernels
+    (csrc/conv_stem.hip): forward (bias + ReLU) and the input gradient (premasked, as DeepDream runs
+    it) vs CPU autograd and vs the GEMM + col2im path of the same unit."""
+    from deconv_api_amd.ops import autograd as AG
+
+    g = torch.Generator().manual_seed(H * W + p)
+    w = (torch.randn(32, 3, 3, 3, generator=g) / 27 ** 0.5).to(torch.bfloat16).float()
+    b = torch.randn(32, generator=g) * 0.1
+    x = torch.randn(2, H, W, 3, generator=g).to(torch.bfloat16).float()
+    cpu = AG.ConvUnit("u", w, b, 2, (p, p), relu=True).build("cpu")
+    gpu = AG.ConvUnit("u", w, b, 2, (p, p), relu=True).build("cuda", torch.bfloat16)
+    assert gpu.stem_w is not None
+    xc = x.clone().requires_grad_(True)
+    yc = cpu(xc)
+    gy = (torch.randn(*yc.shape, generator=g) * (yc > 0)).to(torch.bfloat16).float()  # premasked gradient
+    (gc,) = torch.autograd.grad(yc, xc, gy)
+    x8 = torch.nn.functional.pad(x, (0, 5)).to(torch.bfloat16).cuda()
+    outs = {}
+    for path in ("direct", "gemm"):
+        if path == "gemm":
+            gpu.stem_w = None
+        xd = x8.clone().requires_grad_(True)
+        with AG.premasked_grads():
+            yd = gpu(xd)
+        (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.bfloat16).cuda())
+        gd = gd.float().cpu()
+        outs[path] = (yd.float().cpu(), gd)
+        assert (yd.float().cpu() - yc).abs().max() < 2e-2 * yc.abs().max()
+        assert (gd[..., :3] - gc).abs().max() < 2e-2 * gc.abs().max()
+    assert float(outs["direct"][1][..., 3:].abs().max()) == 0.0  # padding channels get no gradient
+    assert (outs["direct"][1][..., :3] - outs["gemm"][1][..., :3]).abs().max() < 2e-2 * gc.abs().max()
