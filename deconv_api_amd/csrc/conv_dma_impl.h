@@ -1027,6 +1027,10 @@ static int dma_forced(const ConvArgs& a, hipStream_t s, int cfg) {
     case 13: return okn(64) ? dma_cfg<DT, 2, 2, 2, 2, 64, 8, AMODE, EPI>(a, s) : -5;               // 64x64 w4 ST8
     case 14: return okn(64) ? dma_cfg<DT, 4, 1, 2, 4, 64, 6, AMODE, EPI>(a, s) : -5;               // 128x64 w4 ST6
     case 15: return okn(128) ? dma_cfg<DT, 2, 2, 2, 4, 64, 6, AMODE, EPI>(a, s) : -5;              // 64x128 w4 ST6
+    // 8 waves on a 64x64 tile: half the LDS-DMA issues per wave and K tile (the small tiles' K loop
+    // is DMA-issue bound: 4 x ~100 cycles per wave per K tile at 4 waves)
+    case 16: return okn(64) ? dma_cfg<DT, 4, 2, 1, 2, 64, 3, AMODE, EPI>(a, s) : -5;               // 64x64 w8
+    case 17: return okn(64) ? dma_cfg<DT, 4, 2, 1, 2, 64, 4, AMODE, EPI>(a, s) : -5;               // 64x64 w8 ST4
     default: return -5;
   }
 }
@@ -1044,7 +1048,11 @@ static int auto_cfg(const ConvArgs& a) {
   // (short K too: M 1600 x N 64 x K 64 4.2 vs 6.0 us for the size-based 256 x 64 tile in a graph,
   // tools/small_conv_latency.py; DV_SMALL_TILE_KMIN=256 restores the round-1 rule)
   static const int kmin = std::getenv("DV_SMALL_TILE_KMIN") ? std::atoi(std::getenv("DV_SMALL_TILE_KMIN")) : 0;
-  if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= kmin) return 8;
+  // DV_SMALL_TILE_W8=1 (opt-in): for the smallest M, 8 waves on the 64x64 tile with a 4-deep ring
+  // (half the DMA issues per wave and K tile): M1600 x N160 x K1440 12.8 -> 11.8 us in isolation
+  // (tools/small_conv_latency.py), but config 3 end to end 417 vs 418 img/s (noise), so off
+  static const bool w8 = std::getenv("DV_SMALL_TILE_W8") != nullptr && std::atoi(std::getenv("DV_SMALL_TILE_W8")) != 0;
+  if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= kmin) return (w8 && a.M <= 8192) ? 17 : 8;
   if (a.OCpad % 128 == 0 && a.OC > 64 && a.Kpad < 4096 && (a.Kpad < 1024 || mn < 50000000LL)) return 3;
   return 0;
 }
@@ -1128,7 +1136,7 @@ static void dma_tile_dims(const ConvArgs& a, bool mask, int& BM, int& BN) {
   BN = 16;
   if (!mask) {
     const int c = auto_cfg(a);
-    if (c == 8) { BM = 64; BN = 64; return; }
+    if (c == 8 || c == 17) { BM = 64; BN = 64; return; }
     if (c == 3) { BM = 128; BN = 128; return; }
   }
   if (mask) {

@@ -45,8 +45,9 @@ def graph_time(fn, reps=50, iters=5):
 
 
 # (tile config, split-K) pairs: 0/0 = the shipped policy; configs in csrc/conv_dma_impl.h:dma_forced
-# (8: 64x64 4 waves 3 stages, 12: same 6 stages, 13: 8 stages, 7: 128x64 4 waves, 3: 128x128)
-SWEEP = [(0, 0), (8, 1), (12, 1), (13, 1), (7, 1), (3, 1), (8, 2), (8, 4), (12, 4)]
+# (8: 64x64 4 waves 3 stages, 16: 64x64 8 waves, 17: 8 waves 4 stages, 12: 4 waves 6 stages,
+#  7: 128x64 4 waves)
+SWEEP = [(0, 0), (8, 1), (16, 1), (17, 1), (12, 1), (7, 1), (8, 4), (16, 4)]
 
 
 def main():
