@@ -68,6 +68,16 @@ def create_app(service=None, cfg: Optional[Config] = None, dream_service=None) -
 
     app.state.get_service = get_service
 
+    if cfg.asyncio_debug:  # asyncio debug mode (blocking callbacks, unawaited coroutines)
+        @app.on_event("startup")
+        async def _loop_debug():
+            import asyncio
+
+            loop = asyncio.get_running_loop()
+            loop.set_debug(True)
+            loop.slow_callback_duration = cfg.slow_callback_ms / 1000.0
+            app.state.loop_debug = True
+
     @app.get("/health-check")
     def healthcheck():
         M.REQUESTS.inc(route="/health-check", status="200")

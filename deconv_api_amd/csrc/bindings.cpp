@@ -290,12 +290,15 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     // A/B switches: DV_HS_EMASK_OFF (masked dgrads back on the DMA kernel), DV_HS_PAD_OFF (pad != 1)
     static const bool hs_emask_off = std::getenv("DV_HS_EMASK_OFF") != nullptr;
     static const bool hs_pad_off = std::getenv("DV_HS_PAD_OFF") != nullptr;
+    // smallest map side routed to the halo-stream kernels (DV_HS_MIN_W, default 64)
+    static const int64_t hs_min_w = std::getenv("DV_HS_MIN_W") ? std::atoll(std::getenv("DV_HS_MIN_W")) : 64;
     // 3x3 s1 convs (pad 0..2) with 64/128 padded output channels at large maps: halo-stream kernel
     // (every input pixel fetched once per 32-channel chunk instead of once per tap); also the ReLU-
     // masked (emask) input gradients of such convs (InceptionV3 stem / ResNet 3x3 dgrads)
     if (impl == 0 && amode == dv::CONV_A_FWD && (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_POOL) &&
         !mask.has_value() && !a.res && !a.ucode && !a.accumulate && a.relu_cols <= 0 &&
-        (int64_t)a.H * a.W >= 64 * 64 && a.W >= 64 && (!a.emask || !hs_emask_off) && (a.pad_h == 1 || !hs_pad_off)) {
+        (int64_t)a.H * a.W >= hs_min_w * hs_min_w && a.W >= hs_min_w && (!a.emask || !hs_emask_off) &&
+        (a.pad_h == 1 || !hs_pad_off)) {
       const int rc = dv::conv3x3_hs_launch(a, (int)epi, cur_stream());
       if (rc >= 0) {
         check_rc(rc, "conv_halo_stream");

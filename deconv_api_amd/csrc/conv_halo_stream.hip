@@ -627,6 +627,28 @@ static int hs_ring() {
 
 int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
   if (std::getenv("DV_NO_HS") != nullptr) return -4;
+  // 192 / 256 padded output channels (InceptionV3 conv2d_5: 96 -> 192): two launches over the
+  // channel halves [0, 128) and [128, OCpad), each re-reading the (small) input halo
+  if ((a.OCpad == 192 || a.OCpad == 256) && a.OC > 128 && epi == CONV_E_BF16 && std::getenv("DV_NO_HS_SPLIT") == nullptr) {
+    ConvArgs a1 = a, a2 = a;
+    a1.OC = 128;
+    a1.OCpad = 128;
+    a2.OC = a.OC - 128;
+    a2.OCpad = a.OCpad - 128;
+    a2.w = a.w + (long long)128 * a.Kpad;
+    a2.bias = a.bias ? a.bias + 128 : nullptr;
+    a2.out = reinterpret_cast<uint16_t*>(a.out) + 128;
+    a2.out_elems = a.out_elems - 128;
+    if (a.emask) {
+      a2.emask = a.emask + 128;
+      a2.emask_elems = a.emask_elems - 128;
+    }
+    if (a2.OC % 4 != 0) return -4;
+    // both halves must be supported before either launches
+    const int r1 = conv3x3_hs_launch(a1, epi, s);
+    if (r1 < 0) return r1;
+    return conv3x3_hs_launch(a2, epi, s);
+  }
   // 3x3 / stride 1, symmetric pad 0..2 (output = input + 2 pad - 2)
   const bool geom = a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad_h == a.pad_w && a.pad_h >= 0 && a.pad_h <= 2 &&
                     a.OH == a.H + 2 * a.pad_h - 2 && a.OW == a.W + 2 * a.pad_w - 2 && a.OH > 0 && a.OW > 0;

@@ -280,3 +280,35 @@ def test_deepdream_requests_are_batched():
             ds.prepare(np.zeros((40, 40, 3), np.uint8), 4)
     finally:
         ds.close()
+
+
+def test_asyncio_debug_mode_enables_loop_debug():
+    """DV_ASYNCIO_DEBUG: the app's startup hook puts the event loop in debug mode (slow-callback
+    logging at cfg.slow_callback_ms)."""
+    from fastapi.testclient import TestClient
+
+    from deconv_api_amd.api.app import create_app
+    from deconv_api_amd.config import Config
+
+    cfg = Config(asyncio_debug=True, slow_callback_ms=20.0, log_json=False)
+    app = create_app(service=object(), cfg=cfg)
+    with TestClient(app) as c:
+        assert c.get("/health-check").json() == {"healthy": "true"}
+        assert getattr(app.state, "loop_debug", False) is True
+
+
+def test_scale_sweep_efficiency_and_parsing():
+    """tools/scale_sweep.py: JSON-line parsing of bench output and weak-scaling efficiency."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "scale_sweep", os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "scale_sweep.py"))
+    sw = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sw)
+    out = 'noise\n{"metric": "m", "value": 100.0, "unit": "images/s"}\n'
+    assert sw.parse_json_line(out)["value"] == 100.0
+    rows = sw.efficiency([{"n": 1, "value": 100.0}, {"n": 2, "value": 190.0}, {"n": 4, "value": None}])
+    assert rows[0]["efficiency"] == 1.0 and rows[1]["efficiency"] == 0.95 and rows[2]["efficiency"] is None
+    assert sw.bench_cmd(2, type("A", (), dict(steps=3, warmup=1, device="cpu", tiny=True, batch=0))())[1:3] == \
+        ["-m", "torch.distributed.run"]

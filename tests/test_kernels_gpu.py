@@ -722,6 +722,8 @@ def test_dense_layers_as_mfma_gemm(native_lib):
     (64, 64, 64, 64, 1, True),    # hs16 (16-multiple output) with an output mask
     (64, 128, 66, 66, 0, False),  # hs16, 'valid' (64 x 64 output)
     (96, 96, 70, 67, 1, True),    # OC 96 -> 128-channel tile, 3 chunks, ragged
+    (96, 192, 73, 73, 0, False),  # InceptionV3 conv2d_5 (channels padded 80 -> 96): OCpad 192, two launches
+    (192, 96, 71, 71, 2, True),   # its input gradient (full pad, ReLU-masked)
 ])
 def test_conv_halo_stream_pad_emask(native_lib, monkeypatch, dt, C, OC, H, W, pad, use_emask):
     """Halo-stream 3x3 kernels with pad 0/1/2 (output H + 2 pad - 2), ragged tiles and the emask
