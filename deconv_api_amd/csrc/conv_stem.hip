@@ -72,19 +72,20 @@ __global__ void __launch_bounds__(256) stem_conv_fwd_kernel(const uint16_t* __re
   }
 }
 
-// Input gradient of the stride-2 3x3 conv above (no bias / ReLU: the output gradient gy arrives
+// Input gradient of a stride-2 KxK conv from RGB (the 3x3 conv above; ResNet-50's 7x7 conv1) (no bias /
+// ReLU: the output gradient gy arrives
 // masked): gx[n, y, x, c] = sum over taps (kh, kw) with y = 2 oy - P + kh, x = 2 ox - P + kw of
 // gy[n, oy, ox, :] . w[kh][kw][c][:]. Pixels split into the four stride-2 parity classes of
 // (y + P, x + P), one class per blockIdx.y: a class's taps are fixed (even: kh 0 and 2, odd: kh 1),
 // so every branch is wave-uniform and a thread reads <= 4 output-gradient pixels (64 B each).
 // gx gets all 8 (padded) channels, channels >= CR zero.
-template <int DT, int COUT, int CR>
-__global__ void __launch_bounds__(256) stem_conv_dgrad_s2k3_kernel(const uint16_t* __restrict__ gy,
+template <int DT, int COUT, int CR, int K>
+__global__ void __launch_bounds__(256) stem_conv_dgrad_s2_kernel(const uint16_t* __restrict__ gy,
                                                                    const float* __restrict__ w,
                                                                    uint16_t* __restrict__ gx, int N, int H, int W,
                                                                    int OH, int OW, int pad, long long gy_ld,
                                                                    long long gx_ld) {
-  constexpr int NW4 = 9 * CR * COUT / 4;
+  constexpr int NW4 = K * K * CR * COUT / 4;
   __shared__ float4 wl[NW4];  // LDS broadcast weights [tap][c][co]
   for (int i = threadIdx.x; i < NW4; i += 256) wl[i] = reinterpret_cast<const float4*>(w)[i];
   __syncthreads();
@@ -106,11 +107,11 @@ __global__ void __launch_bounds__(256) stem_conv_dgrad_s2k3_kernel(const uint16_
 #pragma unroll
   for (int c = 0; c < CR; ++c) acc[c] = 0.f;
 #pragma unroll
-  for (int kh = 0; kh < 3; ++kh) {
+  for (int kh = 0; kh < K; ++kh) {
     if ((kh & 1) != py) continue;  // wave-uniform
     const int oy = (y + pad - kh) >> 1;
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
+    for (int kw = 0; kw < K; ++kw) {
       if ((kw & 1) != px) continue;
       const int ox = (x + pad - kw) >> 1;
       if ((unsigned)oy >= (unsigned)OH || (unsigned)ox >= (unsigned)OW) continue;
@@ -129,8 +130,8 @@ __global__ void __launch_bounds__(256) stem_conv_dgrad_s2k3_kernel(const uint16_
         }
 #pragma unroll
         for (int c = 0; c < CR; ++c) {
-          const float4 w0 = wl[((kh * 3 + kw) * CR + c) * (COUT / 4) + 2 * v];
-          const float4 w1 = wl[((kh * 3 + kw) * CR + c) * (COUT / 4) + 2 * v + 1];
+          const float4 w0 = wl[((kh * K + kw) * CR + c) * (COUT / 4) + 2 * v];
+          const float4 w1 = wl[((kh * K + kw) * CR + c) * (COUT / 4) + 2 * v + 1];
           float a0 = acc[c];
           a0 = fmaf(gv[0], w0.x, a0);
           a0 = fmaf(gv[1], w0.y, a0);
@@ -174,17 +175,24 @@ int stem_conv_fwd_launch(const uint16_t* x, const float* w, const float* bias, u
 int stem_conv_dgrad_launch(const uint16_t* gy, const float* w, uint16_t* gx, int N, int H, int W, int OH, int OW,
                            int C, int cr, int cout, int k, int stride, int pad, long long gy_ld, long long gx_ld,
                            int dtype, hipStream_t s) {
-  if (C != 8 || cr != 3 || cout != 32 || k != 3 || stride != 2 || gy_ld % 8 || gx_ld % 8 || pad < 0 || pad > 2 ||
+  // (cout, k): InceptionV3 conv2d_1 (32, 3x3) and ResNet-50 conv1 (64, 7x7), both stride 2 from RGB
+  const bool inc = cout == 32 && k == 3, res = cout == 64 && k == 7;
+  if (C != 8 || cr != 3 || !(inc || res) || stride != 2 || gy_ld % 8 || gx_ld % 8 || pad < 0 || pad >= k ||
       (long long)N * ((H + 2) / 2) * ((W + 2) / 2) > 0x7FFFFFFFLL)
     return -4;
   // grid.y = the 4 parity classes; grid.x sized for the largest class
   const dim3 grid(stem_grid((long long)N * ((H + 2) / 2) * ((W + 2) / 2)), 4);
-  if (dtype == DT_F16)
-    hipLaunchKernelGGL((stem_conv_dgrad_s2k3_kernel<DT_F16, 32, 3>), grid, dim3(256), 0, s, gy, w, gx, N, H, W,
-                       OH, OW, pad, gy_ld, gx_ld);
-  else
-    hipLaunchKernelGGL((stem_conv_dgrad_s2k3_kernel<DT_BF16, 32, 3>), grid, dim3(256), 0, s, gy, w, gx, N, H, W,
-                       OH, OW, pad, gy_ld, gx_ld);
+#define STEM_DG(DT_, CO_, K_)                                                                                  \
+  hipLaunchKernelGGL((stem_conv_dgrad_s2_kernel<DT_, CO_, 3, K_>), grid, dim3(256), 0, s, gy, w, gx, N, H, W, OH, \
+                     OW, pad, gy_ld, gx_ld)
+  if (dtype == DT_F16) {
+    if (inc) STEM_DG(DT_F16, 32, 3);
+    else STEM_DG(DT_F16, 64, 7);
+  } else {
+    if (inc) STEM_DG(DT_BF16, 32, 3);
+    else STEM_DG(DT_BF16, 64, 7);
+  }
+#undef STEM_DG
   return (int)hipGetLastError();
 }
 

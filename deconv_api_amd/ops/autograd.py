@@ -27,6 +27,7 @@ SUBPIXEL = os.environ.get("DV_SUBPIXEL", "1") != "0"
 COL2IM = os.environ.get("DV_COL2IM", "1") != "0"
 # DV_STEM_DIRECT=0: InceptionV3's conv2d_1 (3 -> 32, 3x3 / 2) on the GEMM (+ col2im) path (A/B)
 STEM_DIRECT = os.environ.get("DV_STEM_DIRECT", "1") != "0"
+STEM_DIRECT7 = os.environ.get("DV_STEM_DIRECT7", "0") != "0"
 
 
 _PREMASKED = [False]
@@ -116,9 +117,11 @@ class ConvUnit:
                     self.col_ld = -(-kh * kw * cr // 8) * 8
                 # few-channel strided stem conv (InceptionV3 conv2d_1): direct VALU kernels for the
                 # forward and the input gradient (csrc/conv_stem.hip), fp32 [kh][kw][c][co] weights
+                # (ResNet-50's 7x7 conv1 input gradient on the same kernel is opt-in, DV_STEM_DIRECT7=1:
+                # 23.4 vs 25.0 img/s on config 5 - 2352 FMAs per pixel lose to GEMM + col2im there)
                 self.stem_w = None
-                if STEM_DIRECT and cr == 3 and kh == kw == 3 and self.stride == 2 and self.cout == 32 and \
-                        w8.shape[1] == 8:
+                if STEM_DIRECT and cr == 3 and self.stride == 2 and w8.shape[1] == 8 and \
+                        ((kh == kw == 3 and self.cout == 32) or (kh == kw == 7 and self.cout == 64 and STEM_DIRECT7)):
                     self.stem_w = self.w.permute(2, 3, 1, 0).contiguous().to(self.device)
                 # sub-pixel classes: s^2 stride-1 convs instead of one s^2-times-wasteful gather
                 self.bwd_sub = []
@@ -138,8 +141,8 @@ class ConvUnit:
 
 def _stem_fwd(x, unit: ConvUnit):
     """conv2d_1-style strided few-channel conv on the direct kernel, or None (geometry not covered)."""
-    if getattr(unit, "stem_w", None) is None or unit.pad[0] != unit.pad[1]:
-        return None
+    if getattr(unit, "stem_w", None) is None or unit.pad[0] != unit.pad[1] or unit.w.shape[2] != 3:
+        return None  # (the 7x7 forward stays on the implicit GEMM: 386 TF/s there)
     N, H, W, C = x.shape
     OH = (H + 2 * unit.pad[0] - 3) // unit.stride + 1
     OW = (W + 2 * unit.pad[1] - 3) // unit.stride + 1
@@ -218,7 +221,7 @@ def _dgrad_strided(unit: ConvUnit, gy, mask, in_hw):
         N, OH, OW, _ = gy.shape
         H, W = in_hw
         gx = torch.empty(N, H, W, unit.fwd.cin, dtype=gy.dtype, device=gy.device)
-        g = [N, H, W, OH, OW, unit.fwd.cin, 3, unit.cout, 3, unit.stride, unit.pad[0], 0]
+        g = [N, H, W, OH, OW, unit.fwd.cin, 3, unit.cout, unit.w.shape[2], unit.stride, unit.pad[0], 0]
         if native.lib().stem_conv(gy.contiguous(), unit.stem_w, None, gx, g, 1):
             return gx
     if unit.col_w is not None and COL2IM:

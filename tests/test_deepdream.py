@@ -405,20 +405,23 @@ def test_gpu_tiled_whole_octave_graph_1024(native_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("p,H,W", [(0, 37, 41), (0, 40, 38), (1, 33, 36)])
-def test_gpu_stem_conv_direct(native_lib, p, H, W):
-    """InceptionV3 conv2d_1 geometry (3 -> 32, 3x3 / stride 2) on the direct VALU kernels
-    (csrc/conv_stem.hip): forward (bias + ReLU) and the input gradient (premasked, as DeepDream runs
-    it) vs CPU autograd and vs the GEMM + col2im path of the same unit."""
+@pytest.mark.parametrize("p,H,W,k,cout", [(0, 37, 41, 3, 32), (0, 40, 38, 3, 32), (1, 33, 36, 3, 32),
+                                          (3, 37, 41, 7, 64), (3, 40, 38, 7, 64)])
+def test_gpu_stem_conv_direct(native_lib, monkeypatch, p, H, W, k, cout):
+    """InceptionV3 conv2d_1 geometry (3 -> 32, 3x3 / stride 2) and ResNet-50 conv1 (3 -> 64, 7x7 / 2; opt-in)
+    on the direct VALU kernels (csrc/conv_stem.hip; the 7x7 forward stays on the GEMM): forward
+    (bias + ReLU) and the input gradient (premasked, as DeepDream runs it) vs CPU autograd and vs
+    the GEMM + col2im path of the same unit."""
     from deconv_api_amd.ops import autograd as AG
 
+    monkeypatch.setattr(AG, "STEM_DIRECT7", True)
     g = torch.Generator().manual_seed(H * W + p)
-    w = (torch.randn(32, 3, 3, 3, generator=g) / 27 ** 0.5).to(torch.bfloat16).float()
-    b = torch.randn(32, generator=g) * 0.1
+    w = (torch.randn(cout, 3, k, k, generator=g) / (3 * k * k) ** 0.5).to(torch.bfloat16).float()
+    b = torch.randn(cout, generator=g) * 0.1
     x = torch.randn(2, H, W, 3, generator=g).to(torch.bfloat16).float()
     cpu = AG.ConvUnit("u", w, b, 2, (p, p), relu=True).build("cpu")
     gpu = AG.ConvUnit("u", w, b, 2, (p, p), relu=True).build("cuda", torch.bfloat16)
-    assert gpu.stem_w is not None
+    assert gpu.stem_w is not None and gpu.col_w is not None
     xc = x.clone().requires_grad_(True)
     yc = cpu(xc)
     gy = (torch.randn(*yc.shape, generator=g) * (yc > 0)).to(torch.bfloat16).float()  # premasked gradient
