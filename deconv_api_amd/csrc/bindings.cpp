@@ -42,7 +42,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
           c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
           int64_t epi, int64_t impl, c10::optional<Tensor> res, c10::optional<Tensor> emask,
           c10::optional<Tensor> stats, int64_t stats_div, c10::optional<Tensor> ucode, int64_t ucode_div,
-          int64_t relu_cols) {
+          int64_t relu_cols, c10::optional<Tensor> out2, int64_t split_col) {
   TORCH_CHECK(g.size() == 23, "conv: geometry vector must have 23 entries");
   check_cuda(x, "x");
   check_cuda(w, "w");
@@ -119,7 +119,9 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
   } else {
     TORCH_CHECK(out.scalar_type() == dt, "16-bit epilogue needs out of x's dtype");
   }
-  need(out, ((out_rows - 1) * a.out_ld + a.OC) * (int64_t)out.element_size(), "out");
+  // with out2 only the leading split_col channels land in out
+  const int64_t out_cols = out2.has_value() ? std::min<int64_t>(split_col, a.OC) : a.OC;
+  need(out, ((out_rows - 1) * a.out_ld + out_cols) * (int64_t)out.element_size(), "out");
   a.out = out.data_ptr();
   if (res.has_value()) {  // fused residual: LDS-DMA forward conv with a 16-bit output only
     check_cuda(*res, "res");
@@ -155,10 +157,28 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     a.emask = reinterpret_cast<const uint16_t*>(emask->data_ptr());
     a.emask_elems = avail_bytes(*emask) / 2;
   }
+  if (out2.has_value()) {  // columns >= split_col to a second tensor (plain LDS-staged epilogue only)
+    check_cuda(*out2, "out2");
+    TORCH_CHECK(out2->scalar_type() == dt && out2->dim() == 4 && out2->stride(3) == 1 && epi == dv::CONV_E_BF16 &&
+                    amode == dv::CONV_A_FWD && !a.accumulate && !res.has_value() && !emask.has_value() &&
+                    !ucode.has_value() && !stats.has_value() && impl == 2 && split_col > 0 && split_col % 8 == 0 &&
+                    split_col < a.OC && a.OC % 8 == 0,
+                "conv out2: plain 16-bit forward on the LDS-DMA kernel, split_col % 8 == 0 < OC, OC % 8 == 0");
+    a.out2_ld = out2->stride(2);
+    TORCH_CHECK(out2->size(3) >= a.OC - split_col && out2->stride(1) == a.OW * a.out2_ld &&
+                    out2->stride(0) == (int64_t)a.OH * a.OW * a.out2_ld && a.out2_ld % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(out2->data_ptr()) % 16 == 0,
+                "out2: dense pixels, 16-B aligned rows");
+    need(*out2, ((int64_t)(a.M - 1) * a.out2_ld + (a.OC - split_col)) * 2, "out2");
+    a.out2 = out2->data_ptr();
+    a.out2_elems = avail_bytes(*out2) / 2;
+    a.split_col = (int)split_col;
+  }
   {  // LDS-staged vector epilogue: 16-bit rows (out / res / emask) 16-B aligned
     auto al = [](const void* p, int64_t ld) { return reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 8 == 0; };
     a.vec_epi = epi == dv::CONV_E_BF16 && al(a.out, a.out_ld) && (!a.res || al(a.res, a.res_ld)) &&
-                (!a.emask || al(a.emask, a.emask_ld)) && std::getenv("DV_NO_VEC_EPI") == nullptr;
+                (!a.emask || al(a.emask, a.emask_ld)) && (std::getenv("DV_NO_VEC_EPI") == nullptr || a.out2);
+    TORCH_CHECK(!a.out2 || a.vec_epi, "conv out2: 16-B aligned out rows (LDS-staged epilogue)");
     static const bool no_batch = std::getenv("DV_NO_EPI_BATCH") != nullptr;
     a.epi_batch = !no_batch;
   }
@@ -311,7 +331,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     TORCH_CHECK((int64_t)a.H * a.W * a.x_ld * 2 * imgs_per_tile < 0x7FFFFFF0LL, "conv dma: image too large");
     // split-K when the tile grid would leave most CUs idle (plain epilogues only)
     // (the reduce kernel applies bias / ReLU / accumulate / residual / emask; not the unpool scatter)
-    const bool plain_epi = (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && !a.ucode;
+    const bool plain_epi = (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && !a.ucode && !a.out2;
     const int ks = plain_epi ? dv::conv_dma_splitk(a) : 1;
     Tensor ws;
     if (ks > 1) {
@@ -871,7 +891,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mask"), py::arg("geom"), py::arg("amode"), py::arg("epi"), py::arg("impl"),
         py::arg("res") = py::none(), py::arg("emask") = py::none(), py::arg("stats") = py::none(),
         py::arg("stats_div") = 1, py::arg("ucode") = py::none(), py::arg("ucode_div") = 1,
-        py::arg("relu_cols") = 0);
+        py::arg("relu_cols") = 0, py::arg("out2") = py::none(), py::arg("split_col") = 0);
   m.def("dma_tune", [](int64_t cfg, int64_t ks) { dv::conv_dma_tune((int)cfg, (int)ks); },
         "force the LDS-DMA conv tile config / split-K factor (0 = automatic); tuning only");
   m.def("pool", &pool, "k x k max/avg pooling forward/backward", py::arg("in"), py::arg("out"), py::arg("idx"),

@@ -665,6 +665,12 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
     const int grow = m0 + row, gcol = n0 + cc * 8;
     if (grow >= a.M || gcol >= a.OC) continue;
     uint4 v = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((cc ^ (row & SWZ)) << 4));
+    if (a.out2 != nullptr && gcol >= a.split_col) {  // two-destination merged GEMM (plain epilogue)
+      const long long o2 = (long long)grow * a.out2_ld + (gcol - a.split_col);
+      if (DV_BOUNDS(o2, 8, a.out2_elems, "conv_dma epilogue_lds out2"))
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(a.out2) + o2) = v;
+      continue;
+    }
     const long long o = (long long)grow * a.out_ld + gcol;
     if (!a.ucode && !DV_BOUNDS(o, gcol + 8 > a.OC ? a.OC - gcol : 8, a.out_elems, "conv_dma epilogue_lds out")) continue;
     if (a.res && !DV_BOUNDS((long long)grow * a.res_ld + gcol, gcol + 8 > a.OC ? a.OC - gcol : 8, a.res_elems,

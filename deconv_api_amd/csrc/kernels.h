@@ -58,6 +58,10 @@ struct ConvArgs {
   long long x_elems, out_elems, res_elems, emask_elems;
   int relu_cols;          // > 0: ReLU only on output columns < relu_cols (merged GEMMs whose trailing
                           //   columns are pre-activation values, ops/inception.py); 0: every column
+  void* out2;             // optional (LDS-staged 16-bit epilogue, plain): columns >= split_col go to
+  long long out2_ld;      //   out2[row * out2_ld + col - split_col] instead of out (a merged GEMM whose
+  int split_col;          //   leading columns are one consumer's output and the rest another's)
+  long long out2_elems;
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);

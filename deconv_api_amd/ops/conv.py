@@ -216,7 +216,7 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
            out: Optional[torch.Tensor] = None, accumulate: bool = False, out_hw=None,
            use_bias: bool = True, res: Optional[torch.Tensor] = None, emask: Optional[torch.Tensor] = None,
            stats: Optional[torch.Tensor] = None, stats_div: int = 1, unpool_out: Optional[torch.Tensor] = None,
-           unpool_div: int = 1, relu_cols: int = 0):
+           unpool_div: int = 1, relu_cols: int = 0, out2: Optional[torch.Tensor] = None, split_col: int = 0):
     """NHWC convolution.
 
     x: [N, H, W, C] (channel-slice views allowed: stride(3) == 1). For ``in_mode='unpool'`` x is
@@ -230,6 +230,9 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     epilogue and returned at [N, 2 OH, 2 OW, OC] (the deconvnet's conv-down feeding an unpool).
     ``relu_cols`` > 0: ``relu`` applies to output channels < relu_cols only (a merged GEMM whose
     trailing channels are pre-activation values; LDS-DMA kernel).
+    ``out2`` / ``split_col`` (GPU, plain 16-bit forward): output channels >= split_col go to ``out2``
+    (channel c -> out2[..., c - split_col]) and only the leading ones to ``out`` - one merged GEMM
+    feeding two consumers (InceptionV3: the b1 branch's concat slice and the heads buffer).
     """
     if pad is None:
         pad = (cw.KH // 2, cw.KW // 2)
@@ -255,8 +258,16 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     if x.is_cuda:
         return _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
                            mask, epilogue, out, accumulate, use_bias, res, emask, stats, stats_div, unpool_out,
-                           unpool_div, relu_cols)
+                           unpool_div, relu_cols, out2, split_col)
     assert stats is None, "conv2d: stats are produced by the GPU kernels only"
+    if out2 is not None:  # CPU: the full result, split between the two destinations
+        y = _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
+                        mask, epilogue, None, False, use_bias, res, emask, relu_cols)
+        out2.copy_(y[..., split_col:])
+        if out is not None:
+            out.copy_(y[..., :split_col])
+            return out
+        return y[..., :split_col]
     if unpool_out is not None:
         assert epilogue == "bf16" and out is None and not accumulate, "conv2d: unpool_out needs a fresh 16-bit output"
         y = _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
@@ -317,7 +328,7 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
 
 def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
                 epilogue, out, accumulate, use_bias, res=None, emask=None, stats=None, stats_div=1,
-                unpool_out=None, unpool_div=1, relu_cols=0):
+                unpool_out=None, unpool_div=1, relu_cols=0, out2=None, split_col=0):
     lib = native.lib()
     dt = x.dtype
     assert dt in (torch.bfloat16, torch.float16) and x.stride(3) == 1, \
@@ -342,7 +353,11 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
         out_code = None
         if out is None:
             odt = torch.float32 if epilogue == "f32" else dt
+            # with out2, a fresh out holds the leading split_col channels in a row of OC (the kernel's
+            # storage check covers OC columns); the caller gets the [..., :split_col] view
             out = torch.empty(N, OH, OW, OC, dtype=odt, device=x.device)
+            if out2 is not None:
+                out = out[..., :split_col]
     assert out.stride(-1) == 1
     out_ld = out.stride(-2) if out.dim() == 4 else OC
     mask_ld = 0
@@ -356,11 +371,11 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
     bias = cw.bias_pad if use_bias else None
     # res / unpool_out / relu_cols exist on the LDS-DMA kernel only; emask also on the halo-stream
     # kernels (the binding routes by shape under 'auto')
-    dma_only = res is not None or unpool_out is not None or relu_cols > 0 or \
+    dma_only = res is not None or unpool_out is not None or relu_cols > 0 or out2 is not None or \
         (emask is not None and _policy["impl"] not in ("auto",))
     lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
              IMPL["dma"] if dma_only else IMPL[_policy["impl"]],  # DMA-only epilogue features
-             res, emask, stats, stats_div, unpool_out, unpool_div, relu_cols)
+             res, emask, stats, stats_div, unpool_out, unpool_div, relu_cols, out2, split_col)
     if epilogue == "pool":
         return out, out_code
     return out

@@ -29,6 +29,7 @@ the block masks gY itself. CPU tensors take the plain torch path (the oracle).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Sequence
 
 import torch
@@ -37,6 +38,9 @@ import torch.nn.functional as F
 from . import native
 from .autograd import _PREMASKED, ConvUnit, _is_relu_out, _tag, dgrad_strided_into
 from .conv import conv2d
+
+# DV_MERGE_B1=0: the b1 branch as its own GEMM (A/B); default: it joins the merged head GEMM forward
+MERGE_B1 = os.environ.get("DV_MERGE_B1", "1") != "0"
 
 
 def _pool_out(L: int, k: int, s: int, p: int) -> int:
@@ -50,6 +54,7 @@ class InceptionBlock:
         self.branches = [branches[k] for k in self.order]
         self.units = units
         self.merge = None  # (fwd ConvWeights, bwd ConvWeights, relu_cols, {branch index: (offset, width)})
+        self.merge_b1 = None  # (b1 branch index, b1 width, forward ConvWeights of [W_b1 | heads], relu_cols)
 
     @staticmethod
     def _is_head(u: ConvUnit) -> bool:
@@ -82,6 +87,20 @@ class InceptionBlock:
         fwd = ConvWeights(w, torch.cat(bs, 0), "fwd").to_device(device, dtype)
         bwd = ConvWeights(pad_channels_oihw(w.transpose(0, 1).contiguous()), None, "fwd").to_device(device, dtype)
         self.merge = (fwd, bwd, sum(u.cout for _, u in relu_m), cols)
+        # the b1 branch (a lone 1x1 conv on x, its output a concat slice) joins the FORWARD GEMM as
+        # its leading columns, written straight into Y by the two-destination epilogue (out2): one
+        # launch fewer per block; its backward stays a separate dgrad (its gradient is a gY slice)
+        self.merge_b1 = None
+        if MERGE_B1:
+            for bi, ops in enumerate(self.branches):
+                if len(ops) == 1 and isinstance(ops[0], str) and ops[0] not in ("avg", "max") and \
+                        self._is_head(self.units[ops[0]]) and self.units[ops[0]].cout % 8 == 0:
+                    u1 = self.units[ops[0]]
+                    w1 = pad_channels_oihw(torch.cat([u1.w] + ws, 0))
+                    b1 = torch.cat([u1.b] + bs, 0)
+                    fwd1 = ConvWeights(w1, b1, "fwd").to_device(device, dtype)
+                    self.merge_b1 = (bi, u1.cout, fwd1, u1.cout + self.merge[2])
+                    break
         return self
 
     # ------------------------------------------------------------------ shapes
@@ -146,9 +165,18 @@ class _InceptionFn(torch.autograd.Function):
         saved = [x, Y]
         T = None
         mcols = {}
+        b1_done = None
         if blk.merge is not None:  # every qualifying 1x1 head in one GEMM (pool columns pre-activation)
             mfwd, _, relu_n, mcols = blk.merge
-            T = conv2d(x, mfwd, stride=1, pad=(0, 0), relu=True, use_bias=True, relu_cols=relu_n)
+            if blk.merge_b1 is not None:  # + the b1 branch as leading columns, written into its Y slice
+                b1i, n1, fwd1, relu1 = blk.merge_b1
+                o1 = sum(widths[:b1i])
+                T = torch.empty(N, H, W, mfwd.cout, dtype=x.dtype, device=x.device)
+                conv2d(x, fwd1, stride=1, pad=(0, 0), relu=True, use_bias=True, relu_cols=relu1,
+                       out=Y[..., o1:o1 + n1], out2=T, split_col=n1)
+                b1_done = b1i
+            else:
+                T = conv2d(x, mfwd, stride=1, pad=(0, 0), relu=True, use_bias=True, relu_cols=relu_n)
             saved.append(T)
         plan = []  # per branch: (offset, width, kind, info)
         off = 0
@@ -183,6 +211,9 @@ class _InceptionFn(torch.autograd.Function):
                 for j in range(start, len(ops)):
                     op = ops[j]
                     last = j == len(ops) - 1
+                    if bi == b1_done:  # computed by the merged forward GEMM (backward: its own dgrad)
+                        steps.append(((op,), cur_i))
+                        continue
                     if isinstance(op, tuple):
                         assert last, "split must end its branch"
                         ua, ub = blk.units[op[1]], blk.units[op[2]]

@@ -825,3 +825,25 @@ def test_conv_pointwise_persistent(native_lib, monkeypatch, dt, C, OC, mode):
     finally:
         native_lib.dma_tune(0, 0)
     assert _rel(got, dma) < 1e-2, mode
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,C,OC,split,relu_cols", [(2, 9, 192, 208, 64, 176), (1, 35, 288, 272, 64, 240),
+                                                       (64, 17, 768, 640, 192, 448), (2, 181, 64, 192, 64, 128)])
+def test_conv_two_destination_epilogue(native_lib, dt, N, H, C, OC, split, relu_cols):
+    """Merged 1x1 GEMM with the two-destination epilogue (out2 / split_col; InceptionV3's b1 +
+    heads): leading channels into a channel slice of one buffer, the rest into another, relu_cols
+    honoured; small-M DMA tiles and the large-M persistent kernel (last case)."""
+    g = torch.Generator().manual_seed(OC + split)
+    r = lambda t: t.to(dt).float()  # noqa: E731
+    x = r(torch.randn(N, H, H, C, generator=g))
+    cw = ConvWeights(r(torch.randn(OC, C, 1, 1, generator=g) / np.sqrt(C)), r(torch.randn(OC, generator=g)), "fwd")
+    ref = ops.conv2d(x, cw, pad=0, relu=True, relu_cols=relu_cols)
+    Y = torch.full((N, H, H, split + 104), 7.0).to(dt).to(DEV)  # destination 1: a slice at channel 40
+    T = torch.empty(N, H, H, OC - split, dtype=dt, device=DEV)
+    ops.conv2d(x.to(dt).to(DEV), cw.to_device(DEV, dt), pad=0, relu=True, relu_cols=relu_cols,
+               out=Y[..., 40:40 + split], out2=T, split_col=split)
+    assert _rel(Y[..., 40:40 + split], ref[..., :split]) < 1e-2
+    assert _rel(T, ref[..., split:]) < 1e-2
+    Yc = Y.float().cpu()
+    assert bool((Yc[..., :40] == 7.0).all()) and bool((Yc[..., 40 + split:] == 7.0).all())  # untouched
