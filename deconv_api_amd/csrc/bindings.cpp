@@ -369,11 +369,12 @@ static int64_t pix_ld(const Tensor& t, int64_t H, int64_t W, int64_t C, const ch
 }
 
 void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_t dir, std::vector<int64_t> g,
-          c10::optional<Tensor> bias, bool relu) {
+          c10::optional<Tensor> bias, bool relu, bool accumulate) {
   check_cuda(in, "in");
   check_cuda(out, "out");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(in.device());
   TORCH_CHECK(g.size() == 9, "pool: geometry");
+  TORCH_CHECK(!accumulate || dir == 1, "pool accumulate: backward only");
   const int64_t N = g[0], H = g[1], W = g[2], C = g[3], OH = g[4], OW = g[5], k = g[6], s = g[7], pad = g[8];
   TORCH_CHECK(C % 8 == 0 && k >= 1 && s >= 1 && pad >= 0 && pad < k, "pool: C%8, k, s, pad");
   TORCH_CHECK(OH == (H + 2 * pad - k) / s + 1 && OW == (W + 2 * pad - k) / s + 1, "pool: output size");
@@ -406,7 +407,7 @@ void pool(Tensor in, Tensor out, c10::optional<Tensor> idx, int64_t kind, int64_
   check_rc(dv::pool_launch((int)kind, (int)dir, reinterpret_cast<const uint16_t*>(in.data_ptr()),
                            reinterpret_cast<uint16_t*>(out.data_ptr()), ip, (int)N, (int)H, (int)W, (int)C, (int)OH,
                            (int)OW, (int)k, (int)s, (int)pad, dt == at::kHalf ? dv::DT_F16 : dv::DT_BF16, cur_stream(),
-                           x_ld, y_ld, bp, relu ? 1 : 0),
+                           x_ld, y_ld, bp, relu ? 1 : 0, accumulate ? 1 : 0),
            "pool");
 }
 
@@ -895,7 +896,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dma_tune", [](int64_t cfg, int64_t ks) { dv::conv_dma_tune((int)cfg, (int)ks); },
         "force the LDS-DMA conv tile config / split-K factor (0 = automatic); tuning only");
   m.def("pool", &pool, "k x k max/avg pooling forward/backward", py::arg("in"), py::arg("out"), py::arg("idx"),
-        py::arg("kind"), py::arg("dir"), py::arg("geom"), py::arg("bias") = py::none(), py::arg("relu") = false);
+        py::arg("kind"), py::arg("dir"), py::arg("geom"), py::arg("bias") = py::none(), py::arg("relu") = false,
+        py::arg("accumulate") = false);
   m.def("subpixel_scatter", &subpixel_scatter, "input gradient of a stride-s 1x1 conv from its GEMM result");
   m.def("sumsq_core", &sumsq_core, "DeepDream loss: per-image partial sums of squares over the core");
   m.def("stem_conv", &stem_conv, "strided few-channel stem conv (direct VALU kernels), fwd (dir 0) / dgrad (dir 1)");

@@ -124,7 +124,7 @@ int subpixel_scatter_launch(const uint16_t* E, const uint16_t* emask, uint16_t* 
                             int OW, int s, int dtype, hipStream_t st);
 int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C,
                 int OH, int OW, int k, int s, int pad, int dtype, hipStream_t st, long long x_ld = 0,
-                long long y_ld = 0, const float* bias = nullptr, int relu = 0);
+                long long y_ld = 0, const float* bias = nullptr, int relu = 0, int acc = 0);
 // DeepDream loss: per-(image, block) partial sums of x^2 over the map minus a b-pixel border
 // (part [N][parts]), and its gradient gx = 2*scale[n]*x in the core, 0 on the border
 // fused DeepDream update: per-image mean |g| partials, loss from the sumsq partials, device-side

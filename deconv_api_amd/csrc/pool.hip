@@ -15,6 +15,7 @@ struct PoolGeom {
                          // maps: channel-slice views of concat buffers (InceptionV3 blocks)
   const float* bias;     // avgpool fwd: + bias[c] (the commuted 1x1 conv's bias), or null
   int relu;              // avgpool fwd: ReLU on the output
+  int acc;               // backward: gx += (instead of =) the pooled gradient (Inception max branch)
 };
 
 template <int DT, int KC, typename IT>
@@ -111,6 +112,15 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
         }
       }
     }
+    if (g.acc) {  // accumulate into the existing gradient (one pass instead of pool + add)
+      const uint4 old = *reinterpret_cast<const uint4*>(gx + (long long)pix * g.x_ld + ch * 8);
+      const uint32_t ov[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += to_f<DT>(ov[e] & 0xFFFFu);
+        acc[2 * e + 1] += to_f<DT>(ov[e] >> 16);
+      }
+    }
     uint4 o;
     o.x = pack2<DT>(acc[0], acc[1]);
     o.y = pack2<DT>(acc[2], acc[3]);
@@ -198,6 +208,15 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __rest
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += inv * to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+      }
+    }
+    if (g.acc) {  // accumulate into the existing gradient (one pass instead of pool + add)
+      const uint4 old = *reinterpret_cast<const uint4*>(gx + (long long)pix * g.x_ld + ch * 8);
+      const uint32_t ov[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += to_f<DT>(ov[e] & 0xFFFFu);
+        acc[2 * e + 1] += to_f<DT>(ov[e] >> 16);
       }
     }
     uint4 o;
@@ -292,12 +311,13 @@ int subpixel_scatter_launch(const uint16_t* E, const uint16_t* emask, uint16_t* 
 
 int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C, int OH,
                 int OW, int k, int s, int pad, int dtype, hipStream_t st, long long x_ld, long long y_ld,
-                const float* bias, int relu) {
+                const float* bias, int relu, int acc) {
   if (C % 8 != 0 || k <= 0 || s <= 0 || k > 15) return -1;
   if (x_ld <= 0) x_ld = C;
   if (y_ld <= 0) y_ld = C;
   if (x_ld % 8 || y_ld % 8 || x_ld < C || y_ld < C) return -1;
-  const PoolGeom g{N, H, W, C, OH, OW, k, s, pad, x_ld, y_ld, bias, relu};
+  if (acc && dir != 1) return -1;
+  const PoolGeom g{N, H, W, C, OH, OW, k, s, pad, x_ld, y_ld, bias, relu, acc};
   return dtype == DT_F16 ? pool_dt<DT_F16>(kind, dir, in, out, idx, g, st)
                          : pool_dt<DT_BF16>(kind, dir, in, out, idx, g, st);
 }

@@ -441,3 +441,27 @@ def test_gpu_stem_conv_direct(native_lib, monkeypatch, p, H, W, k, cout):
         assert (gd[..., :3] - gc).abs().max() < 2e-2 * gc.abs().max()
     assert float(outs["direct"][1][..., 3:].abs().max()) == 0.0  # padding channels get no gradient
     assert (outs["direct"][1][..., :3] - outs["gemm"][1][..., :3]).abs().max() < 2e-2 * gc.abs().max()
+
+
+@pytest.mark.gpu
+def test_gpu_pool_backward_accumulate(native_lib):
+    """pool backward with accumulate=True adds the pooled gradient to the existing gx (max and avg)."""
+    from deconv_api_amd.ops import native as nat
+
+    g = torch.Generator().manual_seed(3)
+    N, H, W, C = 2, 13, 11, 24
+    for kind in (0, 1):
+        k, s, p = (3, 2, 0) if kind == 0 else (3, 1, 1)
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        x = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).cuda()
+        y = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device="cuda")
+        idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device="cuda") if kind == 0 else None
+        geom = [N, H, W, C, OH, OW, k, s, p]
+        nat.lib().pool(x, y, idx, kind, 0, geom)
+        gy = torch.randn(N, OH, OW, C, generator=g).to(torch.bfloat16).cuda()
+        plain = torch.empty_like(x)
+        nat.lib().pool(gy, plain, idx, kind, 1, geom)
+        base = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).cuda()
+        acc = base.clone()
+        nat.lib().pool(gy, acc, idx, kind, 1, geom, None, False, True)
+        assert (acc.float() - (base.float() + plain.float())).abs().max() < 2e-2
