@@ -141,7 +141,7 @@ int conv_pw_launch(const ConvArgs& a, hipStream_t s) {
   const int tiles_n = a.OCpad / BN;
   const long long tiles_total = (long long)((a.M + BM - 1) / BM) * tiles_n;
   // persistence pays once every CU walks several tiles
-  if (tiles_total < std::max(4 * cus, min_tiles) || tiles_total > 0x7fffffffLL) return -4;
+  if (tiles_total < (min_tiles > 0 ? min_tiles : 4 * cus) || tiles_total > 0x7fffffffLL) return -4;
   const unsigned G = (unsigned)std::min<long long>(tiles_total, 2 * cus);
   if (BN == 128) {
     if (a.dtype == DT_F16)
