@@ -36,6 +36,7 @@ from deconv_api_amd import ops
 from deconv_api_amd.engine.deconvnet import DeconvNet
 from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
 from deconv_api_amd.parallel import dist as pdist
+from deconv_api_amd.runtime.streams import copy_stream as copy_stream_for
 
 # the reference's implied end-to-end rate for layer=block5_conv3 is ~0.03-0.04 img/s
 # (CPU, one request at a time; a lower bound on its cost). We divide by the favourable 0.04.
@@ -138,7 +139,8 @@ def main(argv=None):
     pending = [None, None]
     cuda = dev.type == "cuda"
     # copy-back of every step's mosaics on its own stream into a pinned double buffer
-    copy_stream = torch.cuda.Stream(dev) if cuda else None
+    # (CU-masked: the D2H blit kernel must not fill the device ahead of the next step's kernels)
+    copy_stream = copy_stream_for(dev) if cuda else None
     host = [torch.empty(B, 2 * S, 2 * S, 3, dtype=torch.uint8, pin_memory=cuda) for _ in range(2)]
     back_done = [None, None]
     lat = []  # (start event, copy-back end event) per timed step

@@ -852,6 +852,93 @@ void resize_preprocess(Tensor img, Tensor out, int64_t mode) {
            "resize_preprocess");
 }
 
+// block1_conv2.down + block1_conv1.down tail: unpool (pooled x + codes) -> 3x3 conv 64 -> 64 -> ReLU ->
+// Z = D W2^T (bf16 [N, H, W, 32]); false if the kernel does not take the shape (caller falls back)
+bool conv_unpool_z(Tensor x, Tensor code, int64_t code_div, Tensor w, Tensor w2, Tensor z) {
+  check_cuda(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.size(3) == 64,
+              "conv_unpool_z: x pooled bf16 [N, H/2, W/2, 64]");
+  TORCH_CHECK(z.dim() == 4 && z.scalar_type() == at::kBFloat16 && z.is_contiguous() && z.size(0) == x.size(0) &&
+                  z.size(1) == 2 * x.size(1) && z.size(2) == 2 * x.size(2) && z.size(3) == 32,
+              "conv_unpool_z: z bf16 [N, H, W, 32]");
+  TORCH_CHECK(code.scalar_type() == at::kByte && code.is_contiguous() && code_div >= 1 && x.size(0) % code_div == 0 &&
+                  code.numel() == x.numel() / code_div,
+              "conv_unpool_z: code u8 [N/code_div, H/2, W/2, 64]");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 && w.size(0) == 64 &&
+                  w.size(1) >= 576 && w.size(1) % 64 == 0,
+              "conv_unpool_z: w bf16 [64, Kpad >= 576]");
+  TORCH_CHECK(w2.scalar_type() == at::kBFloat16 && w2.is_contiguous() && w2.numel() == 32 * 64, "conv_unpool_z: w2 bf16 [32, 64]");
+  check_cuda(code, "code");
+  check_cuda(w, "w");
+  check_cuda(w2, "w2");
+  check_cuda(z, "z");
+  dv::ConvArgs a{};
+  a.N = (int)z.size(0); a.H = a.OH = (int)z.size(1); a.W = a.OW = (int)z.size(2); a.C = 64;
+  a.OC = a.OCpad = 64; a.KH = a.KW = 3; a.stride = 1; a.pad_h = a.pad_w = 1;
+  a.K = 576; a.Kpad = (int)w.size(1); a.M = a.N * a.H * a.W;
+  a.relu = 1; a.relu_in = 1; a.code_div = (int)code_div; a.x_ld = 64; a.out_ld = 32;
+  a.dtype = dv::DT_BF16;
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.w = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  a.w2 = reinterpret_cast<const uint16_t*>(w2.data_ptr());
+  a.code = code.data_ptr<uint8_t>();
+  a.out = z.data_ptr();
+  a.x_elems = avail_bytes(x) / 2;
+  a.out_elems = avail_bytes(z) / 2;
+  const int rc = dv::conv3x3_unpool_z_launch(a, cur_stream());
+  if (rc == -4) return false;
+  check_rc(rc, "conv_unpool_z");
+  return true;
+}
+
+// out fp32 [N, H, W, 3] = ReLU(9-tap shift-add of z [N, H, W, 32]); optional per-image stats
+void zsum3x3(Tensor z, Tensor out, c10::optional<Tensor> stats, int64_t stats_div) {
+  check_cuda(z, "z");
+  check_cuda(out, "out");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(z.device());
+  TORCH_CHECK(z.dim() == 4 && z.scalar_type() == at::kBFloat16 && z.is_contiguous() && z.size(3) == 32,
+              "zsum3x3: z bf16 [N, H, W, 32]");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == z.numel() / 32 * 3,
+              "zsum3x3: out fp32 [N, H, W, 3]");
+  const int N = (int)z.size(0);
+  double* st = nullptr;
+  if (stats.has_value()) {
+    check_cuda(*stats, "stats");
+    TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->is_contiguous() && stats_div >= 1 && N % stats_div == 0 &&
+                    stats->numel() == 2 * (N / stats_div),
+                "zsum3x3: stats fp64 [N/stats_div, 2]");
+    check_rc((int)hipMemsetAsync(stats->data_ptr(), 0, stats->numel() * 8, cur_stream()), "stats memset");
+    st = stats->data_ptr<double>();
+  }
+  check_rc(dv::zsum3x3_launch(reinterpret_cast<const uint16_t*>(z.data_ptr()), out.data_ptr<float>(), N,
+                              (int)z.size(1), (int)z.size(2), st, (int)stats_div, cur_stream()),
+           "zsum3x3");
+}
+
+// A stream whose dispatches may only use `n_cus` CUs (evenly spaced over the device's CU mask bits):
+// host-bound copies (the runtime's D2H blit kernels wait on PCIe writes) then hold a few CUs instead
+// of filling the whole device ahead of the compute stream's next kernels. Returns the hipStream_t
+// handle (never destroyed: one per device and purpose, process lifetime).
+int64_t cu_masked_stream(int64_t device, int64_t n_cus) {
+  int dev_prev = 0;
+  check_rc((int)hipGetDevice(&dev_prev), "hipGetDevice");
+  check_rc((int)hipSetDevice((int)device), "hipSetDevice");
+  int total = 0;
+  check_rc((int)hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, (int)device), "CU count");
+  TORCH_CHECK(n_cus >= 1 && n_cus <= total, "cu_masked_stream: 1 <= n_cus <= ", total);
+  std::vector<uint32_t> mask((total + 31) / 32, 0u);
+  for (int64_t i = 0; i < n_cus; ++i) {
+    const int64_t cu = i * total / n_cus;
+    mask[cu / 32] |= 1u << (cu % 32);
+  }
+  hipStream_t st = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+  hipSetDevice(dev_prev);
+  check_rc((int)e, "hipExtStreamCreateWithCUMask");
+  return reinterpret_cast<int64_t>(st);
+}
+
 void maxpool2x2(Tensor x, Tensor out, Tensor code) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -923,5 +1010,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("preprocess_u8", &preprocess_u8, "resized RGB u8 -> caffe-preprocessed bf16 network input");
   m.def("maxpool2x2", &maxpool2x2);
   m.def("unpool2x2", &unpool2x2);
+  m.def("cu_masked_stream", &cu_masked_stream, "HIP stream restricted to n evenly spaced CUs (handle)");
+  m.def("conv_unpool_z", &conv_unpool_z, "unpool -> conv3x3 64->64 -> ReLU -> per-tap products of the next 64->3 conv");
+  m.def("zsum3x3", &zsum3x3, "9-tap shift-add of a per-tap product map (+ ReLU, per-image stats)");
   m.attr("ARCH") = "gfx950";
 }

@@ -226,9 +226,18 @@ constexpr int V2_A = IH * IW * PIXB;                     // 48960
 constexpr int V2_C = TH * TW * 128;                      // 32768: bf16 output tile staging
 }  // namespace
 
+//
+// ZOUT (block1_conv2.down feeding the final 64 -> 3 block1_conv1.down): instead of the 64-channel map
+// (128 B/px written here, read back by the next conv), the epilogue multiplies the ReLU'd bf16 tile
+// by that conv's weights arranged as W2 [32][64] (row tap*3 + c; rows 27..31 zero) on MFMA and writes
+// Z = D W2^T [N, H, W, 32] bf16 (64 B/px); zsum3x3_kernel finishes the conv as a 9-tap shift-add.
+// Wave w owns tile row w for this GEMM (32 px x 32 Z channels, K = 64: 8 MFMAs); the B operand is the
+// staged output tile read straight from Cst.
+template <bool ZOUT>
 __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * V2_A + V2_C];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * V2_A + V2_C + (ZOUT ? 32 * 128 : 0)];
   uint8_t* Cst = smem + 2 * V2_A;
+  uint8_t* W2s = Cst + V2_C;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int kq = lane >> 4, col = lane & 15;
@@ -251,6 +260,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
   for (int j = 0; j < 2; ++j) {
     const int oc = wc * 32 + j * 16 + col;
     biasv[j] = (a.bias && oc < a.OC) ? a.bias[oc] : 0.f;
+  }
+  // ZOUT: W2 [32][64] bf16 staged once in LDS (4 KiB, 16-B chunks XOR-swizzled by row; in VGPRs it
+  // would spill next to the 144 weight registers); A fragment = row 16 jz + col, K chunk 32 ks + 8 kq
+  if constexpr (ZOUT) {
+    const int r = tid >> 3, c8 = tid & 7;
+    if (tid < 256)
+      *reinterpret_cast<uint4*>(W2s + r * 128 + ((c8 ^ (r & 7)) << 4)) = *reinterpret_cast<const uint4*>(a.w2 + r * C64 + c8 * 8);
   }
 
   uint4 ra[V2_PER_T];
@@ -374,8 +390,47 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
       }
     if (t < ntiles) store_tile(smem + (cur ^ 1) * V2_A, t);
     __syncthreads();
-    // ---- Cst -> global, 16 B per store ----
-    {
+    if constexpr (ZOUT) {  // ---- Z = D W2^T for tile row `wave`, 8-B stores (4 Z channels of one px) ----
+      int b = tcur;
+      const int tx = b % tiles_w;
+      b /= tiles_w;
+      const int ty = b % tiles_h;
+      const int n = b / tiles_h;
+      const int oy = ty * TH + wave;
+      f32x4 z[2][2];
+#pragma unroll
+      for (int jz = 0; jz < 2; ++jz)
+#pragma unroll
+        for (int pf = 0; pf < 2; ++pf) z[jz][pf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int pf = 0; pf < 2; ++pf) {
+        const int pix = wave * TW + pf * 16 + col;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 bd = *reinterpret_cast<const bf16x8*>(Cst + pix * 128 + (((ks * 4 + kq) ^ (pix & 7)) << 4));
+#pragma unroll
+          for (int jz = 0; jz < 2; ++jz) {
+            const bf16x8 wa = *reinterpret_cast<const bf16x8*>(W2s + (jz * 16 + col) * 128 + (((ks * 4 + kq) ^ (col & 7)) << 4));
+            z[jz][pf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bd, z[jz][pf], 0, 0, 0);
+          }
+        }
+      }
+      if (oy < H) {
+#pragma unroll
+        for (int pf = 0; pf < 2; ++pf) {
+          const int ox = tx * TW + pf * 16 + col;
+          if (ox >= W) continue;
+          uint16_t* zo = reinterpret_cast<uint16_t*>(a.out) + (((long long)n * H + oy) * W + ox) * a.out_ld;
+#pragma unroll
+          for (int jz = 0; jz < 2; ++jz) {
+            const int zc = jz * 16 + kq * 4;
+            if (DV_BOUNDS((((long long)n * H + oy) * W + ox) * a.out_ld + zc, 4, a.out_elems, "unpool_z out"))
+              *reinterpret_cast<uint2*>(zo + zc) =
+                  make_uint2(pack_bf2(z[jz][pf][0], z[jz][pf][1]), pack_bf2(z[jz][pf][2], z[jz][pf][3]));
+          }
+        }
+      }
+    } else {  // ---- Cst -> global, 16 B per store ----
       const int tid = opaque_tid();
       int b = tcur;
       const int tx = b % tiles_w;
@@ -1001,7 +1056,7 @@ int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, b
     }();
     const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
     if (ntiles <= 0 || ntiles > 0x7fffffffLL) return -2;
-    hipLaunchKernelGGL(conv3x3_unpool_c64_v2_kernel, dim3((unsigned)std::min<long long>(ntiles, cus)), dim3(512), 0, s,
+    hipLaunchKernelGGL(conv3x3_unpool_c64_v2_kernel<false>, dim3((unsigned)std::min<long long>(ntiles, cus)), dim3(512), 0, s,
                        a);
     return (int)hipGetLastError();
   }
@@ -1041,6 +1096,133 @@ int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, b
   }
 #undef DV_P
   return -1;
+}
+
+int conv3x3_unpool_z_launch(const ConvArgs& a, hipStream_t s) {
+  if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.C != C64 || a.OC != 64 ||
+      a.OCpad != 64 || a.H != a.OH || a.W != a.OW || (a.H & 1) || (a.W & 1) || a.Kpad < KW9 || a.x_ld % 8 ||
+      a.out_ld != 32 || a.w2 == nullptr || a.code == nullptr || a.code_div < 1 || a.N % a.code_div ||
+      a.dtype != DT_BF16 || a.accumulate || a.mask || a.res || a.emask || a.ucode || a.stats || a.bias ||
+      (reinterpret_cast<uintptr_t>(a.out) & 15) || (reinterpret_cast<uintptr_t>(a.w2) & 15) ||
+      (reinterpret_cast<uintptr_t>(a.x) & 15) || (reinterpret_cast<uintptr_t>(a.code) & 7))
+    return -4;
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+  if (ntiles <= 0 || ntiles > 0x7fffffffLL) return -2;
+  hipLaunchKernelGGL(conv3x3_unpool_c64_v2_kernel<true>, dim3((unsigned)std::min<long long>(ntiles, cus)), dim3(512), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// 9-tap shift-add finishing a Z map (see ZOUT above): out[y, x, c] = ReLU(sum_{kh,kw}
+// Z[y+kh-1, x+kw-1, (kh*3+kw)*3 + c]) in fp32, zero padding. One 256-thread workgroup per 16 x 32 output
+// tile: the 18 x 34-px halo of Z (27 used channels of 32, 16-B loads, all in flight before the LDS
+// writes) is staged at a 34-halfword pixel pitch (17 dwords: odd, so the 32 lanes of a row reading
+// consecutive pixels hit distinct banks), each thread sums 2 pixels x 3 channels x 9 taps from LDS.
+// Per-image {sum, sum^2} of the output (the single-pass deprocess) are reduced per workgroup and
+// added with one fp64 atomic pair.
+namespace {
+constexpr int ZS_TH = 16, ZS_TW = 32, ZS_IH = ZS_TH + 2, ZS_IW = ZS_TW + 2;
+constexpr int ZS_PITCH = 34;                               // halfwords per staged pixel
+constexpr int ZS_TASKS = ZS_IH * ZS_IW * 4;                // 16-B chunks (channels 0..31)
+constexpr int ZS_PER_T = (ZS_TASKS + 255) / 256;           // 10
+}  // namespace
+
+__global__ void __launch_bounds__(256) zsum3x3_kernel(const uint16_t* __restrict__ z, float* __restrict__ out, int H,
+                                                      int W, int tiles_x, int tiles_y, double* __restrict__ stats,
+                                                      int stats_div, long long z_elems, long long out_elems) {
+  __shared__ uint32_t zs[ZS_IH * ZS_IW * ZS_PITCH / 2];
+  __shared__ double red[2][4];
+  const int tid = threadIdx.x;
+  const int per_img = tiles_x * tiles_y;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / per_img;
+  const int tr = bid - n * per_img;
+  const int y0 = (tr / tiles_x) * ZS_TH, x0 = (tr % tiles_x) * ZS_TW;
+  uint4 v[ZS_PER_T];
+#pragma unroll
+  for (int q = 0; q < ZS_PER_T; ++q) {
+    const int idx = tid + q * 256;
+    const int p = idx >> 2, ch = idx & 3;
+    const int y = y0 - 1 + p / ZS_IW, x = x0 - 1 + p % ZS_IW;
+    v[q] = make_uint4(0u, 0u, 0u, 0u);
+    const long long off = (((long long)n * H + y) * W + x) * 32 + ch * 8;
+    if (idx < ZS_TASKS && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W &&
+        DV_BOUNDS(off, 8, z_elems, "zsum in"))
+      v[q] = *reinterpret_cast<const uint4*>(z + off);
+  }
+#pragma unroll
+  for (int q = 0; q < ZS_PER_T; ++q) {
+    const int idx = tid + q * 256;
+    if (idx >= ZS_TASKS) continue;
+    const int p = idx >> 2, ch = idx & 3;
+    uint32_t* d = zs + p * (ZS_PITCH / 2) + ch * 4;
+    d[0] = v[q].x;
+    d[1] = v[q].y;
+    d[2] = v[q].z;
+    d[3] = v[q].w;
+  }
+  __syncthreads();
+  const uint16_t* zh = reinterpret_cast<const uint16_t*>(zs);
+  const int lx = tid & 31, ly = tid >> 5;
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ry = ly + 8 * h;
+    float o[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const uint16_t* zp = zh + ((ry + kh) * ZS_IW + lx + kw) * ZS_PITCH + (kh * 3 + kw) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[c] += bf2f(zp[c]);
+      }
+    const int y = y0 + ry, x = x0 + lx;
+    if (y < H && x < W) {
+      const long long pix = ((long long)n * H + y) * W + x;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float r = fmaxf(o[c], 0.f);
+        s1 += r;
+        s2 += (double)r * r;
+        if (DV_BOUNDS(pix * 3 + c, 1, out_elems, "zsum out")) out[pix * 3 + c] = r;
+      }
+    }
+  }
+  if (stats) {
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    const int wave = tid >> 6, lane = tid & 63;
+    if (lane == 0) {
+      red[0][wave] = s1;
+      red[1][wave] = s2;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double* d = stats + 2 * (n / stats_div);
+      atomicAdd(d, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+      atomicAdd(d + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    }
+  }
+}
+
+int zsum3x3_launch(const uint16_t* z, float* out, int N, int H, int W, double* stats, int stats_div, hipStream_t s) {
+  if (N <= 0 || H <= 0 || W <= 0 || (stats && (stats_div < 1 || N % stats_div)) ||
+      (reinterpret_cast<uintptr_t>(z) & 15))
+    return -4;
+  const int tx = (W + ZS_TW - 1) / ZS_TW, ty = (H + ZS_TH - 1) / ZS_TH;
+  const long long nwg = (long long)N * tx * ty;
+  if (nwg > 0x7fffffffLL) return -2;
+  const long long pix = (long long)N * H * W;
+  hipLaunchKernelGGL(zsum3x3_kernel, dim3((unsigned)nwg), dim3(256), 0, s, z, out, H, W, tx, ty, stats, stats_div,
+                     pix * 32, pix * 3);
+  return (int)hipGetLastError();
 }
 
 }  // namespace dv

@@ -62,6 +62,8 @@ struct ConvArgs {
   long long out2_ld;      //   out2[row * out2_ld + col - split_col] instead of out (a merged GEMM whose
   int split_col;          //   leading columns are one consumer's output and the rest another's)
   long long out2_elems;
+  const uint16_t* w2;     // optional second-GEMM weights of a fused epilogue (conv3x3_unpool_z_launch: the
+                          //   next conv-down's taps as a [32][64] matrix, row tap*3+c = W[c][tap][:])
 };
 
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
@@ -160,6 +162,12 @@ int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s);
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, bool* stats_done = nullptr);
 // 3x3 conv 64 -> 64 + bias + ReLU + fused 2x2 max-pool/switch (bf16); < 0 if the shape is unsupported
 int conv3x3_pool_v3_launch(const ConvArgs& a, hipStream_t s);
+// unpool + 3x3 conv 64 -> 64 (ReLU) whose epilogue multiplies the tile by a.w2 ([32][64]): writes the
+// per-tap partial products Z [N, H, W, 32] (bf16, out_ld 32) of the following 64 -> 3 conv-down
+int conv3x3_unpool_z_launch(const ConvArgs& a, hipStream_t s);
+// out[n, y, x, c] = ReLU(sum_taps Z[n, y+kh-1, x+kw-1, (kh*3+kw)*3 + c]) fp32 [N, H, W, 3] + optional
+// per-image {sum, sum^2} (fp64, image n / stats_div): the 3x3 shift-add that finishes a Z map
+int zsum3x3_launch(const uint16_t* z, float* out, int N, int H, int W, double* stats, int stats_div, hipStream_t s);
 // first layer: 3x3 conv of an 8-channel image -> <= 64 channels, bias + ReLU, bf16 (< 0: unsupported)
 int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s);
 // halo-stream 3x3 s1 p1 conv, C % 32 == 0 -> OCpad 64 / 128, 16-bit out or fused 2x2 max-pool +

@@ -219,6 +219,15 @@ class DeconvNet:
             fuse_unpool = (below is not None and below.kind == "pool" and j >= 3 and pending_code is None and
                            cl.dec.cout % 8 == 0 and
                            (not d.is_cuda or self.rt.convs[self.specs[j - 2].name].dec.cin != 64))
+            if pending_code is not None and j == 2 and self.specs[1].kind == "conv" and d.is_cuda:
+                # unpool -> block1_conv2.down -> block1_conv1.down as two kernels (the 64-channel map
+                # stays on chip: ops.deconv_tail); None if the shape is not the kernel's
+                r = ops.deconv_tail(d, pending_code, K, cl.dec, self.rt.convs[self.specs[1].name].dec,
+                                    stats=stats, stats_div=K)
+                if r is not None:
+                    recon = r
+                    pending_code = None
+                    break
             if pending_code is not None:
                 d = ops.conv2d(d, cl.dec, in_mode="unpool", code=pending_code, code_div=K, relu_in=True, **kw)
                 pending_code = None

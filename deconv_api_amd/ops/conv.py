@@ -379,3 +379,71 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
     if epilogue == "pool":
         return out, out_code
     return out
+
+
+# DV_FUSED_TAIL=0 turns off the fused deconvnet tail (unpool -> conv 64->64 -> per-tap products -> shift-add)
+FUSED_TAIL = os.environ.get("DV_FUSED_TAIL", "1") != "0"
+
+
+def tail_w2(last: ConvWeights) -> torch.Tensor:
+    """[32, 64] matrix of a 64 -> 3 (3x3) conv's taps: row (kh*3 + kw)*3 + c = W[c, :, kh, kw]
+    (rows 27..31 zero), in the dtype of the packed GEMM matrix. Cached on ``last``."""
+    w2 = getattr(last, "_tail_w2", None)
+    if w2 is None:
+        w = last.w_oihw.float()  # [3, 64, 3, 3]
+        m = torch.zeros(32, w.shape[1], dtype=torch.float32, device=w.device)
+        m[:27] = w.permute(2, 3, 0, 1).reshape(27, w.shape[1])
+        dt = last.w_gemm.dtype if last.w_gemm is not None else torch.float32
+        w2 = m.to(dt).contiguous()
+        last._tail_w2 = w2
+    return w2
+
+
+def tail_ok(x: torch.Tensor, mid: ConvWeights, last: ConvWeights) -> bool:
+    """Shapes the fused deconvnet tail takes: pooled 64-channel bf16 input, 3x3 64 -> 64 -> 3 downs."""
+    return (FUSED_TAIL and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[3] == 64 and
+            mid.kind == "fwd" and mid.KH == 3 and mid.KW == 3 and mid.cin == 64 and mid.cout == 64 and
+            last.kind == "fwd" and last.KH == 3 and last.KW == 3 and last.cin == 64 and last.cout == 3 and
+            mid.bias is None and last.bias is None)
+
+
+def deconv_tail(x: torch.Tensor, code: torch.Tensor, code_div: int, mid: ConvWeights, last: ConvWeights,
+                stats: Optional[torch.Tensor] = None, stats_div: int = 1) -> Optional[torch.Tensor]:
+    """The deconvnet's last two conv-downs in two kernels (VGG16 block1_conv2.down -> block1_conv1.down):
+    d = ReLU(conv_mid(ReLU(unpool(x, code)))), recon = ReLU(conv_last(d)) as fp32 [N, H, W, 3].
+
+    The 64-channel map d never reaches HBM: the first kernel's epilogue multiplies each bf16 tile of d
+    by the last conv's taps (``tail_w2``: Z = d W2^T, 27 of 32 channels, bf16) on MFMA, and a 9-tap
+    shift-add kernel sums Z over each pixel's neighbourhood (+ ReLU, per-image stats). 64 B/px are
+    written and read instead of 128 (reference: app/deepdream.py:110,260 conv down; :191-209 unpool).
+    Returns None when the device kernel does not take the shape (the caller runs the two convs).
+    """
+    if not tail_ok(x, mid, last):
+        return None
+    N, PH, PW, _ = x.shape
+    z = torch.empty(N, 2 * PH, 2 * PW, 32, dtype=x.dtype, device=x.device)
+    lib = native.lib()
+    if not lib.conv_unpool_z(x.contiguous(), code.contiguous(), int(code_div), mid.w_gemm, tail_w2(last), z):
+        return None
+    out = torch.empty(N, 2 * PH, 2 * PW, 3, dtype=torch.float32, device=x.device)
+    lib.zsum3x3(z, out, stats, int(stats_div))
+    return out
+
+
+def deconv_tail_ref(x: torch.Tensor, code: torch.Tensor, code_div: int, mid: ConvWeights,
+                    last: ConvWeights) -> torch.Tensor:
+    """fp32 oracle of ``deconv_tail`` with the same rounding points (bf16 d, bf16 Z)."""
+    u = torch.relu(unpool_ref(x.float().cpu(), code.cpu(), code_div))
+    wm = mid.w_oihw.to(torch.bfloat16).float().cpu()  # the packed GEMM matrix's rounding
+    d = F.conv2d(u.permute(0, 3, 1, 2), wm, padding=1)
+    d = torch.relu(d).to(torch.bfloat16).float()  # [N, 64, H, W]
+    w2 = tail_w2(last).float().cpu()  # [32, 64]
+    z = torch.einsum("nchw,zc->nzhw", d, w2).to(torch.bfloat16).float()[:, :27]
+    N, _, H, W = z.shape
+    zp = F.pad(z, (1, 1, 1, 1))
+    out = torch.zeros(N, 3, H, W)
+    for kh in range(3):
+        for kw in range(3):
+            t = kh * 3 + kw
+            out += zp[:, t * 3:t * 3 + 3, kh:kh + H, kw:kw + W]
+    return torch.relu(out).permute(0, 2, 3, 1).contiguous()

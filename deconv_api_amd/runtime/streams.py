@@ -44,3 +44,35 @@ def run_parallel(fns: Sequence[Callable[[torch.Tensor], torch.Tensor]], x: torch
         cur.wait_stream(s)
         o.record_stream(cur)
     return outs
+
+
+_copy_streams: Dict[tuple, torch.cuda.Stream] = {}
+
+
+def copy_stream(device: torch.device, cus: int | None = None) -> torch.cuda.Stream:
+    """Long-lived stream for device -> host copies whose dispatches are confined to ``cus`` CUs
+    (``DV_COPY_CUS``, default 8; 0 = an ordinary stream).
+
+    A D2H copy into pinned memory runs as a runtime blit kernel whose waves wait on PCIe writes; on an
+    unrestricted stream it fills every CU for the length of the transfer and the compute stream's next
+    kernel cannot start (measured in ``bench.py``: the 38 us input kernel stretched to 2.7 ms behind the
+    2.8 ms mosaic copy-back, profiles/copyback_overlap_r2.txt). On a CU-masked stream the copy keeps a
+    few CUs and overlaps with compute on the rest."""
+    import os
+
+    idx = torch.device(device).index or 0
+    n = int(os.environ.get("DV_COPY_CUS", "0")) if cus is None else int(cus)
+    key = (idx, n)
+    with _lock:
+        s = _copy_streams.get(key)
+        if s is None:
+            if n > 0:
+                from ..ops import native
+
+                total = torch.cuda.get_device_properties(idx).multi_processor_count
+                handle = native.lib().cu_masked_stream(idx, min(n, total))
+                s = torch.cuda.ExternalStream(handle, device=torch.device("cuda", idx))
+            else:
+                s = torch.cuda.Stream(device=idx)
+            _copy_streams[key] = s
+        return s

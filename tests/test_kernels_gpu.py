@@ -847,3 +847,29 @@ def test_conv_two_destination_epilogue(native_lib, dt, N, H, C, OC, split, relu_
     assert _rel(T, ref[..., split:]) < 1e-2
     Yc = Y.float().cpu()
     assert bool((Yc[..., :40] == 7.0).all()) and bool((Yc[..., 40 + split:] == 7.0).all())  # untouched
+
+
+@pytest.mark.parametrize("N,H,W,div", [(4, 40, 48, 2), (2, 224, 224, 1), (8, 16, 96, 4)])
+def test_deconv_tail_fused(native_lib, N, H, W, div):
+    """Fused deconvnet tail (unpool -> 3x3 conv 64->64 -> ReLU -> per-tap products Z -> 9-tap
+    shift-add -> ReLU, fp32 + per-image stats) vs its fp32 oracle with the same bf16 rounding points,
+    and vs the unfused two-conv path; edge tiles on both kernels (H % 8/16, W % 32 != 0)."""
+    g = torch.Generator().manual_seed(N * H + W)
+    p = _bf(torch.randn(N, H // 2, W // 2, 64, generator=g))
+    code = torch.randint(0, 4, (N // div, H // 2, W // 2, 64), generator=g, dtype=torch.uint8)
+    mid = _cw(64, 64, bias=False, seed=3)
+    last = _cw(3, 64, bias=False, seed=4)
+    ref = ops.deconv_tail_ref(p, code, div, mid, last)
+    midd, lastd = mid.to_device(DEV), last.to_device(DEV)
+    pd, cd = p.to(torch.bfloat16).to(DEV), code.to(DEV)
+    st = torch.full((N // div, 2), 7.0, dtype=torch.float64, device=DEV)
+    got = ops.deconv_tail(pd, cd, div, midd, lastd, stats=st, stats_div=div)
+    assert got is not None and got.shape == (N, H, W, 3)
+    assert _rel(got, ref) < 2e-3
+    yd = got.reshape(N // div, -1).double()
+    assert torch.allclose(st, torch.stack([yd.sum(1), (yd * yd).sum(1)], 1), rtol=1e-9, atol=1e-6)
+    d = ops.conv2d(pd, midd, in_mode="unpool", code=cd, code_div=div, relu_in=True, relu=True, use_bias=False)
+    two = ops.conv2d(d, lastd, relu=True, epilogue="f32", use_bias=False)
+    a, b = got.flatten().double().cpu(), two.flatten().double().cpu()
+    assert float(a @ b / (a.norm() * b.norm())) > 0.9999
+    assert _rel(got, two) < 2e-2
