@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 import time
 
@@ -37,6 +38,8 @@ from deconv_api_amd.engine.deconvnet import DeconvNet
 from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
 from deconv_api_amd.parallel import dist as pdist
 from deconv_api_amd.runtime.streams import copy_stream as copy_stream_for
+
+DEFER_COPY = os.environ.get("DV_BENCH_DEFER_COPY", "0") == "1"  # opt-in until measured on the GPU
 
 # the reference's implied end-to-end rate for layer=block5_conv3 is ~0.03-0.04 img/s
 # (CPU, one request at a time; a lower bound on its cost). We divide by the favourable 0.04.
@@ -145,8 +148,35 @@ def main(argv=None):
     back_done = [None, None]
     lat = []  # (start event, copy-back end event) per timed step
 
+    # DV_BENCH_DEFER_COPY=1: the copy-back of step i's mosaics is issued behind step i+1's input
+    # kernel instead of behind step i. The D2H blit slows memory-bound kernels that run next to it
+    # (the input kernel stretched from 58 us to 2.5 ms) but not MFMA-bound ones
+    # (tools/copy_overlap_probe.py), so deferring it should let it overlap the next step's convs.
+    # Every step's copy still lands inside the timed region.
+    deferred = [None]
+
+    def issue_copy():
+        if deferred[0] is None:
+            return
+        slot, mosaic, ev0 = deferred[0]
+        deferred[0] = None
+        if back_done[slot] is not None:
+            back_done[slot].synchronize()  # host slot free again (its step i-2 copy landed)
+        ready = torch.cuda.Event()
+        ready.record()
+        copy_stream.wait_event(ready)
+        mosaic.record_stream(copy_stream)
+        with torch.cuda.stream(copy_stream):
+            host[slot].copy_(mosaic, non_blocking=True)
+            back_done[slot] = torch.cuda.Event(enable_timing=True)
+            back_done[slot].record()
+        if ev0 is not None:
+            lat.append((ev0, back_done[slot]))
+
     def step(i, ev0=None):
         ops.resize_preprocess(images, xbuf)
+        if cuda and DEFER_COPY:
+            issue_copy()  # step i-1's mosaics
         res = eng.run(xbuf, args.layer, k=args.k)
         slot = i % 2
         if info.backend != "none":
@@ -154,23 +184,16 @@ def main(argv=None):
                 pending[slot].wait()  # the gather that last used this buffer (step i-2)
             pending[slot] = dist.all_gather_into_tensor(gathered[slot], res.mosaic.contiguous(), async_op=True)
         if cuda:
-            if back_done[slot] is not None:
-                back_done[slot].synchronize()  # host slot free again (its step i-2 copy landed)
-            ready = torch.cuda.Event()
-            ready.record()
-            copy_stream.wait_event(ready)
-            res.mosaic.record_stream(copy_stream)
-            with torch.cuda.stream(copy_stream):
-                host[slot].copy_(res.mosaic, non_blocking=True)
-                back_done[slot] = torch.cuda.Event(enable_timing=True)
-                back_done[slot].record()
-            if ev0 is not None:
-                lat.append((ev0, back_done[slot]))
+            deferred[0] = (slot, res.mosaic, ev0)
+            if not DEFER_COPY:
+                issue_copy()
         else:
             host[slot].copy_(res.mosaic)
         return res
 
     def drain():
+        if cuda:
+            issue_copy()  # the last step's copy-back
         for s in (0, 1):
             if pending[s] is not None:
                 pending[s].wait()
