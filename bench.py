@@ -88,7 +88,19 @@ def profile(argv, mode: str) -> int:
     import tempfile
 
     here = os.path.dirname(os.path.abspath(__file__))
-    child = [a for a in (argv if argv is not None else sys.argv[1:]) if a not in ("--profile", "trace", "pmc")]
+    args_in = list(argv if argv is not None else sys.argv[1:])
+    child, skip = [], False
+    for a in args_in:  # drop --profile [mode] / --profile=mode so the child never re-profiles itself
+        if skip:
+            skip = False
+            if a in ("trace", "pmc"):
+                continue
+        if a == "--profile":
+            skip = True
+            continue
+        if a.startswith("--profile="):
+            continue
+        child.append(a)
     out = tempfile.mkdtemp(prefix="dv_prof_", dir=os.environ.get("TMPDIR", "/tmp"))
     cmd = ["rocprofv3", "--kernel-trace", "-d", out, "-o", "bench", "--", sys.executable,
            os.path.join(here, "bench.py"), *child]
@@ -110,7 +122,8 @@ def profile(argv, mode: str) -> int:
 
 def main(argv=None):
     args = parse(argv)
-    if args.profile:
+    if args.profile and os.environ.get("DV_PROFILE_CHILD") != "1":
+        os.environ["DV_PROFILE_CHILD"] = "1"  # inherited by the rocprofv3 child: never recurse
         raise SystemExit(profile(argv, args.profile))
     info = pdist.init(device_type=args.device)
     if info.world != args.gpus:
@@ -141,8 +154,8 @@ def main(argv=None):
     gathered = [torch.empty(info.world * B, 2 * S, 2 * S, 3, dtype=torch.uint8, device=dev) for _ in range(2)]
     pending = [None, None]
     cuda = dev.type == "cuda"
-    # copy-back of every step's mosaics on its own stream into a pinned double buffer
-    # (CU-masked: the D2H blit kernel must not fill the device ahead of the next step's kernels)
+    # copy-back of every step's mosaics on its own stream into a pinned double buffer (an
+    # ordinary stream by default; runtime/streams.py:copy_stream)
     copy_stream = copy_stream_for(dev) if cuda else None
     host = [torch.empty(B, 2 * S, 2 * S, 3, dtype=torch.uint8, pin_memory=cuda) for _ in range(2)]
     back_done = [None, None]

@@ -48,6 +48,9 @@ class Control:
         self.seq = 0
         self.backend = info.backend
         self.hb_timeout = hb_timeout
+        # rebuild a process group even for a world of 1 (tools/rccl_selftest.py --reform: the
+        # abort + re-init path on a real RCCL group with the one GPU a test box has)
+        self.single_pg = False
         self.ack_timeout = ack_timeout
         # keep the default store (hosted by rank 0 in env:// init) alive past destroy_process_group
         self._keep = dist.distributed_c10d._get_default_store()
@@ -111,7 +114,7 @@ class Control:
             if dead or time.time() - t0 > self.ack_timeout:
                 raise PeerLost(dead or pending)
             time.sleep(sleep)
-            sleep = min(sleep * 2, 0.005)
+            sleep = min(sleep * 2, 0.001)
 
     def go(self, kind: str, seq: int) -> None:
         self.store.set(self._k(kind, seq), json.dumps({"op": "go"}))
@@ -148,6 +151,20 @@ class Control:
         msg = self._wait_key(self._k(kind, seq))
         return None if msg.get("op") == "go" else msg
 
+    def reform_announced(self) -> bool:
+        """True once rank 0 announced a re-form after this rank's current command (polled by a
+        follower waiting in a collective: a third rank may have died)."""
+        key = self._k("cmd", self.seq + 1)
+        return bool(self.store.check([key])) and json.loads(self.store.get(key)).get("op") == "reform"
+
+    def wait_reform(self) -> dict:
+        """A follower that saw its collective fail: rank 0's re-form announcement (it follows the
+        current command). Anything else means this rank lost sync with the group."""
+        msg = self._wait_key(self._k("cmd", self.seq + 1))
+        if msg.get("op") != "reform":
+            raise RuntimeError(f"collective failed but rank 0 moved on: {msg!r}")
+        return msg
+
     def follow_reform(self, msg: dict) -> bool:
         """Join the re-formed group; False if this rank is no longer a member."""
         if self.orig not in msg["members"]:
@@ -159,12 +176,21 @@ class Control:
     # ------------------------------------------------------------------ group rebuild
     def _rebuild(self, epoch: int, members: List[int]) -> None:
         if dist.is_initialized():
-            dist.destroy_process_group()
+            if self.backend == "nccl":
+                # abort first: destroying an RCCL communicator with an operation still pending on
+                # a dead peer can block; abort tears the communicator down without waiting for it
+                dist.distributed_c10d._abort_process_group()
+                try:
+                    dist.destroy_process_group()
+                except Exception:  # noqa: BLE001 - already torn down by the abort
+                    pass
+            else:
+                dist.destroy_process_group()
         self.epoch = epoch
         self.members = list(members)
         self.seq = 0
         rank, world = members.index(self.orig), len(members)
-        if world > 1:
+        if world > 1 or self.single_pg:
             kw = dict(backend=self.backend, store=dist.PrefixStore(f"dvpg{epoch}", self.store), rank=rank,
                       world_size=world, timeout=datetime.timedelta(seconds=600))
             if self.backend == "nccl":

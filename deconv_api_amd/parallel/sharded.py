@@ -3,31 +3,47 @@ surviving GPUs (the reference is one blocking worker
 Dockerfile:15).
 
 Planes:
-  * control (parallel/elastic.py): the job's TCPStore. Rank 0 posts a command per batch; every
-    collective is entered only after rank 0 has seen every member acknowledge the step before it
-    and released a "go" key, so no rank ever waits in a collective on a dead peer. Followers
-    publish heartbeats; a missing ack plus a stale heartbeat marks a peer dead;
+  * control (parallel/elastic.py): the job's TCPStore. Rank 0 posts a numbered command stream;
+    each collective is entered only after rank 0 has seen every member acknowledge the command
+    and released a "go" key. Followers publish heartbeats; a missing ack plus a stale heartbeat
+    marks a peer dead;
   * data (RCCL over xGMI; Gloo on CPU): rank 0 resizes the whole batch on its GPU from one staged
     upload (runtime/staging.py) into uint8 224x224x3 (150 KB/image) and ``scatter``s each rank
     only its shard; every rank preprocesses its shard and runs the engine from a captured hipGraph
     per (layer, shard bucket); the uint8 mosaics are ``gather``ed to rank 0 only (1/N of the bytes
     of an all-gather; rank 0 is the only rank that answers HTTP).
 
-Per batch (epoch e, sequence s):
-  rank 0:   cmd -> wait ready(all) -> go1 -> scatter -> compute -> wait done(all) -> go2 -> gather
-  follower: wait cmd -> ready -> wait go1 -> scatter -> compute -> done -> wait go2 -> gather
+Two batches in flight. A batch is two commands, ``run`` (scatter + engine) and ``gather``; rank 0
+issues batch i+1's ``run`` before batch i's ``gather`` whenever i+1 is queued (the service's worker
+does that, serve/service.py), so on every rank the engine work of i+1 is on the compute stream
+while i's mosaics drain:
+  rank 0:   run(i):    cmd -> wait ready(all) -> go1 -> scatter -> engine(i) -> copy to slot i%2
+            gather(i): cmd -> wait done(all) -> go2 -> gather on a side stream that waits only for
+                       batch i's event -> D2H into the staging ring's pinned block
+  follower: run(i):    wait cmd -> ready -> wait go1 -> scatter -> engine(i) -> event(i)
+            gather(i): wait cmd -> event(i).synchronize() (not the whole stream) -> done -> wait go2
+                       -> gather on a side stream behind event(i)
 
-Failure: a follower that dies (or stops heartbeating) is detected while rank 0 waits for an ack.
-Rank 0 then publishes ``reform`` on the keys the survivors wait on, the survivors and rank 0
-tear down the process group and build a new one over the survivors (renumbered, new store
-prefix), and the batch is recomputed on the new world. A local error on rank 0 (bad input,
+Collectives with a dead peer: every collective is issued ``async_op=True`` and polled under a
+deadline together with the heartbeats (rank 0) or the reform announcement (followers), so a rank
+that dies between its ack and the collective (the window the ack protocol alone cannot close) is
+detected instead of blocking rank 0 in RCCL until the process-group timeout. Re-forming then
+ABORTS the communicator (``_abort_process_group``) before building the new group: destroying an
+RCCL group with an operation pending on a dead peer can block (parallel/elastic.py).
+
+Failure: rank 0 publishes ``reform`` on every key a survivor can be waiting on, the survivors and
+rank 0 rebuild the group over the survivors (renumbered, new store prefix), and every batch whose
+commands ran on the old group is recomputed on the new world. A local error on rank 0 (bad input,
 kernel check) fails only that batch; it never degrades the group.
+
+What stays uncovered: a follower that hangs inside a kernel while still heartbeating (its thread
+keeps beating) is only caught by the collective deadline (``ack_timeout``), not by staleness.
 """
 from __future__ import annotations
 
-import json
 import time
-from typing import List, Optional
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
@@ -42,9 +58,25 @@ from .elastic import Control, PeerLost
 log = get_logger("deconv_api_amd.sharded")
 
 
+@dataclass
+class Batch:
+    """A batch whose ``run`` command was issued; ``finish`` gathers it."""
+    layer: str
+    images: List[np.ndarray]
+    epoch: int
+    bid: int = 0
+    mos: Optional[torch.Tensor] = None  # this rank's mosaics (its slot buffer)
+    ev: Optional[torch.cuda.Event] = None  # engine done on the compute stream
+    host: Optional[tuple] = None  # world 1: the copy-back handle
+    staged: Optional[object] = None  # rank 0's staging-ring record (GPU)
+    n: int = 0
+    t: Dict[str, float] = field(default_factory=dict)
+
+
 class ShardedRunner:
     def __init__(self, engine, info: DistInfo, image_size: int = 224, k: int = 4, mode: str = "all",
-                 use_graphs: bool = True, hb_timeout: float = 3.0, ack_timeout: float = 600.0):
+                 use_graphs: bool = True, hb_timeout: float = 3.0, ack_timeout: float = 600.0,
+                 poll_s: float = 0.0001):
         self.engine = engine
         self.info = info
         self.S = image_size
@@ -52,19 +84,28 @@ class ShardedRunner:
         self.mode = mode
         self.batches = 0
         self.reforms = 0
+        self.poll_s = poll_s
+        self.ack_timeout = ack_timeout
         self.last_error: Optional[str] = None
         self.faults = FaultInjector.from_env(info.rank)
         self.ctl = Control(info, hb_timeout=hb_timeout, ack_timeout=ack_timeout) if info.world > 1 else None
         self.graphs = None
-        if use_graphs and info.device.type == "cuda":
+        cuda = info.device.type == "cuda"
+        if use_graphs and cuda:
             from ..engine.graphs import GraphedDeconv
 
             self.graphs = GraphedDeconv(engine, image_size, k, mode)
         self.ring = None
-        if info.device.type == "cuda" and info.rank == 0:
+        if cuda and info.rank == 0:
             from ..runtime.staging import StagingRing
 
             self.ring = StagingRing(info.device)
+        # mosaics of the (at most two) batches in flight: the graph-owned output is overwritten by
+        # the next replay, so each batch's mosaics are copied into its own slot on the compute
+        # stream; the gather runs on ``comm_stream`` behind that batch's event only
+        self.slots: List[Optional[torch.Tensor]] = [None, None]
+        self.comm_stream = torch.cuda.Stream(info.device) if cuda else None
+        self._bid = 0
 
     @property
     def world(self) -> int:
@@ -76,17 +117,17 @@ class ShardedRunner:
         return self.reforms > 0
 
     # ----------------------------------------------------------------- shared compute
-    def _resize_u8(self, images: List[np.ndarray], npad: int) -> torch.Tensor:
-        """rank 0: all images -> uint8 [npad, S, S, 3] (zero rows pad to npad) on this rank's device."""
+    def _resize_u8(self, images: List[np.ndarray], npad: int):
+        """rank 0: all images -> uint8 [npad, S, S, 3] (zero rows pad to npad) on this rank's
+        device; returns (tensor, staging record or None)."""
         S = self.S
         if self.ring is not None:
             out = torch.zeros(npad, S, S, 3, dtype=torch.uint8, device=self.info.device)
-            self.ring.stage(images, out)
-            return out
+            return out, self.ring.stage(images, out)
         out = torch.zeros(npad, S, S, 3, dtype=torch.uint8)
         for b, img in enumerate(images):
             out[b] = torch.from_numpy(ops.resize_u8_ref(img, S, S))
-        return out
+        return out, None
 
     def _preprocess(self, u8: torch.Tensor) -> torch.Tensor:
         if u8.is_cuda:
@@ -103,65 +144,159 @@ class ShardedRunner:
 
     def _local(self, layer: str, images: List[np.ndarray]) -> torch.Tensor:
         """Single-process reference of a batch (tests, and the world-1 path)."""
-        u8 = self._resize_u8(images, len(images))
+        u8, _ = self._resize_u8(images, len(images))
         return self._engine(self._preprocess(u8), layer)
+
+    def _keep(self, bid: int, mos: torch.Tensor) -> tuple:
+        """Copy this batch's mosaics into its slot (stream order) and record its done event."""
+        if not mos.is_cuda:
+            return mos.clone(), None
+        s = bid % 2
+        if self.slots[s] is None or self.slots[s].shape != mos.shape:
+            self.slots[s] = torch.empty_like(mos)
+        self.slots[s].copy_(mos)
+        ev = torch.cuda.Event()
+        ev.record()
+        return self.slots[s], ev
+
+    def _await(self, work, what: str, follower: bool = False) -> None:
+        """Poll an async collective under the ack deadline. Rank 0 checks the followers'
+        heartbeats; a follower checks for a reform announcement (rank 0 saw a peer die)."""
+        t0 = last = time.time()
+        sleep = self.poll_s
+        while True:
+            try:
+                if work.is_completed():
+                    work.wait()  # re-raises a transport error (e.g. Gloo: peer closed its socket)
+                    return
+            except RuntimeError as e:
+                if follower:
+                    raise PeerLost([]) from e
+                raise PeerLost(self._which_dead()) from e
+            now = time.time()
+            if now - last > 0.02:  # store round trips only every 20 ms; the work poll is local
+                last = now
+                if follower:
+                    if self.ctl.reform_announced():
+                        raise PeerLost([])
+                else:
+                    dead = self.ctl.stale()
+                    if dead:
+                        raise PeerLost(dead)
+                if now - t0 > self.ack_timeout:
+                    raise PeerLost([] if follower else list(self.ctl.members[1:]))
+            time.sleep(sleep)
+            sleep = min(sleep * 2, 0.002)
+
+    def _which_dead(self) -> List[int]:
+        """rank 0 after a transport error: the error arrives before the dead peer's heartbeat has
+        gone stale, so wait up to two heartbeat timeouts for it to (every follower if none does)."""
+        t_end = time.time() + 2 * self.ctl.hb_timeout
+        while time.time() < t_end:
+            dead = self.ctl.stale()
+            if dead:
+                return dead
+            time.sleep(0.05)
+        return list(self.ctl.members[1:])
 
     # ----------------------------------------------------------------- rank 0
     def run(self, layer: str, images: List[np.ndarray]) -> np.ndarray:
         return self.finish(self.launch(layer, images))
 
-    def launch(self, layer: str, images: List[np.ndarray]):
-        """rank 0: run the batch's control steps and collectives and enqueue the mosaics' copy to
-        pinned host memory; returns a handle for ``finish`` (the D2H may still be in flight, so
-        the service's worker can start the next batch while this one drains)."""
+    def launch(self, layer: str, images: List[np.ndarray]) -> Batch:
+        """rank 0: scatter the batch and enqueue its engine work on every rank; ``finish`` gathers
+        it. Another batch may be launched before this one is finished (two in flight)."""
         assert self.info.rank == 0
         self.batches += 1
         while True:
+            b = Batch(layer, images, self.ctl.epoch if self.ctl else 0, self._bid, n=len(images))
+            self._bid += 1
             if self.world == 1:
                 self.faults.on_batch()
-                return self._to_host(self._local(layer, images), len(images))
+                u8, st = self._resize_u8(images, len(images))
+                mos = self._engine(self._preprocess(u8), layer)
+                b.host = self._copy_back(st, mos, len(images))
+                return b
             try:
-                return self._run_group(layer, images)
+                self._run_cmd(b)
+                return b
             except PeerLost as e:
-                self.last_error = repr(e)
-                log.error("peer lost, re-forming over the survivors", extra={"fields": {"dead": e.dead}})
-                self.ctl.reform(e.dead)
-                self.reforms += 1
+                self._reform(e)
 
-    @staticmethod
-    def _to_host(mos: torch.Tensor, n: int):
+    def finish(self, b: Batch) -> np.ndarray:
+        """rank 0: gather batch ``b``'s mosaics (recomputed on the survivors if the group was
+        re-formed since its launch) -> uint8 [n, 2S, 2S, 3] on the host."""
+        while True:
+            if b.host is not None:
+                return self._host(b.host)
+            if b.epoch != self.ctl.epoch:  # launched on a group that no longer exists
+                b = self.launch(b.layer, b.images)
+                continue
+            try:
+                self._gather_cmd(b)
+            except PeerLost as e:
+                self._reform(e)
+
+    def _reform(self, e: PeerLost) -> None:
+        self.last_error = repr(e)
+        log.error("peer lost, re-forming over the survivors", extra={"fields": {"dead": e.dead}})
+        self.ctl.reform(e.dead)
+        self.reforms += 1
+        self.slots = [None, None]
+
+    def _run_cmd(self, b: Batch) -> None:
+        n = len(b.images)
+        per = shard_sizes(n, self.world)[0]
+        ctl = self.ctl
+        seq = ctl.post_cmd({"op": "run", "layer": b.layer, "n": n, "per": per, "b": b.bid})
+        u8, b.staged = self._resize_u8(b.images, per * self.world)  # overlaps the followers' acks
+        ctl.wait_acks("ready", seq)
+        ctl.go("go1", seq)
+        shard = torch.empty(per, self.S, self.S, 3, dtype=torch.uint8, device=u8.device)
+        self._await(dist.scatter(shard, scatter_list=list(u8.chunk(self.world)), src=0, async_op=True), "scatter")
+        self.faults.on_batch()
+        b.mos, b.ev = self._keep(b.bid, self._engine(self._preprocess(shard), b.layer).contiguous())
+
+    def _gather_cmd(self, b: Batch) -> None:
+        ctl = self.ctl
+        seq = ctl.post_cmd({"op": "gather", "b": b.bid})
+        ctl.wait_acks("done", seq)
+        ctl.go("go2", seq)
+        parts = [torch.empty_like(b.mos) for _ in range(self.world)]
+        if self.comm_stream is not None:
+            self.comm_stream.wait_event(b.ev)
+            with torch.cuda.stream(self.comm_stream):
+                work = dist.gather(b.mos, gather_list=parts, dst=0, async_op=True)
+                self._await(work, "gather")
+                full = torch.cat(parts)
+                ev = torch.cuda.Event()
+                ev.record()
+            torch.cuda.current_stream().wait_event(ev)
+            full.record_stream(torch.cuda.current_stream())
+        else:
+            self._await(dist.gather(b.mos, gather_list=parts, dst=0, async_op=True), "gather")
+            full = torch.cat(parts)
+        b.host = self._copy_back(b.staged, full, b.n)
+
+    def _copy_back(self, st, mos: torch.Tensor, n: int) -> tuple:
         if not mos.is_cuda:
             return ("host", mos[:n].numpy())
+        if st is not None and self.ring is not None:  # reuse the staging ring's slot + stream
+            st.n = n
+            return ("staged", self.ring.copy_back(st, mos))
         host = torch.empty((n, *mos.shape[1:]), dtype=mos.dtype, pin_memory=True)
         host.copy_(mos[:n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return ("event", ev, host)
 
-    @staticmethod
-    def finish(handle) -> np.ndarray:
-        if handle[0] == "host":
-            return handle[1]
-        handle[1].synchronize()
-        return handle[2].numpy()
-
-    def _run_group(self, layer: str, images: List[np.ndarray]):
-        n = len(images)
-        per = shard_sizes(n, self.world)[0]
-        ctl = self.ctl
-        seq = ctl.post_cmd({"op": "run", "layer": layer, "n": n, "per": per})
-        u8 = self._resize_u8(images, per * self.world)  # overlaps the followers' acks
-        ctl.wait_acks("ready", seq)
-        ctl.go("go1", seq)
-        shard = torch.empty(per, self.S, self.S, 3, dtype=torch.uint8, device=u8.device)
-        dist.scatter(shard, scatter_list=list(u8.chunk(self.world)), src=0)
-        self.faults.on_batch()
-        mos = self._engine(self._preprocess(shard), layer).contiguous()
-        ctl.wait_acks("done", seq)
-        ctl.go("go2", seq)
-        parts = [torch.empty_like(mos) for _ in range(self.world)]
-        dist.gather(mos, gather_list=parts, dst=0)
-        return self._to_host(torch.cat(parts), n)
+    def _host(self, h: tuple) -> np.ndarray:
+        if h[0] == "host":
+            return h[1]
+        if h[0] == "staged":
+            return self.ring.finish(h[1])
+        h[1].synchronize()
+        return h[2].numpy()
 
     def ping(self) -> bool:
         """Idle liveness check: re-forms the group if a follower stopped heartbeating."""
@@ -182,39 +317,59 @@ class ShardedRunner:
 
     # ----------------------------------------------------------------- followers
     def follow(self) -> int:
-        """Serve rank 0's batches until 'stop' (or until dropped from the group). Returns the
-        number of batches run."""
+        """Serve rank 0's command stream until 'stop' (or until dropped from the group). Returns
+        the number of batches gathered."""
         assert self.info.rank != 0
         ctl = self.ctl
         done = 0
+        runs = 0
+        pending: Dict[int, tuple] = {}  # batch id -> (mosaics slot, event)
+        dev = self.info.device
         while True:
             seq, msg = ctl.wait_cmd()
-            if msg["op"] == "stop":
+            op = msg["op"]
+            if op == "stop":
                 ctl.close()
                 return done
-            if msg["op"] == "reform":
-                if not ctl.follow_reform(msg):
-                    return done
-                continue
-            per = msg["per"]
-            dev = self.info.device
-            ctl.ack("ready", seq)
-            r = ctl.wait_go("go1", seq)
-            if r is not None:  # reform announced instead of go
+            try:
+                if op == "reform":
+                    raise PeerLost([])
+                if op == "run":
+                    runs += 1
+                    ctl.ack("ready", seq)
+                    self.faults.at("ready", runs)  # fault window: acked, then gone before the scatter
+                    self._go(ctl, "go1", seq)
+                    shard = torch.empty(msg["per"], self.S, self.S, 3, dtype=torch.uint8, device=dev)
+                    self._await(dist.scatter(shard, scatter_list=None, src=0, async_op=True), "scatter", True)
+                    self.faults.on_batch()
+                    mos = self._engine(self._preprocess(shard), msg["layer"]).contiguous()
+                    pending[msg["b"]] = self._keep(msg["b"], mos)
+                    continue
+                if op == "gather":
+                    mos, ev = pending.pop(msg["b"])
+                    if ev is not None:
+                        ev.synchronize()  # this batch's engine work only, not the whole stream
+                    ctl.ack("done", seq)
+                    self.faults.at("done", runs)  # fault window: acked, then gone before the gather
+                    self._go(ctl, "go2", seq)
+                    if self.comm_stream is not None:
+                        self.comm_stream.wait_event(ev)
+                        with torch.cuda.stream(self.comm_stream):
+                            self._await(dist.gather(mos, gather_list=None, dst=0, async_op=True), "gather", True)
+                    else:
+                        self._await(dist.gather(mos, gather_list=None, dst=0, async_op=True), "gather", True)
+                    done += 1
+                    continue
+                raise RuntimeError(f"unknown command {msg!r}")
+            except PeerLost:
+                r = msg if op == "reform" else ctl.wait_reform()
+                pending.clear()
+                self.slots = [None, None]
                 if not ctl.follow_reform(r):
                     return done
-                continue
-            shard = torch.empty(per, self.S, self.S, 3, dtype=torch.uint8, device=dev)
-            dist.scatter(shard, scatter_list=None, src=0)
-            self.faults.on_batch()
-            mos = self._engine(self._preprocess(shard), msg["layer"]).contiguous()
-            if mos.is_cuda:
-                torch.cuda.current_stream(dev).synchronize()
-            ctl.ack("done", seq)
-            r = ctl.wait_go("go2", seq)
-            if r is not None:
-                if not ctl.follow_reform(r):
-                    return done
-                continue
-            dist.gather(mos, gather_list=None, dst=0)
-            done += 1
+
+    @staticmethod
+    def _go(ctl: Control, kind: str, seq: int) -> None:
+        r = ctl.wait_go(kind, seq)
+        if r is not None:  # reform announced instead of go
+            raise PeerLost([])

@@ -77,6 +77,9 @@ class StagingRing:
         self.tab_dev = torch.empty(slots, max_images, 4, dtype=torch.int64, device=device)
         self.out_dev: List[Optional[torch.Tensor]] = [None] * slots
         self.busy: List[Optional[Staged]] = [None] * slots  # the batch last staged in each slot
+        # per slot: recorded on the compute stream right after the slot's resize launch, the last
+        # reader of its device blob and table; the next upload into the slot waits for that only
+        self.resized: List[Optional[torch.cuda.Event]] = [None] * slots
         self._next = 0
         self._lock = threading.Lock()
         for i in range(slots):
@@ -121,7 +124,10 @@ class StagingRing:
         st = Staged(i, n, torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
                     torch.cuda.Event(enable_timing=True))
         cur = torch.cuda.current_stream(self.device)
-        self.copy_stream.wait_stream(cur)  # `out` / previous users of the slot's device blob
+        if self.resized[i] is not None:
+            # the slot's previous resize must have read its blob; NOT wait_stream(cur), which would
+            # also wait for the previous batch's engine work and serialize upload behind compute
+            self.copy_stream.wait_event(self.resized[i])
         with torch.cuda.stream(self.copy_stream):
             st.ev_h2d0.record()
             self.dev[i][:end].copy_(self.host[i][:end], non_blocking=True)
@@ -130,6 +136,9 @@ class StagingRing:
         cur.wait_event(st.ev_h2d1)
         st.ev_comp0.record(cur)
         native.lib().resize_batch(self.dev[i], self.tab_dev[i, :n], out[:n], end)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self.resized[i] = ev
         self.busy[i] = st
         return st
 

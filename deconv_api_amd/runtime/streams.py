@@ -50,14 +50,15 @@ _copy_streams: Dict[tuple, torch.cuda.Stream] = {}
 
 
 def copy_stream(device: torch.device, cus: int | None = None) -> torch.cuda.Stream:
-    """Long-lived stream for device -> host copies whose dispatches are confined to ``cus`` CUs
-    (``DV_COPY_CUS``, default 8; 0 = an ordinary stream).
+    """Long-lived stream for device -> host copies; with ``cus`` > 0 (``DV_COPY_CUS``) its
+    dispatches are confined to that many CUs. Default 0: an ordinary, unmasked stream (CU masking
+    was measured slower end to end, profiles/bench_c2_blit_wg_ab_r2.txt; opt-in for A/B only).
 
     A D2H copy into pinned memory runs as a runtime blit kernel whose waves wait on PCIe writes; on an
     unrestricted stream it fills every CU for the length of the transfer and the compute stream's next
     kernel cannot start (measured in ``bench.py``: the 38 us input kernel stretched to 2.7 ms behind the
     2.8 ms mosaic copy-back, profiles/copyback_overlap_r2.txt). On a CU-masked stream the copy keeps a
-    few CUs and overlaps with compute on the rest."""
+    few CUs and overlaps with compute on the rest, but the copy then takes longer than it hides."""
     import os
 
     idx = torch.device(device).index or 0

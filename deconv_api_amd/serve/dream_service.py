@@ -11,10 +11,11 @@ repeating the last image so the per-(B, H, W) hipGraph cache sees few distinct b
 from __future__ import annotations
 
 import asyncio
+import collections
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Deque, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -65,7 +66,9 @@ class DreamService:
         self._worker: Optional[threading.Thread] = None
         self.max_batch = max(1, self.cfg.dream_max_batch)
         self.window_s = max(0.0, self.cfg.dream_window_ms) / 1e3
-        self.batches: List[int] = []  # real (unpadded) size of every batch run, for tests/metrics
+        # real (unpadded) sizes of the most recent batches, for tests (bounded: a long-running
+        # service must not grow it; M.BATCH_SIZE keeps the full histogram)
+        self.batches: Deque[int] = collections.deque(maxlen=1024)
 
     # ------------------------------------------------------------------ engines
     @staticmethod

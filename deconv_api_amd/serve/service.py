@@ -175,9 +175,9 @@ class DeconvService:
         self.codec.shutdown()
 
     # ------------------------------------------------------------------ GPU worker
-    def _collect(self) -> List[_Job]:
+    def _collect(self, wait_s: float = 0.1) -> List[_Job]:
         try:
-            first = self.q.get(timeout=0.1)
+            first = self.q.get(timeout=wait_s) if wait_s > 0 else self.q.get_nowait()
         except queue.Empty:
             return []
         jobs = [first]
@@ -207,9 +207,17 @@ class DeconvService:
             if self.ring is not None:  # all engine work of this thread on the ring's compute stream
                 torch.cuda.set_stream(self.ring.compute_stream)
         last_beat = time.perf_counter()
+        # multi-GPU: the batch launched last (scattered, engine enqueued on every rank) but not yet
+        # gathered. It is gathered right after the NEXT batch is launched, or as soon as no batch is
+        # queued, so every rank computes batch i+1 while batch i's mosaics drain (two in flight)
+        inflight = None
         while not self._stop.is_set():
-            jobs = self._collect()
+            jobs = self._collect(0.0 if inflight is not None else 0.1)
             if not jobs:
+                if inflight is not None:
+                    self._runner_finish(inflight)
+                    inflight = None
+                    continue
                 if self.runner is not None and time.perf_counter() - last_beat > 10.0:
                     self.runner.ping()  # idle heartbeat to the follower ranks
                     last_beat = time.perf_counter()
@@ -225,11 +233,27 @@ class DeconvService:
                 try:
                     for j in group:
                         j.t_launch = t0
+                    if self.runner is not None:
+                        b = self.runner.launch(layer, [j.image for j in group])
+                        if inflight is not None:
+                            self._runner_finish(inflight)
+                        inflight = (b, group, layer, t0)
+                        continue
                     handle = self.launch_batch(layer, [j.image for j in group])
                     self.done_q.put((handle, group, layer, t0))
                 except Exception as e:  # noqa: BLE001 - delivered to every waiting request
                     self._batch_t0 = None
                     self._fail(group, e)
+        if inflight is not None:
+            self._runner_finish(inflight)
+
+    def _runner_finish(self, item) -> None:
+        b, group, layer, t0 = item
+        try:
+            self.done_q.put((("host", self.runner.finish(b)), group, layer, t0))
+        except Exception as e:  # noqa: BLE001
+            self._batch_t0 = None
+            self._fail(group, e)
 
     def _complete(self):
         """Waits for each batch's copy-back in launch order, then hands the batch to the encode

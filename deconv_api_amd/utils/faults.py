@@ -4,6 +4,9 @@
   raise@3        the 3rd engine batch on this process raises RuntimeError
   hang@2:5       the 2nd batch sleeps 5 s before running (watchdog / timeout tests)
   exit@2/rank=1  rank 1 terminates (os._exit(17)) when its 2nd batch arrives (failover tests)
+  exit_ready@2   terminates right after acknowledging its 2nd batch, before entering the scatter
+  exit_done@2    terminates right after acknowledging that its 2nd batch is computed, before the
+                 gather (the two windows the ack protocol alone cannot close, parallel/sharded.py)
 Batches are counted per process from 1.
 """
 from __future__ import annotations
@@ -38,7 +41,7 @@ def parse(spec: str) -> List[Fault]:
         if ":" in rest:
             rest, a = rest.split(":")
             arg = float(a)
-        if action not in ("raise", "hang", "exit"):
+        if action not in ("raise", "hang", "exit", "exit_ready", "exit_done"):
             raise ValueError(f"unknown fault action {action!r}")
         out.append(Fault(action, int(rest), arg, rank))
     return out
@@ -64,4 +67,10 @@ class FaultInjector:
             if f.action == "hang":
                 time.sleep(f.arg)
             if f.action == "exit":
+                os._exit(17)
+
+    def at(self, point: str, batch: int) -> None:
+        """Named fault point of batch ``batch`` (``exit_<point>@<batch>``)."""
+        for f in self.faults:
+            if f.action == f"exit_{point}" and f.batch == batch and (f.rank is None or f.rank == self.rank):
                 os._exit(17)

@@ -271,3 +271,77 @@ def test_tiled_dream_units_across_ranks():
         # step (0.01) bounds the effect
         d = np.abs(out - ref)
         assert d.mean() < 1e-4 and d.max() < 2e-2, (d.mean(), d.max())
+
+
+def _worker_inflight(rank, world, port, q, fault):
+    try:
+        if fault:
+            os.environ["DV_FAULT"] = fault
+        from deconv_api_amd.engine.deconvnet import DeconvNet
+        from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
+        from deconv_api_amd.parallel.sharded import ShardedRunner
+
+        info = _init(rank, world, port)
+        specs = vgg16_specs(width_div=8, image_size=32, fc=64, classes=10)
+        eng = DeconvNet(VGG16.random(0, specs=specs).build("cpu", torch.float32))
+        runner = ShardedRunner(eng, info, image_size=32, hb_timeout=1.0)
+        if rank == 0:
+            rng = np.random.default_rng(3)
+            sets = [[rng.integers(0, 256, (32 + i, 30, 3), dtype=np.uint8) for i in range(n)] for n in (5, 4, 3, 6)]
+            layers = ["block2_conv1", "block3_conv2", "block1_pool", "block2_conv1"]
+            # launch i+1 before finishing i (the service worker's order): two batches in flight
+            outs = [None] * 4
+            prev = runner.launch(layers[0], sets[0])
+            for i in range(1, 4):
+                cur = runner.launch(layers[i], sets[i])
+                outs[i - 1] = runner.finish(prev)
+                prev = cur
+            outs[3] = runner.finish(prev)
+            single = ShardedRunner(eng, type(info)(), image_size=32)
+            same = [bool(np.array_equal(o, single._local(l, s).numpy())) for o, l, s in zip(outs, layers, sets)]
+            world_after = runner.world
+            runner.stop()
+            q.put((rank, same, world_after, runner.reforms))
+        else:
+            n = runner.follow()
+            q.put((rank, "follower returned", n, runner.world))
+        from deconv_api_amd.parallel import dist as pdist
+
+        pdist.shutdown()
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None))
+
+
+@pytest.mark.parametrize("fault", ["", "exit_ready@2/rank=2", "exit_done@3/rank=1"])
+def test_two_batches_in_flight(fault):
+    """Rank 0 launches batch i+1 before gathering batch i (world 3): every batch equals the single-
+    process result bit for bit. With a fault, a follower dies in one of the windows between its ack
+    and the collective (after acking 'ready' of its 2nd run / 'done' of its 3rd): rank 0 detects it
+    inside the polled collective, the survivors re-form, and every batch launched on the old group is
+    recomputed on the new one."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_inflight, args=(r, world, port, q, fault)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world - (1 if fault else 0)):
+        r = q.get(timeout=300)
+        res[r[0]] = r
+    for p in ps:
+        p.join(timeout=60)
+    assert 0 in res, res
+    r0 = res[0]
+    assert isinstance(r0[1], list), r0
+    assert r0[1] == [True] * 4, r0
+    if fault:
+        dead = int(fault.split("rank=")[1])
+        assert ps[dead].exitcode == 17
+        assert r0[2] == world - 1 and r0[3] == 1, r0
+    else:
+        assert r0[2] == world and r0[3] == 0, r0
+        assert all(res[r][2] == 4 for r in range(1, world)), res

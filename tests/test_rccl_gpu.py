@@ -39,6 +39,14 @@ def test_rccl_collectives_selftest():
 
 
 @pytest.mark.gpu
+def test_rccl_reform_aborts_and_rebuilds():
+    """The failover's re-form path on a real RCCL group (world 1, same membership): abort the
+    communicator with a collective in flight, build the new group, run a collective on it."""
+    out = _torchrun(["tools/rccl_selftest.py", "--reform"])
+    assert out["backend"] == "nccl" and out["reform_epoch"] == 1 and out["reform_all_reduce"] is True, out
+
+
+@pytest.mark.gpu
 def test_bench_under_torchrun_uses_rccl():
     out = _torchrun(["bench.py", "--gpus", "1", "--steps", "2", "--warmup", "1", "--batch", "8"])
     assert out["process_group"] == "nccl" and out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1"

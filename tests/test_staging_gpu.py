@@ -35,3 +35,26 @@ def test_staging_ring_matches_per_image_resize(native_lib):
         handles.append((ring.copy_back(st, mos), mos.cpu().numpy()))
     for st, ref in handles:  # results stay valid after their slot was reused
         assert np.array_equal(ring.finish(st), ref)
+
+
+def test_staging_upload_overlaps_engine_work(native_lib):
+    """A slot's next upload waits only for that slot's previous resize (per-slot event), not for
+    everything queued on the compute stream: batch i+2's H2D completes while batch i+1's 'engine'
+    (a long sleep kernel) still runs."""
+    from deconv_api_amd.runtime.staging import StagingRing
+
+    dev = torch.device("cuda", 0)
+    ring = StagingRing(dev, slots=2, slot_bytes=1 << 20, max_images=4)
+    rng = np.random.default_rng(1)
+    imgs = [rng.integers(0, 256, (240, 260, 3), dtype=np.uint8) for _ in range(3)]
+    xs = [torch.empty(3, 224, 224, 8, dtype=torch.bfloat16, device=dev) for _ in range(3)]
+    with torch.cuda.stream(ring.compute_stream):
+        ring.stage(imgs, xs[0])
+        ring.stage(imgs, xs[1])
+        torch.cuda._sleep(400_000_000)  # stands in for the engine: ~0.2 s of one busy wave
+        st = ring.stage(imgs, xs[2])  # slot 0 again
+        st.ev_h2d1.synchronize()
+        overlapped = not ring.compute_stream.query()
+        torch.cuda.synchronize()
+    assert overlapped
+    assert torch.equal(xs[2], xs[0])

@@ -39,11 +39,34 @@ def main():
     dist.gather(shard, gather_list=parts, dst=0)
     gath_ok = torch.equal(torch.cat(parts), src) if info.rank == 0 else True
     torch.cuda.synchronize()
+    out = {"backend": info.backend, "world": info.world, "broadcast_state": bcast_ok,
+           "all_gather_rows": gather_ok, "all_reduce_max": mx == info.world - 0.5,
+           "scatter": scatter_ok, "gather": gath_ok}
+    if "--reform" in sys.argv:
+        out.update(reform(info))
     if info.rank == 0:
-        print(json.dumps({"backend": info.backend, "world": info.world, "broadcast_state": bcast_ok,
-                          "all_gather_rows": gather_ok, "all_reduce_max": mx == info.world - 0.5,
-                          "scatter": scatter_ok, "gather": gath_ok}), flush=True)
+        print(json.dumps(out), flush=True)
     pdist.shutdown()
+
+
+def reform(info):
+    """The serving failover's group rebuild on RCCL: an async collective is in flight, the
+    communicator is ABORTED (parallel/elastic.py:_rebuild) and a new group is built over the same
+    membership under a new store prefix; collectives then run on the new group."""
+    from deconv_api_amd.parallel.elastic import Control
+
+    ctl = Control(info, hb_timeout=5.0)
+    ctl.single_pg = True
+    t = torch.ones(1 << 20, device=info.device)
+    work = dist.all_reduce(t, async_op=True)
+    ctl._rebuild(ctl.epoch + 1, list(ctl.members))
+    del work
+    y = torch.full((4,), 2.0, device=info.device)
+    dist.all_reduce(y)
+    torch.cuda.synchronize()
+    ok = bool(torch.all(y == 2.0 * info.world)) and dist.is_initialized() and dist.get_backend() == "nccl"
+    ctl.close()
+    return {"reform_epoch": ctl.epoch, "reform_all_reduce": ok}
 
 
 if __name__ == "__main__":
