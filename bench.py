@@ -39,7 +39,13 @@ from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
 from deconv_api_amd.parallel import dist as pdist
 from deconv_api_amd.runtime.streams import copy_stream as copy_stream_for
 
-DEFER_COPY = os.environ.get("DV_BENCH_DEFER_COPY", "0") == "1"  # opt-in until measured on the GPU
+# Where each step's mosaic copy-back (of the PREVIOUS step) is issued: right before this layer's
+# forward conv (DV_BENCH_COPY_AT; "" = right after the step that produced it). The D2H copy runs as
+# a blit kernel that waits on PCIe (154 MB, ~2.8 ms); next to memory-bound kernels it slows them
+# (the 58 us input kernel took 2.3 ms beside it, profiles/copyback_overlap_r2.txt), next to MFMA-
+# bound ones it costs little (tools/copy_overlap_probe.py: a GEMM loop 9.06 -> 9.18 ms). block3's
+# convs are the first MFMA-bound layers of the step.
+COPY_AT = os.environ.get("DV_BENCH_COPY_AT", "block3_conv1")
 
 # the reference's implied end-to-end rate for layer=block5_conv3 is ~0.03-0.04 img/s
 # (CPU, one request at a time; a lower bound on its cost). We divide by the favourable 0.04.
@@ -161,11 +167,9 @@ def main(argv=None):
     back_done = [None, None]
     lat = []  # (start event, copy-back end event) per timed step
 
-    # DV_BENCH_DEFER_COPY=1: the copy-back of step i's mosaics is issued behind step i+1's input
-    # kernel instead of behind step i. The D2H blit slows memory-bound kernels that run next to it
-    # (the input kernel stretched from 58 us to 2.5 ms) but not MFMA-bound ones
-    # (tools/copy_overlap_probe.py), so deferring it should let it overlap the next step's convs.
-    # Every step's copy still lands inside the timed region.
+    # the copy-back of step i's mosaics is issued from step i+1's forward (COPY_AT hook) or, if the
+    # target comes before that layer, right after step i+1 is enqueued; every copy still lands
+    # inside the timed region (drain)
     deferred = [None]
 
     def issue_copy():
@@ -188,9 +192,10 @@ def main(argv=None):
 
     def step(i, ev0=None):
         ops.resize_preprocess(images, xbuf)
-        if cuda and DEFER_COPY:
-            issue_copy()  # step i-1's mosaics
-        res = eng.run(xbuf, args.layer, k=args.k)
+        hook = (COPY_AT, issue_copy) if cuda and COPY_AT else None
+        res = eng.run(xbuf, args.layer, k=args.k, hook=hook)
+        if cuda:
+            issue_copy()  # no-op when the hook already issued step i-1's copy
         slot = i % 2
         if info.backend != "none":
             if pending[slot] is not None:
@@ -198,7 +203,7 @@ def main(argv=None):
             pending[slot] = dist.all_gather_into_tensor(gathered[slot], res.mosaic.contiguous(), async_op=True)
         if cuda:
             deferred[0] = (slot, res.mosaic, ev0)
-            if not DEFER_COPY:
+            if not COPY_AT:
                 issue_copy()
         else:
             host[slot].copy_(res.mosaic)

@@ -85,10 +85,20 @@ def main(argv=None):
             "data": "synthetic uint8 images, seeded random-init weights", "hip_graphs": not a.no_graphs,
             "finite": bool(torch.isfinite(out).all()),
             "sub_batch_streams": dd.split if dd.fused else 1,
+            **(_tile_info(dd) if a.tile else {}),
             "config": {"model": a.model, "batch": a.batch, "image_size": a.size, "tile": a.tile,
                        "parallelism": f"{'tiles' if a.tile else 'dp'}{info.world}"},
         }), flush=True)
     pdist.shutdown()
+
+
+def _tile_info(dd) -> dict:
+    """how the tiled octaves ran: whole-octave graphs (collectives captured inside when the
+    collective path is on) vs per-step graphs with eager collectives"""
+    sts = [st for st in dd._tgraphs.values() if hasattr(st, "graph")]
+    return {"tile_octave_graphs": sum(st.graph is not None for st in sts),
+            "tile_step_graph_octaves": sum(st.step_graph is not None for st in sts),
+            "tile_collective": any(dd._collective(st) for st in sts)}
 
 
 if __name__ == "__main__":

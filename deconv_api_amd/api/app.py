@@ -129,6 +129,8 @@ def create_app(service=None, cfg: Optional[Config] = None, dream_service=None) -
             return JSONResponse(status_code=503, content={"ready": False, "reason": "service not started"})
         st = svc.status()
         ok = st.get("worker_alive", False)
+        if state["dream"] is not None and hasattr(state["dream"], "status"):
+            st["deepdream"] = state["dream"].status()  # world it runs tiled across, tile size
         return JSONResponse(status_code=200 if ok else 503, content={"ready": ok, **st})
 
     @app.get("/metrics")

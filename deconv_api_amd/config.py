@@ -51,6 +51,8 @@ class Config:
     resnet_weights: str = ""             # /deepdream ResNet-50: same
     dream_max_batch: int = 8              # /deepdream: same-shape requests run as one DeepDream batch
     dream_window_ms: float = 20.0         # /deepdream: how long the worker waits to fill a batch
+    dream_tile: int = 512                 # /deepdream: images with a side above this (or any image when
+                                          #   world > 1) run tiled (TiledDeepDream), across every rank
     log_json: bool = True
     asyncio_debug: bool = False           # DV_ASYNCIO_DEBUG=1: event-loop debug mode, slow-callback log
     slow_callback_ms: float = 50.0        # ... threshold for logging a blocking callback (debug mode)

@@ -36,6 +36,67 @@ void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " launch failed with code ", rc);
 }
 
+// Grouped launches (conv_group_begin / conv_group_end): between the two calls every conv that would
+// run on the LDS-DMA kernel with a groupable small-problem tile config (dv::conv_dma_group_cfg) is
+// recorded instead of launched; the end call launches the recorded problems as grouped kernels of up
+// to kGroupMax problems per (A mode, epilogue, config, dtype), in recording order. The caller
+// guarantees the recorded convs are independent (no one reads what another writes) and keeps their
+// tensors alive until the end call (ops/conv.py:conv_group). One group per thread at a time.
+struct PendingConv {
+  dv::ConvArgs a;
+  int amode, epi, cfg;
+};
+thread_local bool g_group_active = false;
+thread_local bool g_group_paused = false;  // recording suspended: convs launch at once, in order
+thread_local std::vector<PendingConv> g_group;
+
+void conv_group_begin() {
+  TORCH_CHECK(!g_group_active, "conv_group_begin: a group is already open on this thread");
+  g_group_active = true;
+  g_group.clear();
+}
+
+// returns the number of grouped kernel launches issued
+int64_t conv_group_end() {
+  TORCH_CHECK(g_group_active, "conv_group_end: no open group");
+  g_group_active = false;
+  g_group_paused = false;
+  std::vector<PendingConv> pend;
+  pend.swap(g_group);
+  std::vector<bool> done(pend.size(), false);
+  int64_t launches = 0;
+  for (size_t i = 0; i < pend.size(); ++i) {
+    if (done[i]) continue;
+    dv::ConvArgs ps[dv::kGroupMax];
+    int n = 0;
+    for (size_t j = i; j < pend.size() && n < dv::kGroupMax; ++j) {
+      if (done[j] || pend[j].amode != pend[i].amode || pend[j].epi != pend[i].epi || pend[j].cfg != pend[i].cfg ||
+          pend[j].a.dtype != pend[i].a.dtype)
+        continue;
+      ps[n++] = pend[j].a;
+      done[j] = true;
+    }
+    if (n == 1) {  // nothing to run beside it: the one-problem path, with its split-K planning
+      dv::ConvArgs a = ps[0];
+      const int ks = dv::conv_dma_splitk(a);
+      Tensor ws;
+      if (ks > 1) {
+        int dev = 0;
+        check_rc((int)hipGetDevice(&dev), "hipGetDevice");
+        ws = at::empty({(int64_t)ks * a.M * a.OCpad}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
+        a.ws = ws.data_ptr<float>();
+        a.ksplit = ks;
+      }
+      check_rc(dv::conv_dma_launch(a, pend[i].amode, pend[i].epi, cur_stream()), "conv_dma");
+      if (ks > 1) check_rc(dv::splitk_reduce_launch(a, pend[i].epi, cur_stream()), "splitk_reduce");
+    } else {
+      check_rc(dv::conv_dma_group_launch(ps, n, pend[i].amode, pend[i].epi, cur_stream()), "conv_dma_group");
+    }
+    ++launches;
+  }
+  return launches;
+}
+
 // geom: N,H,W,C, OH,OW,OC,OCpad, KH,KW,stride,pad_h,pad_w, K,Kpad, M, relu,relu_in,accumulate,
 //       code_div, x_ld, mask_ld, out_ld
 void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
@@ -329,6 +390,14 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     // the DMA kernel addresses A with 32-bit offsets relative to the tile's first image
     const int64_t imgs_per_tile = 512 / std::max(1, a.OH * a.OW) + 2;
     TORCH_CHECK((int64_t)a.H * a.W * a.x_ld * 2 * imgs_per_tile < 0x7FFFFFF0LL, "conv dma: image too large");
+    if (g_group_active && !g_group_paused && (impl == 0 || impl == 2) && !mask.has_value() && !unpooled.defined() &&
+        !relu_x.defined() && !a.ucode && !a.out2 && !stats.has_value()) {
+      const int cfg = dv::conv_dma_group_cfg(a, (int)amode, (int)epi);
+      if (cfg != 0) {  // recorded (no split-K: the group runs its problems side by side); launched by conv_group_end
+        g_group.push_back(PendingConv{a, (int)amode, (int)epi, cfg});
+        return;
+      }
+    }
     // split-K when the tile grid would leave most CUs idle (plain epilogues only)
     // (the reduce kernel applies bias / ReLU / accumulate / residual / emask; not the unpool scatter)
     const bool plain_epi = (epi == dv::CONV_E_BF16 || epi == dv::CONV_E_F32) && !a.ucode && !a.out2;
@@ -980,6 +1049,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res") = py::none(), py::arg("emask") = py::none(), py::arg("stats") = py::none(),
         py::arg("stats_div") = 1, py::arg("ucode") = py::none(), py::arg("ucode_div") = 1,
         py::arg("relu_cols") = 0, py::arg("out2") = py::none(), py::arg("split_col") = 0);
+  m.def("conv_group_begin", &conv_group_begin, "start recording groupable small-problem convs (this thread)");
+  m.def("conv_group_pause", [](bool p) { g_group_paused = p; }, "suspend / resume recording (dependent convs)");
+  m.def("conv_group_end", &conv_group_end, "launch the recorded convs as grouped kernels; returns the launch count");
   m.def("dma_tune", [](int64_t cfg, int64_t ks) { dv::conv_dma_tune((int)cfg, (int)ks); },
         "force the LDS-DMA conv tile config / split-K factor (0 = automatic); tuning only");
   m.def("pool", &pool, "k x k max/avg pooling forward/backward", py::arg("in"), py::arg("out"), py::arg("idx"),

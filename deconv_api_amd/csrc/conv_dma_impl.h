@@ -93,9 +93,12 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
 // through LDS before the epilogue. Each wave then owns a (16*FM) x (16*FN) = 128 x 64 tile where
 // a plain 8-wave layout would own 64 x 64: 12 instead of 16 fragment reads per 32 MFMAs, for the
 // 128- and 64-output-channel layers whose 256 x 128 / 512 x 64 tiles are LDS-read bound.
+// The workgroup body: output tile ``wgid`` (row-major over tiles_n column tiles) of problem ``a``,
+// K slice ky of nky. Shared by the one-problem kernel below and the grouped kernel
+// (conv_dma_group_kernel), whose workgroups each look their problem up in a table.
 template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED,
           bool MASK = false, bool FRAGPIPE = false, bool KS2 = false>
-__global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(const ConvArgs a, int tiles_n) {
+__device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, int wgid, int ky, int nky) {
   constexpr int NW = WM * WN * (KS2 ? 2 : 1);
   static_assert(!KS2 || (BK == 64 && !MASK), "KS2: BK=64 (one 32-deep sub-step per group), no mask");
   constexpr int BM = WM * FM * 16;
@@ -120,7 +123,6 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
   const int kg = KS2 ? wave / (WM * WN) : 0;  // K group (KS2)
   const int wl = KS2 ? wave - kg * (WM * WN) : wave;
   const int wm = wl / WN, wn = wl % WN;
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_n = wgid % tiles_n;
   const int tile_m = wgid / tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
@@ -299,10 +301,10 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
 #pragma unroll
   for (int s = 0; s < BK / 32; ++s) sw[s] = (((s * 4 + (lane >> 4)) ^ rx) << 4);
 
-  // split-K (gridDim.y > 1): this workgroup reduces K tiles [k0, k0 + nk) into a partial sum
+  // split-K (nky > 1): this workgroup reduces K tiles [k0, k0 + nk) into a partial sum
   const int nk_all = a.Kpad / BK;
-  const int k0 = (int)(((long long)nk_all * blockIdx.y) / gridDim.y);
-  const int nk = (int)(((long long)nk_all * (blockIdx.y + 1)) / gridDim.y) - k0;
+  const int k0 = (int)(((long long)nk_all * ky) / nky);
+  const int nk = (int)(((long long)nk_all * (ky + 1)) / nky) - k0;
   k_init(k0);
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
@@ -404,7 +406,7 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
   // ---- epilogue ----
   if (a.ws != nullptr) {  // split-K partial: raw fp32 sums to ws[split][row][OCpad]
     if (kg != 0) return;
-    float* ws = a.ws + (long long)blockIdx.y * a.M * a.OCpad;
+    float* ws = a.ws + (long long)ky * a.M * a.OCpad;
     const int row_l = (lane >> 4) * 4, col_l = lane & 15;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -438,6 +440,26 @@ __global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(co
     epilogue<DT, FM, FN, EPI, true>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
   else
     epilogue<DT, FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
+}
+
+template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED,
+          bool MASK = false, bool FRAGPIPE = false, bool KS2 = false>
+__global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(const ConvArgs a, int tiles_n) {
+  conv_dma_body<DT, WM, WN, FM, FN, BK, STAGES, AMODE, EPI, CALIGNED, MASK, FRAGPIPE, KS2>(
+      a, tiles_n, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, gridDim.y);
+}
+
+// Grouped launch: up to kGroupMax INDEPENDENT problems of one tile config in one grid (the parallel
+// branch convs / dgrads of an InceptionV3 block, ops/inception.py). Workgroup b (XCD-remapped over
+// the whole grid) runs tile b - start[p] of the problem p with start[p] <= b < start[p + 1]: one
+// launch instead of n dependent ones, and the small problems' tiles run side by side.
+template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED>
+__global__ void __launch_bounds__(WM * WN * 64) conv_dma_group_kernel(const ConvGroup g) {
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < kGroupMax; ++i) p += (i < g.n && wgid >= g.start[i]) ? 1 : 0;
+  conv_dma_body<DT, WM, WN, FM, FN, BK, STAGES, AMODE, EPI, CALIGNED>(g.p[p], g.tiles_n[p], wgid - g.start[p], 0, 1);
 }
 
 // residual epilogue (ResNet block tail): out = [ReLU](acc + bias + res), then optionally zeroed

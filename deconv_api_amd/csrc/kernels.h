@@ -66,6 +66,15 @@ struct ConvArgs {
                           //   next conv-down's taps as a [32][64] matrix, row tap*3+c = W[c][tap][:])
 };
 
+// grouped LDS-DMA launch of up to kGroupMax independent problems (conv_dma.hip:conv_dma_group_launch)
+constexpr int kGroupMax = 4;
+struct ConvGroup {
+  ConvArgs p[kGroupMax];
+  int start[kGroupMax + 1];  // first workgroup of each problem (prefix sums of the tile counts)
+  int tiles_n[kGroupMax];
+  int n;
+};
+
 int conv_igemm_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
 // LDS-DMA variant (FWD / TRANSPOSE, no mask): 8-wave 128x64-per-wave tiles
 int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t stream);
@@ -74,6 +83,10 @@ int conv_dma_splitk(const ConvArgs& a);
 // tuning override: force DMA tile config cfg (> 0, conv_dma.hip:dma_forced) and split-K ks (> 0); 0 = auto
 void conv_dma_tune(int cfg, int ks);
 int splitk_reduce_launch(const ConvArgs& a, int epi, hipStream_t stream);
+// tile config a grouped launch of ``a`` would use (conv_dma.hip), 0 = not groupable; and the launch
+// of 1..kGroupMax problems that share it (same dtype, A mode, epilogue and config; no split-K)
+int conv_dma_group_cfg(const ConvArgs& a, int amode, int epi);
+int conv_dma_group_launch(const ConvArgs* ps, int n, int amode, int epi, hipStream_t stream);
 // direct VALU kernels for InceptionV3's conv2d_1 (8-ch padded RGB -> 32, 3x3 / stride 2): forward and
 // input gradient (conv_stem.hip); < 0: unsupported geometry
 int stem_conv_fwd_launch(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,

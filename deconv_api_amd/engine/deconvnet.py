@@ -88,14 +88,19 @@ class DeconvNet:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, target: str, fuse_pools: bool = True,
-                keep_all: bool = False) -> ForwardState:
-        """x: preprocessed [B, 224, 224, 8] (bf16 on device). Runs ``up`` through ``target``."""
+                keep_all: bool = False, hook=None) -> ForwardState:
+        """x: preprocessed [B, 224, 224, 8] (bf16 on device). Runs ``up`` through ``target``.
+        ``hook`` = (layer name, fn): fn() runs on the host right before that layer's forward work is
+        enqueued (bench.py issues the previous step's copy-back there, so the PCIe blit overlaps
+        MFMA-bound convs instead of the memory-bound first layers)."""
         ti = self._check_layer(target)
         seq = self.specs[1: ti + 1]
         st = ForwardState(target, x)
         i = 0
         while i < len(seq):
             s = seq[i]
+            if hook is not None and s.name == hook[0]:
+                hook[1]()
             if s.kind == "conv":
                 cl = self.rt.convs[s.name]
                 nxt = seq[i + 1] if i + 1 < len(seq) else None
@@ -248,11 +253,11 @@ class DeconvNet:
 
     # ------------------------------------------------------------------ one call
     def run(self, x: torch.Tensor, layer: str, k: int = 4, mode: str = "all",
-            batch_topk: str = "per_image", mosaic: bool = True) -> DeconvResult:
+            batch_topk: str = "per_image", mosaic: bool = True, hook=None) -> DeconvResult:
         if mode not in VALID_MODES:
             raise ValueError(f"Illegal visualize mode {mode!r}; use 'all' or 'max'")
         with tracing.range_("dv.forward"):
-            st = self.forward(x, layer)
+            st = self.forward(x, layer, hook=hook)
         with tracing.range_("dv.select"):
             idx, val = self.select_filters(st.out, k, batch_topk)
         stats = None

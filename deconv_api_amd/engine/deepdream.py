@@ -29,10 +29,12 @@ import torch
 import torch.nn.functional as F
 
 from ..ops import native
+from ..utils.logging import get_logger
 from ..ops.autograd import loss_tap, premasked_grads, sumsq_core
 
 # DV_DREAM_FUSED=0: the step tail (loss, normalization, update) as torch ops instead of the fused
 # HIP kernels (A/B); DV_DREAM_GRAPHS: hipGraph cache entries (octave shapes) kept, LRU-evicted
+log = get_logger("deconv_api_amd.deepdream")
 FUSED_STEP = os.environ.get("DV_DREAM_FUSED", "1") != "0"
 GRAPH_CACHE = int(os.environ.get("DV_DREAM_GRAPHS", "8"))
 # DV_DREAM_OCTAVE_GRAPH=0: one graph per step, replayed `iterations` times (A/B). Default: the
@@ -48,6 +50,11 @@ SPLIT = int(os.environ.get("DV_DREAM_SPLIT", "2"))
 # DV_DREAM_TAPS=0: intermediate loss layers get their loss gradient through autograd's sum (A/B);
 # default: a loss tap adds it into the gradient from above in the loss-gradient kernel itself
 TAPS = os.environ.get("DV_DREAM_TAPS", "1") != "0"
+# tiled multi-rank octaves: capture the per-step all-gathers inside the octave's hipGraph
+# (DV_TILE_CAPTURE_COLL=0: per-step graphs + eager collectives); DV_TILE_COLLECTIVE=1 takes the
+# collective path even on a 1-rank process group (torchrun rehearsal of the multi-rank octave)
+CAPTURE_COLLECTIVE = os.environ.get("DV_TILE_CAPTURE_COLL", "1") != "0"
+TILE_COLLECTIVE = os.environ.get("DV_TILE_COLLECTIVE", "0") == "1"
 # DV_DREAM_FUSED_LOSS=0: separate forward loss-partial launches (A/B); default: every loss layer's
 # partial sums of squares come out of its loss-gradient kernel (one launch per loss layer, not two)
 FUSED_LOSS = os.environ.get("DV_DREAM_FUSED_LOSS", "1") != "0"
@@ -351,9 +358,11 @@ class TiledDeepDream(DeepDream):
                     unit losses ride along: no separate loss all-reduce)
       tile_update   per-image mean|g| and loss from the pack tails, device-side max_loss flag,
                     x += step * g / mean|g| straight from the packs (identical on every rank)
-    On one rank the whole octave (``iterations`` steps, shifts in a device table) is ONE captured
-    hipGraph; with several ranks each step's compute is a graph and the collective runs between
-    replays. CPU tensors use the torch implementation below (the oracle)."""
+    The whole octave (``iterations`` steps, shifts in a device table staged through pinned memory)
+    is ONE captured hipGraph, the per-step all-gathers included when there are several ranks
+    (fallback if the capture is refused: a graph per step, the collective between replays).
+    ``virtual_octave`` runs the multi-rank step for W virtual ranks on one device (tests). CPU
+    tensors use the torch implementation below (the oracle)."""
 
     def __init__(self, net, settings: Optional[DreamSettings] = None, tile: int = 512, info=None, seed: int = 0,
                  dtype=None, use_graphs: bool = True):
@@ -367,6 +376,7 @@ class TiledDeepDream(DeepDream):
         self.tile_graphs = use_graphs and self.device.type == "cuda"
         self._tgraphs: "OrderedDict[tuple, object]" = OrderedDict()
         self.tile_fused = FUSED_STEP and self.device.type == "cuda"
+        self._shift_pin, self._shift_ev = None, None
 
     @staticmethod
     def _axis_tiles(L: int, tile: int):
@@ -518,46 +528,74 @@ class TiledDeepDream(DeepDream):
         native.lib().tile_update(st.packs, st.ucap, st.plan, st.shifts[it], st.x, st.done, st.loss, float(self.s.step),
                                  ml, st.world, st.Th, st.Tw)
 
+    def _collective(self, st) -> bool:
+        """Whether the octave all-gathers the packs: several ranks, or DV_TILE_COLLECTIVE=1 with a
+        real 1-rank process group (the multi-rank code path, rehearsed on one GPU)."""
+        if st.world > 1:
+            return True
+        return TILE_COLLECTIVE and self.info is not None and self.info.backend != "none"
+
     def _tile_steps(self, st) -> None:
         import torch.distributed as dist
 
+        coll = self._collective(st)
         for it in range(self.s.iterations):
             self._tile_compute(st, it)
-            if st.world > 1:
+            if coll:
                 dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
             self._tile_apply(st, it)
+
+    def _stage_shifts(self, st) -> None:
+        """This octave's random roll table -> the device, without a host sync: through a pinned
+        buffer (a pageable H2D copy blocks the host until the stream drains, once per octave)."""
+        shifts = torch.randint(-self.tile // 2, self.tile // 2 + 1, (self.s.iterations, 2), generator=self.gen)
+        pin = getattr(self, "_shift_pin", None)
+        if pin is None or pin.shape != shifts.shape:
+            pin = self._shift_pin = torch.empty(shifts.shape, dtype=torch.int32, pin_memory=True)
+        elif self._shift_ev is not None:
+            self._shift_ev.synchronize()  # the previous octave's upload from this buffer (long done)
+        pin.copy_(shifts)
+        st.shifts.copy_(pin, non_blocking=True)
+        self._shift_ev = torch.cuda.Event()
+        self._shift_ev.record()
+
+    def _capture(self, fn) -> torch.cuda.CUDAGraph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        return g
 
     def _gradient_ascent_fused(self, x: torch.Tensor) -> torch.Tensor:
         import torch.distributed as dist
 
         B, H, W, _ = x.shape
         st = self._tstate(B, H, W)
-        shifts = torch.randint(-self.tile // 2, self.tile // 2 + 1, (self.s.iterations, 2), generator=self.gen)
-        st.shifts.copy_(shifts.to(torch.int32))
+        self._stage_shifts(st)
         st.x.copy_(x)
         st.done.zero_()
-        if self.tile_graphs and st.world == 1 and st.graph is None:
+        coll = self._collective(st)
+        if self.tile_graphs and st.graph is None and st.step_graph is None:
             # warm up on a side stream (autograd / allocator), restore the image, capture the octave
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
                 self._tile_compute(st, 0)
+                if coll:  # the collective's communicator is set up outside the capture
+                    dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
             torch.cuda.current_stream(self.device).wait_stream(s)
-            st.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(st.graph):
-                self._tile_steps(st)
-        elif self.tile_graphs and st.world > 1 and st.step_graph is None:
-            s = torch.cuda.Stream(self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
-                self._tile_compute(st, 0)
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            st.step_graph = []
-            for it in range(self.s.iterations):  # one graph per step index (each reads its shift row)
-                gph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gph):
-                    self._tile_compute(st, it)
-                st.step_graph.append(gph)
+            if not coll or CAPTURE_COLLECTIVE:
+                # the whole octave, all-gathers included (RCCL collectives are graph-capturable):
+                # one replay per octave instead of `iterations` replays + eager collectives
+                try:
+                    st.graph = self._capture(lambda: self._tile_steps(st))
+                except RuntimeError as e:  # capture of the collective refused: per-step graphs
+                    if not coll:
+                        raise
+                    log.warning("octave capture with collectives failed, per-step graphs", extra={"fields": {"err": repr(e)}})
+                    st.graph = None
+            if st.graph is None and coll:
+                st.step_graph = [self._capture(lambda it=it: self._tile_compute(st, it))
+                                 for it in range(self.s.iterations)]
         if st.graph is not None:
             st.graph.replay()
         elif st.step_graph is not None:
@@ -568,6 +606,44 @@ class TiledDeepDream(DeepDream):
         else:
             self._tile_steps(st)
         return st.x.clone()
+
+    def virtual_octave(self, x: torch.Tensor, world: int) -> torch.Tensor:
+        """One octave of the ``world``-rank fused tiled step on THIS device, without collectives: for
+        every step each virtual rank gathers its units, runs the network and packs into its own slot
+        of the packs buffer (exactly what the all-gather assembles on every real rank), then ONE
+        tile_update with ``world`` packs applies the step. Eager; for tests / tools (the multi-rank
+        kernels' rank/world indexing exercised on a one-GPU box)."""
+        lib = native.lib()
+        B, H, W, _ = x.shape
+        Th, Tw, plan, ntiles = self._gplan(B, H, W)
+        nunits = plan.shape[0]
+        ucap = -(-nunits // world)
+        dev = self.device
+        plan = plan.to(dev)
+        pe = lib.tile_pack_elems(ucap, Th, Tw)
+        packs = torch.zeros(world, pe, dtype=self.dtype, device=dev)
+        st = type("TileState", (), {})()
+        st.Th, st.Tw, st.ntiles, st.world, st.ucap, st.plan = Th, Tw, ntiles, world, ucap, plan
+        st.x = x.clone()
+        st.done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        st.loss = torch.zeros(B, device=dev)
+        st.shifts = torch.zeros(self.s.iterations, 2, dtype=torch.int32, device=dev)
+        self._stage_shifts(st)
+        st.packs = packs
+        st.lcoef, st.scales = None, None
+        ranks = []
+        for r in range(world):
+            rs = type("TileRank", (), {})()
+            rs.__dict__.update(st.__dict__)
+            rs.rank, rs.mine, rs.pack = r, len(range(r, nunits, world)), packs[r]
+            rs.xin = torch.zeros(max(rs.mine, 1), Th, Tw, 8, dtype=self.dtype, device=dev, requires_grad=True)
+            rs.lpart = torch.zeros(len(self.s.layers), max(rs.mine, 1), LOSS_PARTS, device=dev)
+            ranks.append(rs)
+        for it in range(self.s.iterations):
+            for rs in ranks:
+                self._tile_compute(rs, it)
+            self._tile_apply(st, it)
+        return st.x
 
     def gradient_ascent(self, x: torch.Tensor) -> torch.Tensor:
         if self.tile_fused and x.is_cuda:

@@ -12,6 +12,8 @@ Reference semantics being implemented (rashanarshad/deconv_api):
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 from dataclasses import dataclass
 from typing import Optional
@@ -326,6 +328,50 @@ def _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
     return y.to(odt).contiguous()
 
 
+# DV_CONV_GROUP=0: every conv its own launch (A/B of the grouped launches)
+GROUPED = os.environ.get("DV_CONV_GROUP", "1") != "0"
+_group_refs: list = []  # tensors of the open group's recorded convs (kept alive until it launches)
+_group_open = [False]
+
+
+@contextlib.contextmanager
+def conv_group(device=None):
+    """Launch the INDEPENDENT convs issued inside the block together: every one the LDS-DMA kernel
+    would run with a small-problem tile config is recorded and, at exit, launched as grouped kernels
+    (csrc/conv_dma_group.hip: one grid, each workgroup runs a tile of one problem); the rest launch
+    immediately as usual. No conv inside may read another's output. Numerics are unchanged: the same
+    tile program runs on the same data. CPU tensors and DV_CONV_GROUP=0: a no-op."""
+    if not GROUPED or _group_open[0] or (device is not None and torch.device(device).type != "cuda"):
+        yield
+        return
+    lib = native.lib()
+    lib.conv_group_begin()
+    _group_open[0] = True
+    try:
+        yield
+    finally:
+        _group_open[0] = False
+        try:
+            lib.conv_group_end()
+        finally:
+            _group_refs.clear()
+
+
+@contextlib.contextmanager
+def conv_group_paused():
+    """Inside a conv_group: the convs issued here launch at once, in order (a pair where the second
+    accumulates into the first's output); the group's recorded convs stay recorded."""
+    if not _group_open[0]:
+        yield
+        return
+    lib = native.lib()
+    lib.conv_group_pause(True)
+    try:
+        yield
+    finally:
+        lib.conv_group_pause(False)
+
+
 def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
                 epilogue, out, accumulate, use_bias, res=None, emask=None, stats=None, stats_div=1,
                 unpool_out=None, unpool_div=1, relu_cols=0, out2=None, split_col=0):
@@ -373,6 +419,8 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
     # kernels (the binding routes by shape under 'auto')
     dma_only = res is not None or unpool_out is not None or relu_cols > 0 or out2 is not None or \
         (emask is not None and _policy["impl"] not in ("auto",))
+    if _group_open[0]:
+        _group_refs.append((x, cw, out, code, mask, res, emask, out2))
     lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
              IMPL["dma"] if dma_only else IMPL[_policy["impl"]],  # DMA-only epilogue features
              res, emask, stats, stats_div, unpool_out, unpool_div, relu_cols, out2, split_col)

@@ -37,7 +37,7 @@ import torch.nn.functional as F
 
 from . import native
 from .autograd import _PREMASKED, ConvUnit, _is_relu_out, _tag, dgrad_strided_into
-from .conv import conv2d
+from .conv import conv2d, conv_group, conv_group_paused
 
 # DV_MERGE_B1=0: the b1 branch as its own GEMM (A/B); default: it joins the merged head GEMM forward
 MERGE_B1 = os.environ.get("DV_MERGE_B1", "1") != "0"
@@ -178,7 +178,12 @@ class _InceptionFn(torch.autograd.Function):
             else:
                 T = conv2d(x, mfwd, stride=1, pad=(0, 0), relu=True, use_bias=True, relu_cols=relu_n)
             saved.append(T)
-        plan = []  # per branch: (offset, width, kind, info)
+        # Per branch: (offset, width, kind, info). Pool branches run first; the conv chains then
+        # advance in LEVELS: level l runs op l of every chain that still has one (a merged head's
+        # op 0 already ran in the head GEMM). The convs of one level read only their own chain's
+        # previous output, so each level is one conv_group: its small problems launch together.
+        plan = [None] * len(blk.branches)
+        chains = {}  # branch index -> [ops, next op index, cur, cur_i, steps, Y slice]
         off = 0
         for bi, (ops, wdt) in enumerate(zip(blk.branches, widths)):
             ysl = Y[..., off:off + wdt]
@@ -192,28 +197,34 @@ class _InceptionFn(torch.autograd.Function):
                 else:
                     t = _conv_fwd(u, x, relu=False, bias=False)
                 lib.pool(t, ysl, None, 1, 0, _pool_geom(N, H, W, u.cout, 3, 1, 1), u.fwd.bias_pad, True)
-                plan.append((off, wdt, "avg", [u.name, mcols.get(bi)]))
+                plan[bi] = (off, wdt, "avg", [u.name, mcols.get(bi)])
             elif ops == ["max"]:
                 idx = torch.empty(N, OH, OW, Cin, dtype=torch.uint8, device=x.device)
                 lib.pool(x, ysl, idx, 0, 0, _pool_geom(N, H, W, Cin, 3, 2, 0))
                 saved.append(idx)
-                plan.append((off, wdt, "max", [len(saved) - 1]))
+                plan[bi] = (off, wdt, "max", [len(saved) - 1])
             else:
                 steps = []  # (unit name(s), index of its saved input | ("T", cols) for a merged head)
-                cur, cur_i = x, 0
-                start = 0
+                ch = [ops, 0, x, 0, steps, ysl]
                 if bi in mcols:  # the head ran in the merged GEMM: its output is a slice of T
                     mo, mw = mcols[bi]
-                    cur = T[..., mo:mo + mw]
-                    cur_i = ("T", mo, mw)
+                    ch[2], ch[3] = T[..., mo:mo + mw], ("T", mo, mw)
                     steps.append(((ops[0],), "merged"))
-                    start = 1
-                for j in range(start, len(ops)):
+                    ch[1] = 1
+                if bi == b1_done:  # computed by the merged forward GEMM (backward: its own dgrad)
+                    steps.append(((ops[0],), 0))
+                    ch[1] = len(ops)
+                chains[bi] = ch
+                plan[bi] = (off, wdt, "convs", steps)
+            off += wdt
+        while any(ch[1] < len(ch[0]) for ch in chains.values()):
+            with conv_group(x.device):
+                for ch in chains.values():
+                    ops, j, cur, cur_i, steps, ysl = ch
+                    if j >= len(ops):
+                        continue
                     op = ops[j]
                     last = j == len(ops) - 1
-                    if bi == b1_done:  # computed by the merged forward GEMM (backward: its own dgrad)
-                        steps.append(((op,), cur_i))
-                        continue
                     if isinstance(op, tuple):
                         assert last, "split must end its branch"
                         ua, ub = blk.units[op[1]], blk.units[op[2]]
@@ -225,9 +236,8 @@ class _InceptionFn(torch.autograd.Function):
                         steps.append(((op,), cur_i))
                         if not last:
                             saved.append(y)
-                            cur, cur_i = y, len(saved) - 1
-                plan.append((off, wdt, "convs", steps))
-            off += wdt
+                            ch[2], ch[3] = y, len(saved) - 1
+                    ch[1] = j + 1
         ctx.blk = blk
         ctx.plan = plan
         ctx.merged = T is not None
@@ -283,6 +293,7 @@ class _InceptionFn(torch.autograd.Function):
             return dgrad_strided_into(u, g, (inp.shape[1], inp.shape[2]), out, accumulate, emask=inp)
 
         deferred = []  # head-conv contributions on x go last: their epilogue applies the x mask
+        chains = []  # per conv branch: [reversed steps, next index, current gradient]
         for off, wdt, kind, info in ctx.plan:
             gsl = gY[..., off:off + wdt]
             if kind == "max":
@@ -305,33 +316,42 @@ class _InceptionFn(torch.autograd.Function):
                     lib.pool(gsl, gp, None, 1, 1, _pool_geom(N, H, W, u.cout, 3, 1, 1))
                     deferred.append((u.bwd, gp))
                 continue
-            # conv chain: walk it backwards; the gradient w.r.t. each ReLU output is premasked
-            g = gsl
-            for names, in_i in reversed(info):
-                units = [blk.units[n] for n in names]
-                if in_i == "merged":
-                    continue  # the head's own dgrad is part of the merged G_T GEMM below
-                inp = None if in_i == 0 else inp_of(in_i)
-                into = GT[..., in_i[1]:in_i[1] + in_i[2]] if isinstance(in_i, tuple) else None
-                if in_i == 0:  # unmerged head conv(s) on the block input
-                    if len(units) == 2:
+            chains.append([list(reversed(info)), 0, gsl])
+        # conv chains walked backwards in levels (step l of every chain; the gradient w.r.t. each
+        # ReLU output is premasked): one conv_group per level, like the forward
+        while any(c[1] < len(c[0]) for c in chains):
+            with conv_group(x.device):
+                for c in chains:
+                    if c[1] >= len(c[0]):
+                        continue
+                    names, in_i = c[0][c[1]]
+                    c[1] += 1
+                    g = c[2]
+                    units = [blk.units[n] for n in names]
+                    if in_i == "merged":
+                        continue  # the head's own dgrad is part of the merged G_T GEMM below
+                    inp = None if in_i == 0 else inp_of(in_i)
+                    into = GT[..., in_i[1]:in_i[1] + in_i[2]] if isinstance(in_i, tuple) else None
+                    if in_i == 0:  # unmerged head conv(s) on the block input
+                        if len(units) == 2:
+                            ua, ub = units
+                            deferred.append((ua.bwd, g[..., : ua.cout]))
+                            deferred.append((ub.bwd, g[..., ua.cout:]))
+                        elif units[0].stride == 1:
+                            deferred.append((units[0].bwd, g))
+                        else:  # strided head on x: straight into gx (written / accumulated)
+                            dgrad_strided_into(units[0], g, (H, W), gx, accumulate=state["written"])
+                            state["written"] = True
+                            state["masked"] = False
+                        continue
+                    if len(units) == 2:  # split: sum of two dgrads, masked by inp > 0
                         ua, ub = units
-                        deferred.append((ua.bwd, g[..., : ua.cout]))
-                        deferred.append((ub.bwd, g[..., ua.cout:]))
-                    elif units[0].stride == 1:
-                        deferred.append((units[0].bwd, g))
-                    else:  # strided head on x: straight into gx (written / accumulated)
-                        dgrad_strided_into(units[0], g, (H, W), gx, accumulate=state["written"])
-                        state["written"] = True
-                        state["masked"] = False
-                    continue
-                if len(units) == 2:  # split: sum of two dgrads, masked by inp > 0
-                    ua, ub = units
-                    gi = dgrad_into(ua, g[..., : ua.cout], inp, out=into)
-                    dgrad_into(ub, g[..., ua.cout:], inp, out=gi, accumulate=True)
-                    g = gi
-                else:
-                    g = dgrad_into(units[0], g, inp, out=into)
+                        with conv_group_paused():  # the second accumulates into the first: in order
+                            gi = dgrad_into(ua, g[..., : ua.cout], inp, out=into)
+                            dgrad_into(ub, g[..., ua.cout:], inp, out=gi, accumulate=True)
+                        c[2] = gi
+                    else:
+                        c[2] = dgrad_into(units[0], g, inp, out=into)
         if GT is not None:
             deferred.append((blk.merge[1], GT))
         for cw, g in deferred:

@@ -41,6 +41,7 @@ keeps beating) is only caught by the collective deadline (``ack_timeout``), not 
 """
 from __future__ import annotations
 
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -76,8 +77,16 @@ class Batch:
 class ShardedRunner:
     def __init__(self, engine, info: DistInfo, image_size: int = 224, k: int = 4, mode: str = "all",
                  use_graphs: bool = True, hb_timeout: float = 3.0, ack_timeout: float = 600.0,
-                 poll_s: float = 0.0001):
+                 poll_s: float = 0.0001, cfg=None):
+        """``cfg`` (serve/config.Config): what the /deepdream engines are built from on every rank
+        (seed, weight files, tile size); the default config when None."""
         self.engine = engine
+        self.cfg = cfg
+        # one command (its store keys and collectives) at a time: the deconv worker and the
+        # /deepdream worker both drive the group
+        self._cmd_lock = threading.RLock()
+        self._dream_tiled: Dict[tuple, object] = {}
+        self._dream_nets: Dict[str, object] = {}
         self.info = info
         self.S = image_size
         self.k = k
@@ -207,6 +216,10 @@ class ShardedRunner:
         """rank 0: scatter the batch and enqueue its engine work on every rank; ``finish`` gathers
         it. Another batch may be launched before this one is finished (two in flight)."""
         assert self.info.rank == 0
+        with self._cmd_lock:
+            return self._launch(layer, images)
+
+    def _launch(self, layer: str, images: List[np.ndarray]) -> Batch:
         self.batches += 1
         while True:
             b = Batch(layer, images, self.ctl.epoch if self.ctl else 0, self._bid, n=len(images))
@@ -226,11 +239,15 @@ class ShardedRunner:
     def finish(self, b: Batch) -> np.ndarray:
         """rank 0: gather batch ``b``'s mosaics (recomputed on the survivors if the group was
         re-formed since its launch) -> uint8 [n, 2S, 2S, 3] on the host."""
+        with self._cmd_lock:
+            return self._finish(b)
+
+    def _finish(self, b: Batch) -> np.ndarray:
         while True:
             if b.host is not None:
                 return self._host(b.host)
             if b.epoch != self.ctl.epoch:  # launched on a group that no longer exists
-                b = self.launch(b.layer, b.images)
+                b = self._launch(b.layer, b.images)
                 continue
             try:
                 self._gather_cmd(b)
@@ -242,7 +259,55 @@ class ShardedRunner:
         log.error("peer lost, re-forming over the survivors", extra={"fields": {"dead": e.dead}})
         self.ctl.reform(e.dead)
         self.reforms += 1
+        self._after_reform()
+
+    def _after_reform(self) -> None:
         self.slots = [None, None]
+        for dd in self._dream_tiled.values():  # unit plans / packs / graphs were for the old world
+            dd._tgraphs.clear()
+            dd._plans.clear()
+
+    # ----------------------------------------------------------------- /deepdream across ranks
+    def _dream_engine(self, model: str, octaves: int, steps: int):
+        from ..config import Config
+        from ..serve.dream_service import tiled_engine
+
+        return tiled_engine(self._dream_tiled, self._dream_nets, self.cfg or Config(), model, octaves, steps,
+                            self.info.device, info=self.info)
+
+    def _dream_local(self, dd, x_u8: torch.Tensor, seed: int) -> torch.Tensor:
+        dd.gen.manual_seed(seed)  # identical rolls on every rank
+        return dd.dream_u8(x_u8)
+
+    def dream(self, imgs: torch.Tensor, model: str, octaves: int, steps: int) -> np.ndarray:
+        """rank 0: DeepDream of u8 [n, H, W, 3] tiled across every rank -> u8 [n, H, W, 3]. The
+        images are broadcast (RCCL); each rank runs its share of the (tile, image) units and the
+        per-step pack all-gathers inside the tiled engine assemble every step on every rank."""
+        assert self.info.rank == 0
+        seed = (self.cfg.seed if self.cfg is not None else 0)
+        with self._cmd_lock:
+            while True:
+                if self.world == 1:
+                    dd = self._dream_engine(model, octaves, steps)
+                    return self._dream_local(dd, imgs.to(self.info.device), seed).cpu().numpy()
+                try:
+                    return self._dream_cmd(imgs, model, octaves, steps, seed)
+                except PeerLost as e:
+                    self._reform(e)
+
+    def _dream_cmd(self, imgs: torch.Tensor, model: str, octaves: int, steps: int, seed: int) -> np.ndarray:
+        ctl = self.ctl
+        n, H, W, _ = imgs.shape
+        seq = ctl.post_cmd({"op": "dream", "model": model, "octaves": octaves, "steps": steps, "n": n, "H": H,
+                            "W": W, "seed": seed})
+        dd = self._dream_engine(model, octaves, steps)  # overlaps the followers' acks
+        x = imgs.to(self.info.device).contiguous()
+        ctl.wait_acks("ready", seq)
+        ctl.go("go1", seq)
+        self._await(dist.broadcast(x, src=0, async_op=True), "broadcast")
+        out = self._dream_local(dd, x, seed)
+        ctl.wait_acks("done", seq)
+        return out.cpu().numpy()
 
     def _run_cmd(self, b: Batch) -> None:
         n = len(b.images)
@@ -345,6 +410,17 @@ class ShardedRunner:
                     mos = self._engine(self._preprocess(shard), msg["layer"]).contiguous()
                     pending[msg["b"]] = self._keep(msg["b"], mos)
                     continue
+                if op == "dream":
+                    ctl.ack("ready", seq)
+                    self._go(ctl, "go1", seq)
+                    x = torch.empty(msg["n"], msg["H"], msg["W"], 3, dtype=torch.uint8, device=dev)
+                    self._await(dist.broadcast(x, src=0, async_op=True), "broadcast", True)
+                    dd = self._dream_engine(msg["model"], msg["octaves"], msg["steps"])
+                    out = self._dream_local(dd, x, msg["seed"])
+                    if out.is_cuda:
+                        torch.cuda.current_stream(dev).synchronize()
+                    ctl.ack("done", seq)
+                    continue
                 if op == "gather":
                     mos, ev = pending.pop(msg["b"])
                     if ev is not None:
@@ -364,7 +440,7 @@ class ShardedRunner:
             except PeerLost:
                 r = msg if op == "reform" else ctl.wait_reform()
                 pending.clear()
-                self.slots = [None, None]
+                self._after_reform()
                 if not ctl.follow_reform(r):
                     return done
 

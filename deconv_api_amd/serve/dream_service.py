@@ -2,6 +2,13 @@
 DeepDream (InceptionV3 or ResNet-50) on the GPU worker -> JPEG data URL (same conventions as
 ``POST /``).
 
+Engines: images up to ``dream_tile`` per side on one GPU run the untiled engine (one hipGraph per
+octave); larger ones run TiledDeepDream (rolled tiles as one batch). With several
+ranks (``runner``: parallel/sharded.py) every batch runs TILED ACROSS ALL RANKS: rank 0 posts a
+``dream`` command on the control plane, broadcasts the images over RCCL, and every rank runs its
+share of the (tile, image) units with the packs all-gathered each step; every rank ends with the
+same result and rank 0 answers.
+
 Requests are batched: a request joins the pending list after decode + size validation; the GPU
 worker takes the oldest request and every pending one with the same (model, octaves, steps,
 H, W) key (waiting up to ``dream_window_ms`` for more, at most ``dream_max_batch``) and runs them
@@ -22,7 +29,7 @@ import torch
 
 from ..codec import encode_data_url, read_data_url
 from ..config import Config
-from ..engine.deepdream import RESNET_LAYERS, DeepDream, DreamSettings
+from ..engine.deepdream import RESNET_LAYERS, DeepDream, DreamSettings, TiledDeepDream
 from ..utils import metrics as M
 
 MAX_SIDE = 1024
@@ -54,12 +61,50 @@ def _resolve(fut: asyncio.Future, value=None, exc: Optional[BaseException] = Non
         fut.set_result(value)
 
 
+def make_dream_net(cfg: Config, model: str, device):
+    """The /deepdream network on ``device``: seeded random init or the configured weights. Every
+    rank builds it from the same seed / file, so the replicas are identical without a broadcast."""
+    from ..models.dream_import import load_weights, new_model
+
+    net = new_model(model, cfg.seed)
+    path = cfg.inception_weights if model == "inception_v3" else cfg.resnet_weights
+    if path:
+        load_weights(net, path)
+    return net.build(device)
+
+
+def dream_settings(model: str, octaves: int, steps: int) -> DreamSettings:
+    s = DreamSettings() if model == "inception_v3" else DreamSettings(layers=dict(RESNET_LAYERS))
+    s.octaves, s.iterations = octaves, steps
+    return s
+
+
+def tiled_engine(cache: Dict[Tuple[str, int, int], TiledDeepDream], nets: Dict[str, Any], cfg: Config, model: str,
+                 octaves: int, steps: int, device, info=None) -> TiledDeepDream:
+    """One TiledDeepDream per (model, octaves, steps) with its own settings (no shared mutable
+    settings between batches of different keys); the shift generator is re-seeded per batch by the
+    caller so every rank rolls identically."""
+    key = (model, octaves, steps)
+    if key not in cache:
+        if model not in nets:
+            nets[model] = make_dream_net(cfg, model, device)
+        cache[key] = TiledDeepDream(nets[model], dream_settings(model, octaves, steps), tile=cfg.dream_tile,
+                                    info=info, seed=cfg.seed, use_graphs=cfg.hip_graphs)
+    return cache[key]
+
+
 class DreamService:
-    def __init__(self, cfg: Optional[Config] = None):
+    def __init__(self, cfg: Optional[Config] = None, runner=None):
+        """``runner``: parallel.sharded.ShardedRunner of a multi-rank service: every /deepdream batch
+        then runs tiled across all ranks (its control plane and process group)."""
         self.cfg = cfg or Config.from_env()
-        self.device = torch.device(self.cfg.resolve_device())
+        self.runner = runner
+        self.device = torch.device(self.cfg.resolve_device() if runner is None else str(runner.info.device))
         self._engines: Dict[str, DeepDream] = {}
+        self._tiled: Dict[Tuple[str, int, int], TiledDeepDream] = {}
+        self._nets: Dict[str, Any] = {}
         self._lock = threading.Lock()
+        self._run_lock = threading.RLock()  # one batch at a time (engine settings are per batch)
         self._cv = threading.Condition()
         self._pending: List[_Req] = []
         self._stop = False
@@ -79,21 +124,33 @@ class DreamService:
             raise ValueError("octaves must be 1..6 and steps 1..100")
 
     def engine(self, model: str, octaves: int, steps: int) -> DeepDream:
+        """The untiled engine of ``model``. Its settings are set per batch, so it is only handed out
+        under ``_run_lock``, which ``run_batch`` holds for the whole batch (a second thread's batch
+        waits instead of changing octaves / steps under a running one)."""
         self.validate(model, octaves, steps)
+        assert self._run_lock._is_owned(), "DreamService.engine: hold _run_lock (run_batch does)"
         with self._lock:
             if model not in self._engines:
-                from ..models.dream_import import load_weights, new_model
-
-                net = new_model(model, self.cfg.seed)
-                path = self.cfg.inception_weights if model == "inception_v3" else self.cfg.resnet_weights
-                if path:
-                    load_weights(net, path)
-                net.build(self.device)
-                s = DreamSettings() if model == "inception_v3" else DreamSettings(layers=dict(RESNET_LAYERS))
-                self._engines[model] = DeepDream(net, s, use_graphs=self.cfg.hip_graphs)
+                if model not in self._nets:
+                    self._nets[model] = make_dream_net(self.cfg, model, self.device)
+                s = dream_settings(model, octaves, steps)
+                self._engines[model] = DeepDream(self._nets[model], s, use_graphs=self.cfg.hip_graphs)
             e = self._engines[model]
         e.s.octaves, e.s.iterations = octaves, steps
         return e
+
+    def tiled(self, model: str, octaves: int, steps: int) -> TiledDeepDream:
+        self.validate(model, octaves, steps)
+        with self._lock:
+            return tiled_engine(self._tiled, self._nets, self.cfg, model, octaves, steps, self.device)
+
+    @property
+    def world(self) -> int:
+        return self.runner.world if self.runner is not None else 1
+
+    def status(self) -> dict:
+        return {"world": self.world, "tile": self.cfg.dream_tile, "models": sorted(self._nets),
+                "batches": len(self.batches)}
 
     # ------------------------------------------------------------------ request prep (codec pool)
     def prepare(self, img: np.ndarray, octaves: int) -> torch.Tensor:
@@ -142,13 +199,27 @@ class DreamService:
             return batch
 
     def run_batch(self, imgs: List[torch.Tensor], model: str, octaves: int, steps: int) -> np.ndarray:
-        """u8 [H, W, 3] images of one shape -> dreamed u8 [n, H, W, 3] (one engine batch)."""
-        e = self.engine(model, octaves, steps)
+        """u8 [H, W, 3] images of one shape -> dreamed u8 [n, H, W, 3] (one engine batch): across
+        every rank when the service has several, tiled on this GPU for sides > dream_tile, else the
+        untiled engine."""
+        with self._run_lock:
+            return self._run_batch(imgs, model, octaves, steps)
+
+    def _run_batch(self, imgs: List[torch.Tensor], model: str, octaves: int, steps: int) -> np.ndarray:
         n = len(imgs)
-        pad = _bucket(n, self.max_batch) - n
-        x = torch.stack(imgs + [imgs[-1]] * pad)
         t0 = time.perf_counter()
-        out = e.dream_u8(x)[:n].cpu().numpy()
+        H, W = imgs[0].shape[:2]
+        if self.world > 1:
+            out = self.runner.dream(torch.stack(imgs), model, octaves, steps)
+        elif max(H, W) > self.cfg.dream_tile:
+            e = self.tiled(model, octaves, steps)
+            e.gen.manual_seed(self.cfg.seed)  # same rolls as the multi-rank path for the same input
+            out = e.dream_u8(torch.stack(imgs)).cpu().numpy()
+        else:
+            e = self.engine(model, octaves, steps)
+            pad = _bucket(n, self.max_batch) - n
+            x = torch.stack(imgs + [imgs[-1]] * pad)
+            out = e.dream_u8(x)[:n].cpu().numpy()
         M.ENGINE_TIME.observe(time.perf_counter() - t0, stage="deepdream")
         M.BATCH_SIZE.observe(n, route="/deepdream")
         M.IMAGES.inc(n, route="/deepdream")

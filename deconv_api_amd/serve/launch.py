@@ -43,7 +43,7 @@ def main(argv=None):
     setup(cfg.log_json)
     info = pdist.init()
     eng = build_engine(cfg, info)
-    runner = ShardedRunner(eng, info, cfg.image_size, cfg.filters, cfg.mode) if info.world > 1 else None
+    runner = ShardedRunner(eng, info, cfg.image_size, cfg.filters, cfg.mode, cfg=cfg) if info.world > 1 else None
     if not info.is_main:
         n = runner.follow()
         log.info("follower done", extra={"fields": {"rank": info.rank, "batches": n}})
@@ -53,8 +53,12 @@ def main(argv=None):
 
     from ..api.app import create_app
 
+    from .dream_service import DreamService
+
     svc = DeconvService(cfg, engine=eng, runner=runner)
-    app = create_app(svc, cfg)
+    # /deepdream: tiled across every rank when there are several (the same control plane)
+    dream = DreamService(cfg, runner=runner)
+    app = create_app(svc, cfg, dream_service=dream)
     log.info("serving", extra={"fields": {"world": info.world, "device": str(info.device), "port": cfg.port}})
     try:
         uvicorn.run(app, host=cfg.host, port=cfg.port, log_level="info")
@@ -62,6 +66,7 @@ def main(argv=None):
         if runner is not None:
             runner.stop()
         svc.close()
+        dream.close()
         pdist.shutdown()
 
 

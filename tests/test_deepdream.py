@@ -465,3 +465,50 @@ def test_gpu_pool_backward_accumulate(native_lib):
         acc = base.clone()
         nat.lib().pool(gy, acc, idx, kind, 1, geom, None, False, True)
         assert (acc.float() - (base.float() + plain.float())).abs().max() < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_tiled_virtual_ranks_match_one_rank(native_lib, world):
+    """The multi-rank fused tiled step (each rank's tile_gather / network / tile_pack into ITS slot
+    of the packs, then tile_update over ``world`` packs) run for virtual ranks on one GPU equals the
+    1-rank octave: the rank/world indexing of tile_pack (unit offsets, ucap) and tile_update (world
+    packs) is exercised without a multi-GPU box. Units land in different rank batches, so conv tile
+    choices (and fp32 summation order) differ slightly: compared up to rounding."""
+    from deconv_api_amd.models.resnet50 import ResNet50
+
+    net = ResNet50(0).build("cuda", torch.float16)
+    s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=1, iterations=3, max_loss=None)
+    x = (torch.rand(2, 256, 320, 3, generator=torch.Generator().manual_seed(3)) * 2 - 1).cuda()
+    ref = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).gradient_ascent(x)
+    got = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).virtual_octave(x, world)
+    d = (got - ref).abs()
+    assert _cos((got - x).flatten().cpu(), (ref - x).flatten().cpu()) > 0.999
+    assert float(d.mean()) < 1e-3 and float(d.max()) < 5e-2, (float(d.mean()), float(d.max()))
+
+
+@pytest.mark.gpu
+def test_gpu_tiled_collective_octave_captured(native_lib):
+    """torchrun, one rank, DV_TILE_COLLECTIVE=1: the collective code path of the tiled octave (the
+    per-step all-gather of the packs over RCCL) is captured INSIDE the octave's hipGraph and equals
+    the collective-free 1-rank octave bit for bit."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "tools/tiled_collective.py"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["backend"] == "nccl" and out["collective"] is True, out
+    assert out["octave_graph"] is True and out["step_graphs"] is False, out
+    assert out["equal"] is True, out

@@ -345,3 +345,56 @@ def test_two_batches_in_flight(fault):
     else:
         assert r0[2] == world and r0[3] == 0, r0
         assert all(res[r][2] == 4 for r in range(1, world)), res
+
+
+def _worker_dream_service(rank, world, port, q):
+    try:
+        from deconv_api_amd.config import Config
+        from deconv_api_amd.engine.deconvnet import DeconvNet
+        from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
+        from deconv_api_amd.parallel.sharded import ShardedRunner
+
+        info = _init(rank, world, port)
+        cfg = Config(device="cpu", dream_tile=96, seed=4, hip_graphs=False)
+        specs = vgg16_specs(width_div=8, image_size=32, fc=64, classes=10)
+        eng = DeconvNet(VGG16.random(0, specs=specs).build("cpu", torch.float32))
+        runner = ShardedRunner(eng, info, image_size=32, cfg=cfg)
+        if rank == 0:
+            from deconv_api_amd.serve.dream_service import DreamService
+
+            rng = np.random.default_rng(2)
+            img = torch.from_numpy(rng.integers(0, 256, (160, 176, 3), dtype=np.uint8))
+            ds = DreamService(cfg, runner=runner)
+            got = ds.run_batch([img], "resnet50", 1, 2)  # 2 x 2 tiles of <= 96 px over 2 ranks
+            imgs = [rng.integers(0, 256, (30, 28, 3), dtype=np.uint8) for _ in range(3)]
+            mos = runner.run("block2_conv1", imgs)  # the deconv service keeps working on the same group
+            st = ds.status()
+            runner.stop()
+            single = DreamService(cfg)  # one process: the same image tiled locally (side > 96)
+            want = single.run_batch([img], "resnet50", 1, 2)
+            want_mos = ShardedRunner(eng, type(info)(), image_size=32)._local("block2_conv1", imgs).numpy()
+            d = np.abs(got.astype(np.int32) - want.astype(np.int32))
+            q.put((rank, got.shape, int(d.max()), float(d.mean()), st["world"], bool(np.array_equal(mos, want_mos))))
+        else:
+            n = runner.follow()
+            q.put((rank, "follower returned", n, None, None, None))
+        from deconv_api_amd.parallel import dist as pdist
+
+        pdist.shutdown()
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None, None, None))
+
+
+def test_deepdream_service_tiled_across_ranks():
+    """POST /deepdream's batch on a 2-rank group: rank 0 broadcasts the image, both ranks run their
+    (tile, image) units with the per-step pack all-gather, rank 0 answers; equals the single-process
+    tiled result up to CPU conv rounding (the units sit in different batches), the deconv command
+    stream keeps working on the same group, and the dream service reports the world."""
+    res = _run(_worker_dream_service, 2)
+    r0 = res[0]
+    assert r0[1] == (1, 160, 176, 3), r0
+    assert r0[2] <= 3 and r0[3] < 0.05, r0  # uint8 output: at most a few levels apart, rarely
+    assert r0[4] == 2 and r0[5] is True, r0
+    assert res[1][1] == "follower returned" and res[1][2] == 1, res[1]

@@ -74,3 +74,82 @@ def test_strict_backward_parity(engines, layer, mode):
     mg = ops.deprocess_mosaic(rg.reshape(4, 224, 224, 3))
     mc = ops.deprocess_mosaic(rc.reshape(4, 224, 224, 3))
     assert _psnr(mg, mc) >= 30.0, (layer, mode, _psnr(mg, mc))
+
+
+# ---- B > 1: cross-image indexing of the folded B*K backward (code_div / unpool_div = K) ----
+
+B3_LAYERS = ["block1_pool", "block2_conv2", "block3_conv3", "block4_pool", "block5_conv3", "block5_pool", "fc1",
+             "predictions"]
+
+
+@pytest.fixture(scope="module")
+def x3(native_lib):
+    g = torch.Generator().manual_seed(5)
+    img = torch.randint(0, 256, (3, 224, 224, 3), generator=g, dtype=torch.uint8)
+    img[1] = img[1].flip(0) // 2  # three different images (different switches and top filters)
+    img[2] = (img[2].float() * 0.6 + 80).to(torch.uint8)
+    x = torch.empty(3, 224, 224, 8, dtype=torch.bfloat16, device="cuda")
+    for b in range(3):
+        ops.resize_preprocess(img[b].cuda(), x[b])
+    return x
+
+
+def _cpu_state(st, layer):
+    return ForwardState(layer, st.out.float().cpu(), {k: v.cpu() for k, v in st.codes.items()},
+                        {k: v.float().cpu() for k, v in st.outputs.items()})
+
+
+@pytest.mark.parametrize("batch_topk", ["per_image", "global"])
+@pytest.mark.parametrize("mode", ["all", "max"])
+@pytest.mark.parametrize("layer", B3_LAYERS)
+def test_strict_backward_parity_batch3(engines, x3, layer, mode, batch_topk):
+    """B = 3 different images, K = 4: image b's chains must use image b's switches (a wrong
+    ``b // K`` would pair reconstructions with another image's codes); per-image and the
+    reference's across-batch ('global', app/deepdream.py:369-380) filter selection."""
+    gpu, cpu, _ = engines
+    st = gpu.forward(x3, layer)
+    idx, _ = gpu.select_filters(st.out, 4, batch_topk)
+    rg = gpu.backward(st, idx, mode=mode, batch_topk=batch_topk).cpu()
+    rc = cpu.backward(_cpu_state(st, layer), idx.cpu(), mode=mode, batch_topk=batch_topk)
+    assert rg.shape == rc.shape == (3, 4, 224, 224, 3)
+    n = 0
+    for b in range(3):
+        for k in range(4):
+            if int(idx[b, k]) < 0 or float(rc[b, k].abs().max()) == 0.0:
+                continue
+            c = _cos(rg[b, k], rc[b, k])
+            assert c >= 0.999, (layer, mode, batch_topk, b, k, c)
+            n += 1
+    assert n >= 3, (layer, mode, batch_topk, idx)
+
+
+@pytest.mark.parametrize("target", ["block3_conv3", "block5_pool", "fc1"])
+def test_visualize_all_layers_k8_parity(engines, target):
+    """The library API (app/deepdream.py:383-476: every named layer <= target, top-8 filters,
+    across-batch sums) on the GPU engine, each of its reconstructions vs the fp32 CPU backward fed
+    the same forward state and filters."""
+    from deconv_api_amd.engine.deconvnet import visualize_all_layers
+
+    gpu, cpu, x = engines
+    res = visualize_all_layers(gpu, x, target, "all", all_layers=True, top=8)
+    st = gpu.forward(x, target, fuse_pools=False, keep_all=True)
+    stc = _cpu_state(st, target)
+    ti = gpu.names.index(target)
+    want_layers = [s.name for s in gpu.specs[1: ti + 1] if s.kind in ("conv", "pool", "flatten", "dense")]
+    assert sorted(res) == sorted(want_layers)
+    checked = 0
+    for name, lst in res.items():
+        out = st.outputs[name]
+        idx, _ = gpu.select_filters(out, 8, "global")
+        nsel = int((idx[0] >= 0).sum())
+        assert len(lst) == nsel, (name, len(lst), nsel)
+        sub = ForwardState(name, stc.outputs[name], stc.codes, stc.outputs)
+        rc = cpu.backward(sub, idx.cpu(), "all", "global", layer=name)
+        for kk in range(nsel):
+            got = torch.from_numpy(lst[kk])
+            if float(rc[0, kk].abs().max()) == 0.0:
+                continue
+            c = _cos(got, rc[0, kk])
+            assert c >= 0.999, (target, name, kk, c)
+            checked += 1
+    assert checked >= 8 * len(want_layers) // 2, checked
