@@ -34,6 +34,7 @@ import torch
 import torch.distributed as dist
 
 from deconv_api_amd import ops
+from deconv_api_amd.codec.image import encode_gpu
 from deconv_api_amd.engine.deconvnet import DeconvNet
 from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
 from deconv_api_amd.parallel import dist as pdist
@@ -46,6 +47,9 @@ from deconv_api_amd.runtime.streams import copy_stream as copy_stream_for
 # bound ones it costs little (tools/copy_overlap_probe.py: a GEMM loop 9.06 -> 9.18 ms). block3's
 # convs are the first MFMA-bound layers of the step.
 COPY_AT = os.environ.get("DV_BENCH_COPY_AT", "block3_conv1")
+# DV_BENCH_JPEG=1: each step also JPEG-encodes its mosaics on the GPU (csrc/jpeg_gpu.hip, what the
+# service does) and copies back the scans instead of the raw mosaics (~10x fewer PCIe bytes)
+JPEG = os.environ.get("DV_BENCH_JPEG", "0") == "1"
 
 # the reference's implied end-to-end rate for layer=block5_conv3 is ~0.03-0.04 img/s
 # (CPU, one request at a time; a lower bound on its cost). We divide by the favourable 0.04.
@@ -172,6 +176,9 @@ def main(argv=None):
     # inside the timed region (drain)
     deferred = [None]
 
+    off_host = [torch.empty(B + 1, dtype=torch.int64, pin_memory=cuda) for _ in range(2)]
+    scans_host = [None, None]
+
     def issue_copy():
         if deferred[0] is None:
             return
@@ -179,6 +186,19 @@ def main(argv=None):
         deferred[0] = None
         if back_done[slot] is not None:
             back_done[slot].synchronize()  # host slot free again (its step i-2 copy landed)
+        if JPEG:  # mosaic = (device scans, event of the offsets' copy into off_host[slot])
+            packed, off_ev = mosaic
+            off_ev.synchronize()  # step i's scan sizes (long done: the GPU is in step i+1)
+            total = int(off_host[slot][-1])
+            if scans_host[slot] is None or scans_host[slot].numel() < total:
+                scans_host[slot] = torch.empty(max(total, 1) * 5 // 4, dtype=torch.uint8, pin_memory=True)
+            with torch.cuda.stream(copy_stream):
+                scans_host[slot][:total].copy_(packed[:total], non_blocking=True)
+                back_done[slot] = torch.cuda.Event(enable_timing=True)
+                back_done[slot].record()
+            if ev0 is not None:
+                lat.append((ev0, back_done[slot]))
+            return
         ready = torch.cuda.Event()
         ready.record()
         copy_stream.wait_event(ready)
@@ -202,7 +222,19 @@ def main(argv=None):
                 pending[slot].wait()  # the gather that last used this buffer (step i-2)
             pending[slot] = dist.all_gather_into_tensor(gathered[slot], res.mosaic.contiguous(), async_op=True)
         if cuda:
-            deferred[0] = (slot, res.mosaic, ev0)
+            out = res.mosaic
+            if JPEG:
+                packed, off = encode_gpu(res.mosaic)
+                done = torch.cuda.Event()
+                done.record()
+                copy_stream.wait_event(done)
+                packed.record_stream(copy_stream)
+                with torch.cuda.stream(copy_stream):
+                    off_host[slot].copy_(off, non_blocking=True)
+                    off_ev = torch.cuda.Event()
+                    off_ev.record()
+                out = (packed, off_ev)
+            deferred[0] = (slot, out, ev0)
             if not COPY_AT:
                 issue_copy()
         else:
@@ -274,6 +306,7 @@ def main(argv=None):
         "vs_baseline": round(value / REF_IMG_PER_S, 1),
         "baseline_img_per_s": REF_IMG_PER_S,
         "dtype": "bf16" if cuda else "fp32",
+        "gpu_jpeg": bool(JPEG and cuda),
         "process_group": info.backend,
         "data": "synthetic uint8 224x224 images, seeded random-init VGG16 weights",
         "config": {"model": f"vgg16_deconvnet_{args.layer}", "global_batch": B * info.world, "seq_len": S,

@@ -126,6 +126,31 @@ def encode_data_urls(mosaics: np.ndarray, quality: int = JPEG_QUALITY, threads: 
                               DATA_URL_PREFIX, int(threads))
 
 
+def encode_gpu(mosaics, quality: int = JPEG_QUALITY):
+    """uint8 [B, H, W, 3] DEVICE tensor -> (packed scans, offsets [B + 1]) device tensors: baseline
+    JPEG on the GPU (csrc/jpeg_gpu.hip; restart marker per MCU row). Enqueued on the current stream;
+    ``gpu_data_urls`` turns the host copies into response strings."""
+    from ..ops import native
+
+    return native.lib().jpeg_gpu(mosaics.contiguous(), int(quality))
+
+
+def gpu_data_urls(packed, off, H: int, W: int, quality: int = JPEG_QUALITY, threads: int = 8):
+    """Host copies of ``encode_gpu``'s outputs (only off[-1] bytes of ``packed`` are read) -> B data
+    URLs (header + scan + EOI, base64, the reference's quote escaping), GIL released."""
+    from ..ops import native
+
+    return native.lib().jpeg_gpu_data_urls(packed, off, int(H), int(W), int(quality), DATA_URL_PREFIX, int(threads))
+
+
+def gpu_jpeg_bytes(packed, off, b: int, H: int, W: int, quality: int = JPEG_QUALITY) -> bytes:
+    """JPEG file of image ``b`` from host copies of ``encode_gpu``'s outputs (tests / tools)."""
+    from ..ops import native
+
+    o = off.tolist()
+    return native.lib().jpeg_gpu_header(H, W, quality) + bytes(packed[o[b]:o[b + 1]].numpy()) + b"\xff\xd9"
+
+
 def quote_b64(b64: str) -> str:
     """``urllib.parse.quote`` restricted to base64 text: letters, digits and '/' are kept, so only
     '+' -> '%2B' and '=' -> '%3D' change. Identical output, C-speed (quote() walks the ~100 KB

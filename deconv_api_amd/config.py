@@ -43,6 +43,8 @@ class Config:
     encode_chunk: int = 16                # images per encode call; each chunk is delivered at once
     gil_switch_us: int = 500              # sys.setswitchinterval for the serving process (0 = leave)
     native_codec: bool = True             # native encoder for responses (PIL fallback when False/unbuilt)
+    gpu_jpeg: bool = True                 # GPU: responses JPEG-encoded on the device (csrc/jpeg_gpu.hip);
+                                          #   the host only base64s the scans
     cors_origins: Tuple[str, ...] = ("*",)  # app/main.py:22-32
     host: str = "0.0.0.0"
     port: int = 80                        # Dockerfile:10,15

@@ -9,6 +9,9 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
 
 namespace {
 
@@ -708,6 +711,36 @@ void tile_update(Tensor packs, int64_t ucap, Tensor plan, Tensor shift, Tensor x
 int64_t tile_pack_elems(int64_t ucap, int64_t Th, int64_t Tw) { return dv::tile_pack_elems((int)ucap, (int)Th, (int)Tw); }
 
 // geom: KH, KW, stride, pad_h, pad_w, Cr; cols [N, OH, OW, J_ld] (J = KH*KW*Cr), gx [N, H, W, 8]
+// g = KH, KW, stride, pad, Cr; false: not the fused kernel's geometry (caller falls back)
+bool stem_dgrad_fused(Tensor gy, c10::optional<Tensor> mask, Tensor w, Tensor gx, std::vector<int64_t> g) {
+  check_cuda(gy, "gy");
+  check_cuda(w, "w");
+  check_cuda(gx, "gx");
+  TORCH_CHECK(g.size() == 5, "stem_dgrad_fused: geometry");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gy.device());
+  TORCH_CHECK(gy.dim() == 4 && gx.dim() == 4 && w.dim() == 2 && gy.is_contiguous() && gx.is_contiguous() &&
+                  w.is_contiguous() && gy.scalar_type() == gx.scalar_type() && w.scalar_type() == gy.scalar_type() &&
+                  gx.size(3) == 8 && gx.size(0) == gy.size(0),
+              "stem_dgrad_fused: gy [N,OH,OW,C], gx [N,H,W,8], w [rows, C] contiguous, one 16-bit dtype");
+  dv::StemDgradGeom G{(int)gy.size(0), (int)gx.size(1), (int)gx.size(2), (int)gy.size(1), (int)gy.size(2),
+                      (int)gy.size(3), (int)g[0], (int)g[1], (int)g[2], (int)g[3], (int)g[4], (int)w.size(0),
+                      (int)w.size(1)};
+  TORCH_CHECK(w.size(1) >= G.C, "stem_dgrad_fused: w rows must hold C weights");
+  const uint16_t* m = nullptr;
+  if (mask.has_value()) {
+    check_cuda(*mask, "mask");
+    TORCH_CHECK(mask->sizes() == gy.sizes() && mask->is_contiguous() && mask->scalar_type() == gy.scalar_type(),
+                "stem_dgrad_fused: mask like gy");
+    m = reinterpret_cast<const uint16_t*>(mask->data_ptr());
+  }
+  const int rc = dv::stem_dgrad_fused_launch(reinterpret_cast<const uint16_t*>(gy.data_ptr()), m,
+                                             reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                             reinterpret_cast<uint16_t*>(gx.data_ptr()), G, dt_of(gy), cur_stream());
+  if (rc == -4) return false;
+  check_rc(rc, "stem_dgrad_fused");
+  return true;
+}
+
 void col2im(Tensor cols, Tensor gx, std::vector<int64_t> g) {
   check_cuda(cols, "cols");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(cols.device());
@@ -738,6 +771,70 @@ py::list jpeg_data_urls(Tensor img, int64_t quality, std::string prefix, int64_t
   py::list res;
   for (auto& s : out) res.append(py::str(s));
   return res;
+}
+
+// GPU JPEG (jpeg_gpu.hip): img uint8 [B, H, W, 3] on the device -> {packed entropy-coded scans
+// (device uint8, capacity B * worst case), offsets int64 [B + 1] (device)}; the stream of image b is
+// jpeg_gpu_header(H, W, q) + packed[off[b]:off[b+1]] + EOI
+std::vector<Tensor> jpeg_gpu(Tensor img, int64_t quality) {
+  check_cuda(img, "img");
+  TORCH_CHECK(img.scalar_type() == at::kByte && img.dim() == 4 && img.size(3) == 3 && img.is_contiguous(),
+              "jpeg_gpu: uint8 [B, H, W, 3] contiguous");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(img.device());
+  const int B = (int)img.size(0), H = (int)img.size(1), W = (int)img.size(2);
+  TORCH_CHECK(B >= 1 && H >= 1 && W >= 1 && H <= 65500 && W <= 65500, "jpeg_gpu: image size");
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, Tensor> tables;  // (device, quality) -> device GpuTables
+  Tensor tab;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair((int)img.get_device(), (int)quality);
+    auto it = tables.find(key);
+    if (it == tables.end()) {
+      const dvjpeg::GpuTables t = dvjpeg::gpu_tables((int)quality);
+      Tensor h = at::empty({(int64_t)sizeof(t)}, at::TensorOptions().dtype(at::kByte));
+      std::memcpy(h.data_ptr(), &t, sizeof(t));
+      it = tables.emplace(key, h.to(img.device())).first;
+    }
+    tab = it->second;
+  }
+  long long raw_words = 0, out_cap = 0;
+  dv::jpeg_gpu_caps(H, W, &raw_words, &out_cap);
+  auto opt = img.options();
+  Tensor ws = at::empty({dv::jpeg_gpu_ws_bytes(B, H, W)}, opt);
+  Tensor packed = at::empty({(int64_t)B * out_cap}, opt);
+  Tensor off = at::empty({B + 1}, opt.dtype(at::kLong));
+  check_rc(dv::jpeg_gpu_launch(img.data_ptr<uint8_t>(), B, H, W, tab.data_ptr(), ws.data_ptr(),
+                               packed.data_ptr<uint8_t>(), reinterpret_cast<long long*>(off.data_ptr<int64_t>()),
+                               cur_stream()),
+           "jpeg_gpu");
+  return {packed, off};
+}
+
+py::bytes jpeg_gpu_header(int64_t H, int64_t W, int64_t quality) {
+  return py::bytes(dvjpeg::jpeg_header((int)H, (int)W, (int)quality, 1));
+}
+
+// host: GPU scans (CPU tensors) -> data URLs (header + scan + EOI, base64, quote escaping), GIL released
+py::list jpeg_gpu_data_urls(Tensor packed, Tensor off, int64_t H, int64_t W, int64_t quality, std::string prefix,
+                            int64_t threads) {
+  TORCH_CHECK(!packed.is_cuda() && !off.is_cuda() && packed.scalar_type() == at::kByte &&
+                  off.scalar_type() == at::kLong && off.dim() == 1 && off.size(0) >= 1 && packed.is_contiguous() &&
+                  off.is_contiguous(),
+              "jpeg_gpu_data_urls: CPU uint8 scans + int64 offsets");
+  const int B = (int)off.size(0) - 1;
+  const int64_t* o = off.data_ptr<int64_t>();
+  TORCH_CHECK(o[0] == 0 && o[B] <= packed.numel(), "jpeg_gpu_data_urls: offsets outside the scans");
+  for (int b = 0; b < B; ++b) TORCH_CHECK(o[b + 1] >= o[b], "jpeg_gpu_data_urls: offsets not increasing");
+  const std::string header = dvjpeg::jpeg_header((int)H, (int)W, (int)quality, 1);
+  std::vector<std::string> out;
+  {
+    py::gil_scoped_release nogil;
+    out = dvjpeg::data_urls_from_scans(header, packed.data_ptr<uint8_t>(), o, B, prefix, (int)threads);
+  }
+  py::list l;
+  for (auto& u : out) l.append(py::str(u));
+  return l;
 }
 
 py::bytes jpeg_encode(Tensor img, int64_t quality) {
@@ -985,29 +1082,6 @@ void zsum3x3(Tensor z, Tensor out, c10::optional<Tensor> stats, int64_t stats_di
            "zsum3x3");
 }
 
-// A stream whose dispatches may only use `n_cus` CUs (evenly spaced over the device's CU mask bits):
-// host-bound copies (the runtime's D2H blit kernels wait on PCIe writes) then hold a few CUs instead
-// of filling the whole device ahead of the compute stream's next kernels. Returns the hipStream_t
-// handle (never destroyed: one per device and purpose, process lifetime).
-int64_t cu_masked_stream(int64_t device, int64_t n_cus) {
-  int dev_prev = 0;
-  check_rc((int)hipGetDevice(&dev_prev), "hipGetDevice");
-  check_rc((int)hipSetDevice((int)device), "hipSetDevice");
-  int total = 0;
-  check_rc((int)hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, (int)device), "CU count");
-  TORCH_CHECK(n_cus >= 1 && n_cus <= total, "cu_masked_stream: 1 <= n_cus <= ", total);
-  std::vector<uint32_t> mask((total + 31) / 32, 0u);
-  for (int64_t i = 0; i < n_cus; ++i) {
-    const int64_t cu = i * total / n_cus;
-    mask[cu / 32] |= 1u << (cu % 32);
-  }
-  hipStream_t st = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
-  hipSetDevice(dev_prev);
-  check_rc((int)e, "hipExtStreamCreateWithCUMask");
-  return reinterpret_cast<int64_t>(st);
-}
-
 void maxpool2x2(Tensor x, Tensor out, Tensor code) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -1067,9 +1141,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tile_update", &tile_update, "tiled DeepDream: normalize + update the image from every rank's packs");
   m.def("tile_pack_elems", &tile_pack_elems);
   m.def("dream_update", &dream_update, "fused DeepDream normalize + update + next network input");
+  m.def("stem_dgrad_fused", &stem_dgrad_fused, "fused GEMM + col2im input gradient of a 7x7/2 RGB stem conv");
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
   m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");
   m.def("softmax_rows", &softmax_rows, "row softmax (classifier head)");
+  m.def("jpeg_gpu", &jpeg_gpu, "GPU baseline JPEG scans of uint8 [B,H,W,3] (restart per MCU row)");
+  m.def("jpeg_gpu_header", &jpeg_gpu_header, "SOI..SOS of the GPU encoder's streams");
+  m.def("jpeg_gpu_data_urls", &jpeg_gpu_data_urls, "GPU scans -> data URLs (host base64, GIL released)");
   m.def("jpeg_encode", &jpeg_encode, "native baseline JPEG encode (GIL released)");
   m.def("channel_sum", &channel_sum);
   m.def("topk_pos", &topk_pos);
@@ -1082,7 +1160,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("preprocess_u8", &preprocess_u8, "resized RGB u8 -> caffe-preprocessed bf16 network input");
   m.def("maxpool2x2", &maxpool2x2);
   m.def("unpool2x2", &unpool2x2);
-  m.def("cu_masked_stream", &cu_masked_stream, "HIP stream restricted to n evenly spaced CUs (handle)");
   m.def("conv_unpool_z", &conv_unpool_z, "unpool -> conv3x3 64->64 -> ReLU -> per-tap products of the next 64->3 conv");
   m.def("zsum3x3", &zsum3x3, "9-tap shift-add of a per-tap product map (+ ReLU, per-image stats)");
   m.attr("ARCH") = "gfx950";

@@ -25,7 +25,7 @@ int conv_dma_splitk(const ConvArgs& a) {
   static const bool small_off = std::getenv("DV_NO_SMALL_SPLITK") != nullptr;
   if (off) return 1;
   const int nk = a.Kpad / 64;
-  if (g_cfg == 0 && (auto_cfg(a) == 8 || auto_cfg(a) == 17)) {
+  if (g_cfg == 0 && auto_cfg(a) == 8) {
     // only the smallest problems: the reduce pass re-reads ks x M x OCpad fp32 partials, which
     // outweighs the shorter K loop once M x OCpad grows (full-model A/B, docs/KERNELS.md)
     static const long long mn_max =

@@ -1076,11 +1076,9 @@ static int auto_cfg(const ConvArgs& a) {
   // (short K too: M 1600 x N 64 x K 64 4.2 vs 6.0 us for the size-based 256 x 64 tile in a graph,
   // tools/small_conv_latency.py; DV_SMALL_TILE_KMIN=256 restores the round-1 rule)
   static const int kmin = std::getenv("DV_SMALL_TILE_KMIN") ? std::atoi(std::getenv("DV_SMALL_TILE_KMIN")) : 0;
-  // DV_SMALL_TILE_W8=1 (opt-in): for the smallest M, 8 waves on the 64x64 tile with a 4-deep ring
-  // (half the DMA issues per wave and K tile): M1600 x N160 x K1440 12.8 -> 11.8 us in isolation
-  // (tools/small_conv_latency.py), but config 3 end to end 417 vs 418 img/s (noise), so off
-  static const bool w8 = std::getenv("DV_SMALL_TILE_W8") != nullptr && std::atoi(std::getenv("DV_SMALL_TILE_W8")) != 0;
-  if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= kmin) return (w8 && a.M <= 8192) ? 17 : 8;
+  // (an 8-wave 64x64 tile with a 4-deep ring, config 17, was -8 % per launch in isolation but
+  // neutral end to end, 417 vs 418 img/s: it stays a tuner-only config)
+  if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= kmin) return 8;
   if (a.OCpad % 128 == 0 && a.OC > 64 && a.Kpad < 4096 && (a.Kpad < 1024 || mn < 50000000LL)) return 3;
   return 0;
 }

@@ -423,6 +423,52 @@ std::string assemble(const Plan& p, const std::vector<std::string>& segs) {
 
 }  // namespace
 
+GpuTables gpu_tables(int quality) {
+  const Plan p = make_plan(16, 16, quality, 1);
+  GpuTables g{};
+  std::memcpy(g.rl, p.rl, sizeof g.rl);
+  std::memcpy(g.rc, p.rc, sizeof g.rc);
+  std::memcpy(g.zz_src, p.zz_src, sizeof g.zz_src);
+  const auto& T = tables();
+  for (int c = 0; c < 2; ++c) {
+    for (int i = 0; i < 12; ++i) {
+      g.dc_code[c][i] = T.dc[c].code[i];
+      g.dc_len[c][i] = T.dc[c].len[i];
+    }
+    for (int i = 0; i < 256; ++i) {
+      g.ac_code[c][i] = T.ac[c].code[i];
+      g.ac_len[c][i] = T.ac[c].len[i];
+    }
+  }
+  return g;
+}
+
+std::string jpeg_header(int H, int W, int quality, int restart_rows) {
+  const int mcuy = (H + 15) / 16;
+  return make_plan(H, W, quality, restart_rows > 0 ? (mcuy + restart_rows - 1) / restart_rows : 1).header;
+}
+
+std::vector<std::string> data_urls_from_scans(const std::string& header, const uint8_t* scans, const int64_t* off,
+                                              int B, const std::string& prefix, int threads) {
+  std::vector<std::string> out(B);
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    std::string jpg;
+    for (int b = next++; b < B; b = next++) {
+      jpg.assign(header);
+      jpg.append(reinterpret_cast<const char*>(scans + off[b]), (size_t)(off[b + 1] - off[b]));
+      jpg.append("\xFF\xD9", 2);  // EOI
+      out[b] = data_url(jpg, prefix);
+    }
+  };
+  const int nt = std::max(1, std::min(threads, B));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  return out;
+}
+
 std::string encode_jpeg(const uint8_t* rgb, int H, int W, int quality, int segments) {
   const Plan p = make_plan(H, W, quality, segments);
   std::vector<std::string> segs(p.nseg);

@@ -17,4 +17,24 @@ std::string data_url(const std::string& jpeg, const std::string& prefix);
 std::vector<std::string> encode_data_urls(const uint8_t* rgb, int B, int H, int W, int quality,
                                           const std::string& prefix, int threads);
 
+// Everything the GPU encoder (jpeg_gpu.hip) needs, laid out as its kernels read it: quantizer
+// reciprocals in the AAN DCT's transposed coefficient layout, the zig-zag source map, and the
+// Annex K Huffman codes (DC: 12 symbols, AC: 256) for luma (0) / chroma (1).
+struct GpuTables {
+  float rl[64], rc[64];
+  uint8_t zz_src[64];
+  uint16_t dc_code[2][12];
+  uint8_t dc_len[2][12];
+  uint16_t ac_code[2][256];
+  uint8_t ac_len[2][256];
+};
+GpuTables gpu_tables(int quality);
+// SOI .. SOS of the stream encode_jpeg writes for (H, W, quality) with a restart marker after every
+// ``restart_rows`` MCU rows (0: none)
+std::string jpeg_header(int H, int W, int quality, int restart_rows);
+// B images from the GPU encoder: header + entropy-coded bytes [off[b], off[b+1]) + EOI, base64'd
+// with the quote() escaping, on `threads` native threads (call with the GIL released)
+std::vector<std::string> data_urls_from_scans(const std::string& header, const uint8_t* scans, const int64_t* off,
+                                              int B, const std::string& prefix, int threads);
+
 }  // namespace dvjpeg

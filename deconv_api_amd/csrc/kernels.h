@@ -169,6 +169,21 @@ struct Col2ImGeom {
   int N, H, W, OH, OW, KH, KW, stride, pad_h, pad_w, Cr, J_ld;
 };
 int col2im_launch(const uint16_t* cols, uint16_t* gx, const Col2ImGeom& g, int dtype, hipStream_t s);
+// fused GEMM + col2im input gradient of ResNet-50's conv1 (conv_stem_dgrad.hip): dy [N,OH,OW,C],
+// optional ReLU mask like dy, wb = the cols GEMM's B^T [w_rows][w_ld] (row (kh*KW+kw)*Cr+c),
+// gx [N,H,W,8]; < 0: geometry not covered
+struct StemDgradGeom {
+  int N, H, W, OH, OW, C, KH, KW, stride, pad, Cr, w_rows, w_ld;
+};
+int stem_dgrad_fused_launch(const uint16_t* gy, const uint16_t* mask, const uint16_t* wb, uint16_t* gx,
+                            const StemDgradGeom& g, int dtype, hipStream_t s);
+// GPU baseline JPEG encode of B same-size RGB images (jpeg_gpu.hip): entropy-coded scans (restart
+// marker after every MCU row, no header/EOI) packed back to back into `packed` at off[0..B];
+// `tables` = a device copy of dvjpeg::GpuTables, `ws` = jpeg_gpu_ws_bytes(B, H, W) of workspace
+long long jpeg_gpu_ws_bytes(int B, int H, int W);
+void jpeg_gpu_caps(int H, int W, long long* raw_words, long long* out_cap);
+int jpeg_gpu_launch(const uint8_t* rgb, int B, int H, int W, const void* tables, void* ws, uint8_t* packed,
+                    long long* off, hipStream_t s);
 // row softmax (fp32 [M][N])
 int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)

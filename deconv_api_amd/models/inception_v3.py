@@ -17,16 +17,12 @@ import torch
 
 from ..ops.autograd import ConvUnit, avg_pool, cat_channels, max_pool
 from ..ops.inception import InceptionBlock
-from ..runtime.streams import run_parallel
 
-# DV_BRANCH_STREAMS=1: unfused blocks run their branches on side streams (measured no gain in a
-# graph: the launches already fill the CUs, profiles/kstats_c3_streams.txt); DV_INCEPTION_FUSED=0:
-# per-op autograd units + torch.cat instead of the one-node blocks of ops/inception.py (A/B)
-BRANCH_STREAMS = os.environ.get("DV_BRANCH_STREAMS", "0") != "0"
+# DV_INCEPTION_FUSED=0: per-op autograd units + torch.cat instead of the one-node blocks of
+# ops/inception.py (the oracle-shaped path; GPU tests compare the two). Removed after measuring:
+# branches on side streams (no gain in a graph, profiles/kstats_c3_r2_branch_streams.txt) and
+# conv2d_4/5 padded to 96 channels (neutral, profiles/dream_c3_r2_padstem.txt).
 FUSED_BLOCKS = os.environ.get("DV_INCEPTION_FUSED", "1") != "0"
-# DV_PAD_STEM=1 (opt-in): conv2d_4 / conv2d_5 at 96 channels on the halo-stream kernels instead of 80 on
-# the implicit GEMM; measured neutral on config 3 (417 vs 419 img/s, profiles/dream_c3_r2_padstem.txt)
-PAD_STEM = os.environ.get("DV_PAD_STEM", "0") != "0"
 
 MIXED = [f"mixed{i}" for i in range(11)]
 
@@ -95,30 +91,10 @@ class InceptionV3:
             cin = 2048
 
     # ----------------------------------------------------------------- runtime
-    def _pad_stem_channels(self, to: int = 96) -> None:
-        """conv2d_4 (64 -> 80) gets zero output channels up to ``to`` (ReLU(0 + 0) = 0) and conv2d_5
-        zero input channels to match: the same function, but conv2d_5's input has C % 32 == 0, so its
-        forward and its input gradient run on the halo-stream kernels instead of the implicit GEMM."""
-        u4, u5 = self.units["conv2d_4"], self.units["conv2d_5"]
-        if u4.cout != 80 or u5.cin != 80:
-            return
-        before = sum(u.w.numel() + u.b.numel() for u in (u4, u5))
-        w4 = torch.zeros(to, *u4.w.shape[1:])
-        w4[:80] = u4.w
-        b4 = torch.zeros(to)
-        b4[:80] = u4.b
-        u4.w, u4.b = w4, b4
-        w5 = torch.zeros(u5.w.shape[0], to, *u5.w.shape[2:])
-        w5[:, :80] = u5.w
-        u5.w = w5
-        self._pad_extra = sum(u.w.numel() + u.b.numel() for u in (u4, u5)) - before
-
     def build(self, device, dtype=torch.bfloat16) -> "InceptionV3":
         """Pack weights for ``device``; ``dtype`` is the GPU storage dtype (bf16 or fp16)."""
         self.device = torch.device(device)
         self.dtype = dtype
-        if self.device.type == "cuda" and PAD_STEM:
-            self._pad_stem_channels()
         for u in self.units.values():
             u.build(self.device, dtype)
         for blk in self.iblocks:  # merged head GEMMs (GPU)
@@ -126,8 +102,8 @@ class InceptionV3:
         return self
 
     def num_params(self) -> int:
-        """Keras parameter count (the zero channels of _pad_stem_channels excluded)."""
-        return sum(u.w.numel() + u.b.numel() for u in self.units.values()) - getattr(self, "_pad_extra", 0)
+        """Keras parameter count."""
+        return sum(u.w.numel() + u.b.numel() for u in self.units.values())
 
     def _branch(self, x, ops_):
         for op in ops_:
@@ -154,8 +130,6 @@ class InceptionV3:
                 break
             if x.is_cuda and FUSED_BLOCKS:
                 x = self.iblocks[bi](x)
-            elif x.is_cuda and BRANCH_STREAMS:
-                x = cat_channels(run_parallel([lambda xx, ops_=br[k]: self._branch(xx, ops_) for k in order], x))
             else:
                 x = cat_channels([self._branch(x, br[k]) for k in order])
             if name in want:

@@ -27,7 +27,8 @@ SUBPIXEL = os.environ.get("DV_SUBPIXEL", "1") != "0"
 COL2IM = os.environ.get("DV_COL2IM", "1") != "0"
 # DV_STEM_DIRECT=0: InceptionV3's conv2d_1 (3 -> 32, 3x3 / 2) on the GEMM (+ col2im) path (A/B)
 STEM_DIRECT = os.environ.get("DV_STEM_DIRECT", "1") != "0"
-STEM_DIRECT7 = os.environ.get("DV_STEM_DIRECT7", "0") != "0"
+# DV_STEM_FUSED=0: ResNet-50 conv1's input gradient as GEMM (cols to HBM) + col2im (A/B)
+STEM_FUSED = os.environ.get("DV_STEM_FUSED", "1") != "0"
 
 
 _PREMASKED = [False]
@@ -116,12 +117,12 @@ class ConvUnit:
                     self.col_w = ConvWeights(wc.contiguous(), None, "fwd").to_device(self.device, dtype)
                     self.col_ld = -(-kh * kw * cr // 8) * 8
                 # few-channel strided stem conv (InceptionV3 conv2d_1): direct VALU kernels for the
-                # forward and the input gradient (csrc/conv_stem.hip), fp32 [kh][kw][c][co] weights
-                # (ResNet-50's 7x7 conv1 input gradient on the same kernel is opt-in, DV_STEM_DIRECT7=1:
-                # 23.4 vs 25.0 img/s on config 5 - 2352 FMAs per pixel lose to GEMM + col2im there)
+                # forward and the input gradient (csrc/conv_stem.hip), fp32 [kh][kw][c][co] weights.
+                # (ResNet-50's 7x7 conv1 measured slower there, 2352 FMAs per pixel: its gradient is
+                # the fused MFMA GEMM + col2im kernel, csrc/conv_stem_dgrad.hip)
                 self.stem_w = None
-                if STEM_DIRECT and cr == 3 and self.stride == 2 and w8.shape[1] == 8 and \
-                        ((kh == kw == 3 and self.cout == 32) or (kh == kw == 7 and self.cout == 64 and STEM_DIRECT7)):
+                if STEM_DIRECT and cr == 3 and self.stride == 2 and w8.shape[1] == 8 and kh == kw == 3 and \
+                        self.cout == 32:
                     self.stem_w = self.w.permute(2, 3, 1, 0).contiguous().to(self.device)
                 # sub-pixel classes: s^2 stride-1 convs instead of one s^2-times-wasteful gather
                 self.bwd_sub = []
@@ -234,10 +235,17 @@ def _dgrad_strided(unit: ConvUnit, gy, mask, in_hw):
 
 def _col2im_dgrad(gy, mask, unit: ConvUnit, in_hw):
     """dx of a strided conv with <= 8 input channels: cols = (dy*mask) @ W^T as a 1x1 conv on the
-    LDS-DMA kernel, then the col2im gather kernel."""
+    LDS-DMA kernel, then the col2im gather kernel; for ResNet-50's conv1 geometry both in ONE kernel
+    (csrc/conv_stem_dgrad.hip: the cols tile never leaves LDS)."""
     N, OH, OW, _ = gy.shape
     H, W = in_hw
     kh, kw = unit.w.shape[2:]
+    if STEM_FUSED and unit.fwd.cin == 8 and unit.pad[0] == unit.pad[1]:
+        gx = torch.empty(N, H, W, 8, dtype=gy.dtype, device=gy.device)
+        m = None if mask is None else mask.contiguous()
+        if native.lib().stem_dgrad_fused(gy.contiguous(), m, unit.col_w.w_gemm, gx,
+                                         [kh, kw, unit.stride, unit.pad[0], unit.w.shape[1]]):
+            return gx
     J = unit.col_w.cout
     cols = torch.empty(N, OH, OW, unit.col_ld, dtype=gy.dtype, device=gy.device)
     conv2d(gy, unit.col_w, stride=1, pad=0, relu=False, mask=mask, use_bias=False, out=cols[..., :J])

@@ -318,7 +318,10 @@ class _InceptionFn(torch.autograd.Function):
                 continue
             chains.append([list(reversed(info)), 0, gsl])
         # conv chains walked backwards in levels (step l of every chain; the gradient w.r.t. each
-        # ReLU output is premasked): one conv_group per level, like the forward
+        # ReLU output is premasked): one conv_group per level, like the forward. Inside a group a
+        # recorded conv runs only at the group's end, so every step that reads a conv result it
+        # launched itself (strided dgrads: sub-pixel GEMMs + copies; a split's accumulating pair)
+        # runs with recording paused
         while any(c[1] < len(c[0]) for c in chains):
             with conv_group(x.device):
                 for c in chains:
@@ -340,7 +343,8 @@ class _InceptionFn(torch.autograd.Function):
                         elif units[0].stride == 1:
                             deferred.append((units[0].bwd, g))
                         else:  # strided head on x: straight into gx (written / accumulated)
-                            dgrad_strided_into(units[0], g, (H, W), gx, accumulate=state["written"])
+                            with conv_group_paused():  # may be GEMMs + torch ops reading them
+                                dgrad_strided_into(units[0], g, (H, W), gx, accumulate=state["written"])
                             state["written"] = True
                             state["masked"] = False
                         continue
@@ -350,8 +354,11 @@ class _InceptionFn(torch.autograd.Function):
                             gi = dgrad_into(ua, g[..., : ua.cout], inp, out=into)
                             dgrad_into(ub, g[..., ua.cout:], inp, out=gi, accumulate=True)
                         c[2] = gi
-                    else:
+                    elif units[0].stride == 1:  # one conv: recorded into the level's group
                         c[2] = dgrad_into(units[0], g, inp, out=into)
+                    else:  # strided: sub-pixel GEMMs + torch ops that read them, in order
+                        with conv_group_paused():
+                            c[2] = dgrad_into(units[0], g, inp, out=into)
         if GT is not None:
             deferred.append((blk.merge[1], GT))
         for cw, g in deferred:

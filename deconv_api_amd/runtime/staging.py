@@ -43,6 +43,20 @@ class Staged:
     ev_comp1: Optional[torch.cuda.Event] = None
     ev_back1: Optional[torch.cuda.Event] = None
     host_out: Optional[torch.Tensor] = None
+    scans: Optional[torch.Tensor] = None  # GPU JPEG: the device scans (copied once their size is known)
+    hw: tuple = (0, 0)
+
+
+@dataclass
+class GpuScans:
+    """A batch's responses as GPU-encoded JPEG scans on the host (codec.gpu_data_urls input)."""
+    packed: torch.Tensor  # uint8 [off[-1]]
+    off: torch.Tensor     # int64 [n + 1]
+    H: int
+    W: int
+
+    def __len__(self) -> int:
+        return self.off.numel() - 1
 
 
 def resize_batch(images: List[np.ndarray], out: torch.Tensor) -> torch.Tensor:
@@ -166,10 +180,40 @@ class StagingRing:
         st.host_out = host
         return st
 
-    def finish(self, st: Staged) -> np.ndarray:
-        """Wait for the batch's copy-back; record per-stage timings; return a host copy."""
+    def copy_back_jpeg(self, st: Staged, mosaic: torch.Tensor, quality: int) -> Staged:
+        """GPU JPEG instead of raw mosaics: the first ``st.n`` mosaics are encoded on the compute
+        stream (csrc/jpeg_gpu.hip) and only the scan offsets are copied back here; ``finish``
+        copies the scans (~10x fewer bytes than the mosaics) once their total size is known."""
+        from ..codec.image import encode_gpu
+
+        n = st.n
+        cur = torch.cuda.current_stream(self.device)
+        packed, off = encode_gpu(mosaic[:n], quality)
+        st.ev_comp1 = torch.cuda.Event(enable_timing=True)
+        st.ev_comp1.record(cur)
+        host_off = torch.empty(n + 1, dtype=torch.int64, pin_memory=True)
+        self.back_stream.wait_event(st.ev_comp1)
+        packed.record_stream(self.back_stream)
+        with torch.cuda.stream(self.back_stream):
+            host_off.copy_(off, non_blocking=True)
+            st.ev_back1 = torch.cuda.Event(enable_timing=True)
+            st.ev_back1.record()
+        st.host_out, st.scans, st.hw = host_off, packed, (mosaic.shape[1], mosaic.shape[2])
+        return st
+
+    def finish(self, st: Staged):
+        """Wait for the batch's copy-back; record per-stage timings; return a host copy (the
+        mosaics, or GpuScans for a copy_back_jpeg batch)."""
         st.ev_back1.synchronize()
         M.STAGE_TIME.observe(st.ev_h2d0.elapsed_time(st.ev_h2d1) / 1e3, stage="h2d")
         M.STAGE_TIME.observe(st.ev_comp0.elapsed_time(st.ev_comp1) / 1e3, stage="compute")
         M.STAGE_TIME.observe(st.ev_comp1.elapsed_time(st.ev_back1) / 1e3, stage="d2h")
+        if st.scans is not None:
+            total = int(st.host_out[-1])
+            packed = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+            with torch.cuda.stream(self.back_stream):
+                packed.copy_(st.scans[:total], non_blocking=True)
+            self.back_stream.synchronize()
+            st.scans = None
+            return GpuScans(packed, st.host_out, *st.hw)
         return st.host_out.numpy()

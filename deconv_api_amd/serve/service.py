@@ -29,6 +29,8 @@ import torch
 
 from .. import ops
 from ..codec import CodecPool, encode_data_url, encode_data_urls, read_data_url
+from ..codec.image import gpu_data_urls
+from ..runtime.staging import GpuScans
 from ..config import Config
 from ..engine.deconvnet import DeconvNet, UnknownLayerError
 from ..models.vgg16 import VGG16
@@ -278,7 +280,13 @@ class DeconvService:
 
     def _encode_deliver(self, group, mos, layer, t0):
         try:
-            if self.native_codec:
+            if isinstance(mos, GpuScans):  # encoded on the GPU: header + scan + EOI, base64, quote
+                urls = gpu_data_urls(mos.packed, mos.off, mos.H, mos.W, self.cfg.jpeg_quality, self.cfg.encode_threads)
+                te = time.perf_counter()
+                for j, m in zip(group, urls):
+                    j.t_enc = te
+                    _deliver(j.loop, _set_result, j.future, m)
+            elif self.native_codec:
                 # GIL-free native JPEG + base64 + quote, in chunks of ``encode_chunk`` images over
                 # the native threads (a lone request is split into restart segments); each chunk
                 # is delivered as soon as it is encoded
@@ -338,6 +346,8 @@ class DeconvService:
             x = torch.empty(n, S, S, 8, dtype=torch.bfloat16, device=self.device)
             st = self.ring.stage(images, x)
             res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
+        if self.cfg.gpu_jpeg:  # JPEG on the device: only the scans cross PCIe
+            return ("staged", self.ring.copy_back_jpeg(st, res.mosaic, self.cfg.jpeg_quality))
         return ("staged", self.ring.copy_back(st, res.mosaic))
 
     def finish_batch(self, handle) -> np.ndarray:

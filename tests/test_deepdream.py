@@ -405,16 +405,14 @@ def test_gpu_tiled_whole_octave_graph_1024(native_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("p,H,W,k,cout", [(0, 37, 41, 3, 32), (0, 40, 38, 3, 32), (1, 33, 36, 3, 32),
-                                          (3, 37, 41, 7, 64), (3, 40, 38, 7, 64)])
-def test_gpu_stem_conv_direct(native_lib, monkeypatch, p, H, W, k, cout):
-    """InceptionV3 conv2d_1 geometry (3 -> 32, 3x3 / stride 2) and ResNet-50 conv1 (3 -> 64, 7x7 / 2; opt-in)
-    on the direct VALU kernels (csrc/conv_stem.hip; the 7x7 forward stays on the GEMM): forward
-    (bias + ReLU) and the input gradient (premasked, as DeepDream runs it) vs CPU autograd and vs
-    the GEMM + col2im path of the same unit."""
+@pytest.mark.parametrize("p,H,W", [(0, 37, 41), (0, 40, 38), (1, 33, 36)])
+def test_gpu_stem_conv_direct(native_lib, p, H, W):
+    """InceptionV3 conv2d_1 geometry (3 -> 32, 3x3 / stride 2) on the direct VALU kernels
+    (csrc/conv_stem.hip): forward (bias + ReLU) and the input gradient (premasked, as DeepDream runs
+    it) vs CPU autograd and vs the GEMM + col2im path of the same unit."""
     from deconv_api_amd.ops import autograd as AG
 
-    monkeypatch.setattr(AG, "STEM_DIRECT7", True)
+    k, cout = 3, 32
     g = torch.Generator().manual_seed(H * W + p)
     w = (torch.randn(cout, 3, k, k, generator=g) / (3 * k * k) ** 0.5).to(torch.bfloat16).float()
     b = torch.randn(cout, generator=g) * 0.1
@@ -441,6 +439,47 @@ def test_gpu_stem_conv_direct(native_lib, monkeypatch, p, H, W, k, cout):
         assert (gd[..., :3] - gc).abs().max() < 2e-2 * gc.abs().max()
     assert float(outs["direct"][1][..., 3:].abs().max()) == 0.0  # padding channels get no gradient
     assert (outs["direct"][1][..., :3] - outs["gemm"][1][..., :3]).abs().max() < 2e-2 * gc.abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("H,W,premasked", [(37, 41, True), (64, 96, True), (150, 133, False), (224, 224, True)])
+def test_gpu_stem_dgrad_fused(native_lib, monkeypatch, dt, H, W, premasked):
+    """ResNet-50 conv1 (3 -> 64, 7x7 / 2, pad 3) input gradient: the fused MFMA GEMM + col2im kernel
+    (csrc/conv_stem_dgrad.hip) equals the two-kernel GEMM (cols in HBM) + col2im path BIT FOR BIT
+    (same fp32 accumulation order, same 16-bit rounding of the cols) and CPU autograd up to rounding;
+    several dx tiles, odd sizes, with the ReLU mask (not premasked) and without."""
+    from deconv_api_amd.ops import autograd as AG
+
+    g = torch.Generator().manual_seed(H + W)
+    w = (torch.randn(64, 3, 7, 7, generator=g) / (3 * 49) ** 0.5).to(dt).float()
+    b = torch.randn(64, generator=g) * 0.1
+    x = torch.randn(2, H, W, 3, generator=g).to(dt).float()
+    cpu = AG.ConvUnit("u", w, b, 2, (3, 3), relu=True).build("cpu")
+    gpu = AG.ConvUnit("u", w, b, 2, (3, 3), relu=True).build("cuda", dt)
+    assert gpu.stem_w is None and gpu.col_w is not None
+    xc = x.clone().requires_grad_(True)
+    yc = cpu(xc)
+    gy = torch.randn(*yc.shape, generator=g)
+    if premasked:
+        gy = gy * (yc > 0)
+    gy = gy.to(dt).float()
+    (gc,) = torch.autograd.grad(yc, xc, gy)
+    x8 = torch.nn.functional.pad(x, (0, 5)).to(dt).cuda()
+    outs = {}
+    for fused in (True, False):
+        monkeypatch.setattr(AG, "STEM_FUSED", fused)
+        xd = x8.clone().requires_grad_(True)
+        if premasked:
+            with AG.premasked_grads():
+                yd = gpu(xd)
+        else:
+            yd = gpu(xd)
+        (gd,) = torch.autograd.grad(yd, xd, gy.to(dt).cuda())
+        outs[fused] = gd.float().cpu()
+    assert torch.equal(outs[True], outs[False])
+    assert float(outs[True][..., 3:].abs().max()) == 0.0
+    assert (outs[True][..., :3] - gc).abs().max() < 2e-2 * gc.abs().max()
 
 
 @pytest.mark.gpu

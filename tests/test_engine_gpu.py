@@ -111,7 +111,21 @@ def test_service_end_to_end_gpu(native_lib):
         # (batch composition may change split-K summation order -> rounding-level differences)
         d = np.abs(parse_result_data_url(outs[0]).astype(int) - parse_result_data_url(encode_data_url(want)).astype(int))
         assert d.mean() < 1.0
-        # before JPEG: the service's batched mosaics == the engine's, to rounding
+        # the service encodes on the GPU by default: its scans decode to the engine's mosaics
+        from deconv_api_amd.codec.image import gpu_jpeg_bytes
+        from deconv_api_amd.runtime.staging import GpuScans
+
+        sc = svc.run_batch("block3_pool", imgs)
+        assert isinstance(sc, GpuScans) and len(sc) == len(imgs)
+        from PIL import Image
+        import io
+
+        dec = np.asarray(Image.open(io.BytesIO(gpu_jpeg_bytes(sc.packed, sc.off, 0, 448, 448))).convert("RGB"))
+        assert np.abs(dec.astype(int) - parse_result_data_url(outs[0]).astype(int)).mean() < 1.0
+        # before JPEG (gpu_jpeg off): the service's batched mosaics == the engine's, to rounding
+        import dataclasses
+
+        svc.cfg = dataclasses.replace(svc.cfg, gpu_jpeg=False)
         raw = svc.run_batch("block3_pool", imgs)
         ref = eng.run(svc.preprocess(imgs), "block3_pool", k=4).mosaic.cpu().numpy()
         assert np.abs(raw.astype(int) - ref.astype(int)).max() <= 2
