@@ -69,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--tiny", action="store_true", help="scaled VGG16 at 32px (CPU rehearsal only)")
     ap.add_argument("--breakdown", action="store_true", help="per-phase timing to stderr (extra syncs)")
+    ap.add_argument("--no-copyback", action="store_true",
+                    help="DIAGNOSTIC ONLY (not a benchmark number): skip the mosaics' copy to the host, to price it")
     ap.add_argument("--profile", nargs="?", const="trace", default=None, choices=["trace", "pmc"],
                     help="re-run under rocprofv3 and print a per-kernel table (trace) [+ PMC pass]")
     return ap.parse_args(argv)
@@ -178,18 +180,45 @@ def main(argv=None):
 
     off_host = [torch.empty(B + 1, dtype=torch.int64, pin_memory=cuda) for _ in range(2)]
     scans_host = [None, None]
+    # JPEG mode with N > 1: step i's scans are all-gathered from step i+1's hook, padded to the
+    # largest scan total over the ranks (an all-reduce issued at step i, read on the host at the
+    # hook), i.e. ~10x fewer xGMI bytes than gathering the raw mosaics
+    mx_host = [torch.empty(1, dtype=torch.int64, pin_memory=cuda) for _ in range(2)]
+    jpeg_bytes = []  # scan bytes per image, per step
+    gpend = [None, None]
+    gscans = [None, None]
+    goff = [torch.empty(info.world * (B + 1), dtype=torch.int64, device=dev) for _ in range(2)]
+
+    def issue_gather(slot):
+        if gpend[slot] is None:
+            return
+        packed, off, mx_ev = gpend[slot]
+        gpend[slot] = None
+        if pending[slot] is not None:
+            pending[slot].wait()  # the gather that last used this slot's buffers (step i-2)
+        mx_ev.synchronize()
+        cap = -(-int(mx_host[slot][0]) // (1 << 16)) * (1 << 16)  # 64 KiB granules: stable sizes
+        if gscans[slot] is None or gscans[slot].numel() < info.world * cap:
+            gscans[slot] = torch.empty(info.world * cap, dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(goff[slot], off, async_op=False)
+        pending[slot] = dist.all_gather_into_tensor(gscans[slot][: info.world * cap], packed[:cap], async_op=True)
 
     def issue_copy():
         if deferred[0] is None:
+            return
+        if args.no_copyback:
+            deferred[0] = None
             return
         slot, mosaic, ev0 = deferred[0]
         deferred[0] = None
         if back_done[slot] is not None:
             back_done[slot].synchronize()  # host slot free again (its step i-2 copy landed)
         if JPEG:  # mosaic = (device scans, event of the offsets' copy into off_host[slot])
+            issue_gather(slot)
             packed, off_ev = mosaic
             off_ev.synchronize()  # step i's scan sizes (long done: the GPU is in step i+1)
             total = int(off_host[slot][-1])
+            jpeg_bytes.append(total / B)
             if scans_host[slot] is None or scans_host[slot].numel() < total:
                 scans_host[slot] = torch.empty(max(total, 1) * 5 // 4, dtype=torch.uint8, pin_memory=True)
             with torch.cuda.stream(copy_stream):
@@ -217,7 +246,7 @@ def main(argv=None):
         if cuda:
             issue_copy()  # no-op when the hook already issued step i-1's copy
         slot = i % 2
-        if info.backend != "none":
+        if info.backend != "none" and not (JPEG and cuda):
             if pending[slot] is not None:
                 pending[slot].wait()  # the gather that last used this buffer (step i-2)
             pending[slot] = dist.all_gather_into_tensor(gathered[slot], res.mosaic.contiguous(), async_op=True)
@@ -234,6 +263,15 @@ def main(argv=None):
                     off_ev = torch.cuda.Event()
                     off_ev.record()
                 out = (packed, off_ev)
+                if info.backend != "none":  # the largest scan total over the ranks (for the gather)
+                    mx = off[-1:].clone()
+                    work = dist.all_reduce(mx, op=dist.ReduceOp.MAX, async_op=True)
+                    with torch.cuda.stream(copy_stream):
+                        work.wait()  # the copy stream (not the compute stream) waits for the collective
+                        mx_host[slot].copy_(mx, non_blocking=True)
+                        mx_ev = torch.cuda.Event()
+                        mx_ev.record()
+                    gpend[slot] = (packed, off, mx_ev)
             deferred[0] = (slot, out, ev0)
             if not COPY_AT:
                 issue_copy()
@@ -307,6 +345,7 @@ def main(argv=None):
         "baseline_img_per_s": REF_IMG_PER_S,
         "dtype": "bf16" if cuda else "fp32",
         "gpu_jpeg": bool(JPEG and cuda),
+        **({"jpeg_scan_bytes_per_image": round(sum(jpeg_bytes) / len(jpeg_bytes))} if jpeg_bytes else {}),
         "process_group": info.backend,
         "data": "synthetic uint8 224x224 images, seeded random-init VGG16 weights",
         "config": {"model": f"vgg16_deconvnet_{args.layer}", "global_batch": B * info.world, "seq_len": S,
@@ -314,6 +353,8 @@ def main(argv=None):
     }
     if args.tiny:
         line["data"] = "REHEARSAL: scaled VGG16 (width/8, 32px) on CPU - not a benchmark"
+    if args.no_copyback:
+        line["data"] = "DIAGNOSTIC: mosaics not copied back to the host - not a benchmark"
     if info.is_main:
         print(json.dumps(line), flush=True)
     pdist.shutdown()

@@ -785,8 +785,11 @@ namespace {
 __device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; }
 }  // namespace
 
-// BN_: 256 (8 waves of 128 x 64) or 128 (8 waves of 64 x 64) output channels per workgroup
-template <int DT, int EPI, bool FP, int BN_ = 256>
+// BN_: 256 (8 waves of 128 x 64) or 128 (8 waves of 64 x 64) output channels per workgroup.
+// (Measured and removed, round 3: issuing the next step's DMAs in three parts between the kw
+// sub-steps' fragment reads and MFMAs instead of all right after the barrier: config 2 fell from
+// 6.85-7.03k to 5.80-5.83k img/s, profiles/bench_c2_r3_ab.txt.)
+template <int DT, int EPI, int BN_ = 256>
 __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
   constexpr int BN = BN_, BM = 256, NW = 8;
   constexpr int WN = BN == 256 ? 4 : 2, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
@@ -876,36 +879,6 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
     if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
     const uint8_t* As = smem + (k & 1) * STAGE;
     const uint8_t* Bs = As + A_BYTES;
-    if constexpr (FP) {
-      // the next kw's B fragments are read before this kw's MFMAs (a full A+B double buffer spills);
-      // each A fragment is read right before its row of MFMAs
-      v8 bf[2][FN];
-      auto ldb = [&](int kw, int b) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          bf[b][j] = *reinterpret_cast<const v8*>(Bs + kw * (BN * 64) + (brow0 + j * 16) * 64 + bswz);
-      };
-      ldb(0, 0);
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        if (kw < 2) ldb(kw + 1, (kw + 1) & 1);
-        v8 af[FM];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int sr = arow0 + i * 16 + kw;
-          af[i] = *reinterpret_cast<const v8*>(As + sr * 64 + ((q ^ kw3_swz(sr)) << 4));
-          if ((kw == 0 && ((left >> i) & 1)) || (kw == 2 && ((right >> i) & 1)))
-            af[i] = __builtin_bit_cast(v8, make_uint4(0u, 0u, 0u, 0u));
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bf[kw & 1][j], acc[i][j]);
-        __builtin_amdgcn_s_setprio(0);
-      }
-      continue;
-    }
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       v8 bf[FN], af[FM];
@@ -964,13 +937,9 @@ static int kw3_try(const ConvArgs& a, hipStream_t s) {
     const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / BN;
     const long long nwg = (long long)tiles_m * tiles_n;
     if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
-    // DV_KW3_FP=1: B fragments double-buffered across the kw sub-steps (measured equal to the plain
-    // loop, profiles/layers_r1_kw3_{nofp,on}.txt; a full A+B double buffer spills)
-    const char* fp = std::getenv("DV_KW3_FP");
-    if (fp != nullptr && std::atoi(fp) != 0)
-      hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, true, BN>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
-    else
-      hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, false, BN>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
+    // (a B-fragment double buffer across the kw sub-steps measured equal and was removed,
+    // profiles/layers_r1_kw3_{nofp,on}.txt)
+    hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
     return (int)hipGetLastError();
   }
 }

@@ -376,7 +376,6 @@ class TiledDeepDream(DeepDream):
         self.tile_graphs = use_graphs and self.device.type == "cuda"
         self._tgraphs: "OrderedDict[tuple, object]" = OrderedDict()
         self.tile_fused = FUSED_STEP and self.device.type == "cuda"
-        self._shift_pin, self._shift_ev = None, None
 
     @staticmethod
     def _axis_tiles(L: int, tile: int):
@@ -547,17 +546,20 @@ class TiledDeepDream(DeepDream):
 
     def _stage_shifts(self, st) -> None:
         """This octave's random roll table -> the device, without a host sync: through a pinned
-        buffer (a pageable H2D copy blocks the host until the stream drains, once per octave)."""
+        buffer of the octave's own state (a pageable H2D copy blocks the host until the stream
+        drains; one shared pinned buffer would make octave k+1 wait for octave k's upload, which
+        queues behind octave k-1's replay)."""
         shifts = torch.randint(-self.tile // 2, self.tile // 2 + 1, (self.s.iterations, 2), generator=self.gen)
-        pin = getattr(self, "_shift_pin", None)
+        pin = getattr(st, "shift_pin", None)
         if pin is None or pin.shape != shifts.shape:
-            pin = self._shift_pin = torch.empty(shifts.shape, dtype=torch.int32, pin_memory=True)
-        elif self._shift_ev is not None:
-            self._shift_ev.synchronize()  # the previous octave's upload from this buffer (long done)
+            pin = st.shift_pin = torch.empty(shifts.shape, dtype=torch.int32, pin_memory=True)
+            st.shift_ev = None
+        if st.shift_ev is not None:
+            st.shift_ev.synchronize()  # this shape's previous upload (the previous dream batch)
         pin.copy_(shifts)
         st.shifts.copy_(pin, non_blocking=True)
-        self._shift_ev = torch.cuda.Event()
-        self._shift_ev.record()
+        st.shift_ev = torch.cuda.Event()
+        st.shift_ev.record()
 
     def _capture(self, fn) -> torch.cuda.CUDAGraph:
         g = torch.cuda.CUDAGraph()

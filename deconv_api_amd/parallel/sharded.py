@@ -348,6 +348,9 @@ class ShardedRunner:
             return ("host", mos[:n].numpy())
         if st is not None and self.ring is not None:  # reuse the staging ring's slot + stream
             st.n = n
+            if self.cfg is None or self.cfg.gpu_jpeg:  # JPEG on rank 0's GPU: only scans cross PCIe
+                q = self.cfg.jpeg_quality if self.cfg is not None else 95
+                return ("staged", self.ring.copy_back_jpeg(st, mos, q))
             return ("staged", self.ring.copy_back(st, mos))
         host = torch.empty((n, *mos.shape[1:]), dtype=mos.dtype, pin_memory=True)
         host.copy_(mos[:n], non_blocking=True)

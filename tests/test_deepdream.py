@@ -517,13 +517,16 @@ def test_gpu_tiled_virtual_ranks_match_one_rank(native_lib, world):
     from deconv_api_amd.models.resnet50 import ResNet50
 
     net = ResNet50(0).build("cuda", torch.float16)
-    s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=1, iterations=3, max_loss=None)
     x = (torch.rand(2, 256, 320, 3, generator=torch.Generator().manual_seed(3)) * 2 - 1).cuda()
-    ref = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).gradient_ascent(x)
-    got = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).virtual_octave(x, world)
-    d = (got - ref).abs()
-    assert _cos((got - x).flatten().cpu(), (ref - x).flatten().cpu()) > 0.999
-    assert float(d.mean()) < 1e-3 and float(d.max()) < 5e-2, (float(d.mean()), float(d.max()))
+    # one step: only the first gradient's rounding differs; three steps: fp16 rounding feeds back
+    for iters, cos_min, mean_max in ((1, 0.9995, 1e-3), (3, 0.995, 3e-3)):
+        s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=1, iterations=iters, max_loss=None)
+        ref = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).gradient_ascent(x)
+        got = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).virtual_octave(x, world)
+        d = (got - ref).abs()
+        c = _cos((got - x).flatten().cpu(), (ref - x).flatten().cpu())
+        assert c > cos_min, (iters, c)
+        assert float(d.mean()) < mean_max and float(d.max()) < 5e-2, (iters, float(d.mean()), float(d.max()))
 
 
 @pytest.mark.gpu

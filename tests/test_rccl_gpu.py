@@ -51,3 +51,13 @@ def test_bench_under_torchrun_uses_rccl():
     out = _torchrun(["bench.py", "--gpus", "1", "--steps", "2", "--warmup", "1", "--batch", "8"])
     assert out["process_group"] == "nccl" and out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1"
     assert out["value"] > 0 and out["p50_req_latency_ms"] >= out["p50_batch_latency_ms"] * 0.5
+
+
+@pytest.mark.gpu
+def test_bench_gpu_jpeg_gather_under_torchrun(monkeypatch):
+    """bench.py's GPU-JPEG mode on a real RCCL group: per-step scans, the max-size all-reduce and the
+    deferred exact-size all-gather of the scans (the N > 1 data path, at world 1)."""
+    monkeypatch.setenv("DV_BENCH_JPEG", "1")
+    out = _torchrun(["bench.py", "--gpus", "1", "--steps", "3", "--warmup", "1", "--batch", "8"])
+    assert out["process_group"] == "nccl" and out["gpu_jpeg"] is True and out["value"] > 0, out
+    assert 1000 < out["jpeg_scan_bytes_per_image"] < 600000, out

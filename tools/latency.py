@@ -133,6 +133,7 @@ def main():
     ap.add_argument("--switch-us", type=int, default=500)
     ap.add_argument("--enc-workers", type=int, default=2)
     ap.add_argument("--enc-threads", type=int, default=8)
+    ap.add_argument("--gpu-jpeg", type=int, default=1, help="1: responses JPEG-encoded on the GPU (csrc/jpeg_gpu.hip)")
     a = ap.parse_args()
     ops.native.load()
     dev = torch.device("cuda", 0)
@@ -140,7 +141,7 @@ def main():
     res = {"engine": engine_latency(eng, a.layer, [int(s) for s in a.sizes.split(",")], a.reps)}
     cfg = Config.from_env(device="cuda", max_batch=a.max_batch, batch_timeout_ms=a.timeout_ms, codec_workers=a.codec_workers,
                           encode_chunk=a.chunk, gil_switch_us=a.switch_us,
-                          encode_workers=a.enc_workers, encode_threads=a.enc_threads)
+                          encode_workers=a.enc_workers, encode_threads=a.enc_threads, gpu_jpeg=bool(a.gpu_jpeg))
     svc = DeconvService(cfg, engine=eng)
     res["service"] = []
     clients = [int(x) for x in a.clients.split(",")]
@@ -162,7 +163,7 @@ def main():
     res["stage_metrics"] = [l for l in M.REGISTRY.render().splitlines() if l.startswith("dv_stage_seconds_sum")
                             or l.startswith("dv_stage_seconds_count")]
     res["graphs"] = svc.status()["graphs"]
-    res["settings"] = {"enc": [a.enc_workers, a.enc_threads], "switch_us": a.switch_us, "max_batch": a.max_batch, "timeout_ms": a.timeout_ms, "chunk": a.chunk, "codec_workers": a.codec_workers}
+    res["settings"] = {"enc": [a.enc_workers, a.enc_threads], "switch_us": a.switch_us, "max_batch": a.max_batch, "timeout_ms": a.timeout_ms, "chunk": a.chunk, "codec_workers": a.codec_workers, "gpu_jpeg": bool(a.gpu_jpeg)}
     svc.close()
     print(json.dumps(res))
 
