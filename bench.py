@@ -40,16 +40,14 @@ from deconv_api_amd.models.vgg16 import VGG16, vgg16_specs
 from deconv_api_amd.parallel import dist as pdist
 from deconv_api_amd.runtime.streams import copy_stream as copy_stream_for
 
-# Where each step's mosaic copy-back (of the PREVIOUS step) is issued: right before this layer's
-# forward conv (DV_BENCH_COPY_AT; "" = right after the step that produced it). The D2H copy runs as
-# a blit kernel that waits on PCIe (154 MB, ~2.8 ms); next to memory-bound kernels it slows them
-# (the 58 us input kernel took 2.3 ms beside it, profiles/copyback_overlap_r2.txt), next to MFMA-
-# bound ones it costs little (tools/copy_overlap_probe.py: a GEMM loop 9.06 -> 9.18 ms). block3's
-# convs are the first MFMA-bound layers of the step.
-COPY_AT = os.environ.get("DV_BENCH_COPY_AT", "block3_conv1")
 # DV_BENCH_JPEG=1: each step also JPEG-encodes its mosaics on the GPU (csrc/jpeg_gpu.hip, what the
-# service does) and copies back the scans instead of the raw mosaics (~10x fewer PCIe bytes)
+# service does) and copies back only the scans (~10x fewer PCIe bytes). Sizing that copy needs the
+# step's scan total on the host, so it is issued from inside the NEXT step's forward, right before
+# block3_conv1 (the engine's layer hook): by then the GPU has finished the step and still has the
+# next step's first layers queued. Raw mosaics are copied right after their step is enqueued (the
+# copy costs ~0.2 % of the step: --no-copyback 7016 vs 6999 img/s, profiles/bench_c2_r3_copy_ab.txt).
 JPEG = os.environ.get("DV_BENCH_JPEG", "0") == "1"
+COPY_AT = "block3_conv1" if JPEG else ""
 
 # the reference's implied end-to-end rate for layer=block5_conv3 is ~0.03-0.04 img/s
 # (CPU, one request at a time; a lower bound on its cost). We divide by the favourable 0.04.
@@ -321,9 +319,8 @@ def main(argv=None):
     else:
         per_step = sorted(1e3 * t for t in host_steps)
     p50 = pdist.all_reduce_max(per_step[len(per_step) // 2], info)
-    if cuda:
-        req = sorted(a.elapsed_time(b) for a, b in lat)
-    else:
+    req = sorted(a.elapsed_time(b) for a, b in lat) if cuda else []
+    if not req:  # CPU, or --no-copyback (nothing delivered): the batch latency stands in
         req = per_step
     p50_req = pdist.all_reduce_max(req[len(req) // 2], info)
 

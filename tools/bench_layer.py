@@ -21,6 +21,9 @@ CASES = {
     "b1c1down": (1024, 224, 224, 64, 3, False, "f32"),
     "b2c1down": (1024, 112, 112, 128, 64, False, "bf16"),
     "b4c2down": (1024, 28, 28, 512, 512, False, "bf16"),
+    "b3c2down": (1024, 56, 56, 256, 256, False, "bf16"),
+    "b5c2down": (1024, 14, 14, 512, 512, False, "bf16"),
+    "b3c2fwd": (256, 56, 56, 256, 256, False, "bf16"),
     "b1c2fwd": (256, 224, 224, 64, 64, False, "pool"),
     "b1c1fwd": (256, 224, 224, 8, 64, False, "bf16"),
 }

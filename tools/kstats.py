@@ -14,7 +14,8 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    name = re.sub(r"\(.*\)$", "", name.replace("void ", ""))
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    name = re.sub(r"\(.*\)$", "", name)
     return name[:110]
 
 

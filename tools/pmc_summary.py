@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Per-kernel sums of rocprofv3 PMC counters from *counter_collection.csv files (one or more
-passes), with the derived stall fractions used in docs/KERNELS.md:
+passes) or rocpd SQLite databases (*.db: rocprofv3's default output in ROCm 7), with the derived
+stall fractions used in docs/KERNELS.md:
   mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CYCLES * 4 SIMDs... reported raw)
   wait_any / wave_cycles, wait_inst_any / wave_cycles, lds_bank_conflict / lds_idx_active.
   python tools/pmc_summary.py DIR [--top 12]"""
@@ -25,7 +26,18 @@ def main():
             tot[name][row["Counter_Name"]] += float(row["Counter_Value"])
             if "End_Timestamp" in row and "Start_Timestamp" in row:
                 dur[name] += (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3
-    names = sorted(tot, key=lambda n: -tot[n].get("SQ_WAVE_CYCLES", tot[n].get("SQ_BUSY_CYCLES", 0)))
+    import sqlite3
+
+    for f in glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True) + ([a.dir] if a.dir.endswith(".db") else []):
+        seen = set()
+        for kname, cname, val, disp, d in sqlite3.connect(f).execute(
+                "select kernel_name, counter_name, value, dispatch_id, duration from counters_collection"):
+            name = re.sub(r"\(.*\)$", "", kname.replace("void ", "").replace("(anonymous namespace)::", ""))[:90]
+            tot[name][cname] += float(val)
+            if (name, disp) not in seen:
+                seen.add((name, disp))
+                dur[name] += d / 1e3
+    names = sorted(tot, key=lambda n: -dur.get(n, 0.0))
     for n in names[: a.top]:
         c = tot[n]
         wc = c.get("SQ_WAVE_CYCLES", 0) or 1
@@ -47,7 +59,7 @@ def main():
             der.append(f"mfma_util {c['SQ_VALU_MFMA_BUSY_CYCLES'] / (c['GRBM_GUI_ACTIVE'] / 8 * 1024):.2f}")
         if "FETCH_SIZE" in c and dur.get(n):
             # FETCH_SIZE (KB) reads 1/2 of wide coalesced streaming bytes on gfx950 (MI355X_MICROARCH.md)
-            der.append(f"fetch {2 * c['FETCH_SIZE'] / 1e6:.2f} GB ({2 * c['FETCH_SIZE'] * 1e3 / (dur[n] * 1e3):.2f} TB/s x2-corrected)")
+            der.append(f"fetch {2 * c['FETCH_SIZE'] / 1e6:.2f} GB ({2 * c['FETCH_SIZE'] * 1e-3 / dur[n]:.2f} TB/s x2-corrected)")
         if dur.get(n):
             der.append(f"dur {dur[n] / 1e3:.2f} ms")
         print(f"== {n}\n   {'; '.join(der)}\n   {out}")
