@@ -76,7 +76,19 @@ def decode_image(data: bytes) -> np.ndarray:
 
 
 def read_data_url(uri: str) -> np.ndarray:
-    """The reference's ``readb64``."""
+    """The reference's ``readb64``. With the extension built, the payload is split out and
+    base64-decoded natively with the GIL released (csrc/jpeg_enc.cpp:data_url_b64decode, CPython's
+    non-strict semantics and messages): the Python decode held the GIL ~0.24 ms per 60 KB request,
+    serialized across the codec pool's threads."""
+    lib = _native()
+    if lib is not None and isinstance(uri, str) and uri.isascii():
+        if "," not in uri:
+            split_data_url(uri)  # raises the data-URL error
+        try:
+            data = lib.data_url_b64decode(uri)
+        except ValueError as e:
+            raise ImageDecodeError(f"bad base64 payload: {e}") from e
+        return decode_image(data)
     return decode_image(b64decode_lenient(split_data_url(uri)))
 
 
@@ -124,6 +136,13 @@ def encode_data_urls(mosaics: np.ndarray, quality: int = JPEG_QUALITY, threads: 
 
     return lib.jpeg_data_urls(torch.from_numpy(np.ascontiguousarray(mosaics, dtype=np.uint8)), int(quality),
                               DATA_URL_PREFIX, int(threads))
+
+
+def gpu_jpeg_fits(W: int) -> bool:
+    """Whether ``encode_gpu`` takes images of width ``W`` (one MCU row per workgroup, in LDS)."""
+    from ..ops import native
+
+    return int(W) <= native.lib().jpeg_gpu_max_width()
 
 
 def encode_gpu(mosaics, quality: int = JPEG_QUALITY):

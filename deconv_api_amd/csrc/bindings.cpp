@@ -782,7 +782,8 @@ std::vector<Tensor> jpeg_gpu(Tensor img, int64_t quality) {
               "jpeg_gpu: uint8 [B, H, W, 3] contiguous");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(img.device());
   const int B = (int)img.size(0), H = (int)img.size(1), W = (int)img.size(2);
-  TORCH_CHECK(B >= 1 && H >= 1 && W >= 1 && H <= 65500 && W <= 65500, "jpeg_gpu: image size");
+  TORCH_CHECK(B >= 1 && B <= 65535 && H >= 1 && W >= 1 && H <= 65500 && W <= dv::jpeg_gpu_max_width(),
+              "jpeg_gpu: image size (W <= ", dv::jpeg_gpu_max_width(), ")");
   static std::mutex mu;
   static std::map<std::pair<int, int>, Tensor> tables;  // (device, quality) -> device GpuTables
   Tensor tab;
@@ -798,8 +799,7 @@ std::vector<Tensor> jpeg_gpu(Tensor img, int64_t quality) {
     }
     tab = it->second;
   }
-  long long raw_words = 0, out_cap = 0;
-  dv::jpeg_gpu_caps(H, W, &raw_words, &out_cap);
+  const long long out_cap = dv::jpeg_gpu_out_cap(H, W);
   auto opt = img.options();
   Tensor ws = at::empty({dv::jpeg_gpu_ws_bytes(B, H, W)}, opt);
   Tensor packed = at::empty({(int64_t)B * out_cap}, opt);
@@ -809,6 +809,24 @@ std::vector<Tensor> jpeg_gpu(Tensor img, int64_t quality) {
                                cur_stream()),
            "jpeg_gpu");
   return {packed, off};
+}
+
+// data URL (ASCII str) -> decoded payload bytes, GIL released while decoding; raises ValueError
+// with CPython's base64 message (the caller maps it to a 400), TypeError for a non-ASCII str
+py::bytes data_url_b64decode(py::str uri) {
+  PyObject* o = uri.ptr();
+  if (!PyUnicode_IS_ASCII(o)) throw py::type_error("string argument should contain only ASCII characters");
+  Py_ssize_t n = 0;
+  const char* p = PyUnicode_AsUTF8AndSize(o, &n);  // the str's own ASCII buffer: no copy
+  if (p == nullptr) throw py::error_already_set();
+  std::string out, err;
+  bool ok;
+  {
+    py::gil_scoped_release nogil;
+    ok = dvjpeg::data_url_b64decode(p, (size_t)n, out, err);
+  }
+  if (!ok) throw py::value_error(err);
+  return py::bytes(out);
 }
 
 py::bytes jpeg_gpu_header(int64_t H, int64_t W, int64_t quality) {
@@ -1146,7 +1164,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");
   m.def("softmax_rows", &softmax_rows, "row softmax (classifier head)");
   m.def("jpeg_gpu", &jpeg_gpu, "GPU baseline JPEG scans of uint8 [B,H,W,3] (restart per MCU row)");
+  m.def("data_url_b64decode", &data_url_b64decode, "data URL payload -> bytes (lenient base64, GIL released)");
   m.def("jpeg_gpu_header", &jpeg_gpu_header, "SOI..SOS of the GPU encoder's streams");
+  m.def("jpeg_gpu_max_width", &dv::jpeg_gpu_max_width, "widest image the GPU encoder takes");
   m.def("jpeg_gpu_data_urls", &jpeg_gpu_data_urls, "GPU scans -> data URLs (host base64, GIL released)");
   m.def("jpeg_encode", &jpeg_encode, "native baseline JPEG encode (GIL released)");
   m.def("channel_sum", &channel_sum);

@@ -788,7 +788,9 @@ __device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; 
 // BN_: 256 (8 waves of 128 x 64) or 128 (8 waves of 64 x 64) output channels per workgroup.
 // (Measured and removed, round 3: issuing the next step's DMAs in three parts between the kw
 // sub-steps' fragment reads and MFMAs instead of all right after the barrier: config 2 fell from
-// 6.85-7.03k to 5.80-5.83k img/s, profiles/bench_c2_r3_ab.txt.)
+// 6.85-7.03k to 5.80-5.83k img/s, profiles/bench_c2_r3_ab.txt. Equal within noise and removed:
+// static priority for waves 4-7 instead of the per-sub-step flips, a 320-row M tile, and the DMAs
+// issued behind the first sub-step's fragment reads, profiles/kw3_variants_r3.txt.)
 template <int DT, int EPI, int BN_ = 256>
 __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
   constexpr int BN = BN_, BM = 256, NW = 8;
@@ -847,6 +849,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
     uint8_t* Bs = As + A_BYTES;
 #pragma unroll
     for (int u = 0; u < A_I; ++u) {
+      if ((u * NW + wave) * 16 >= BM + 2) continue;  // staged rows past the tile's BM + 2 are never read
       const bool ok = (unsigned)(r_oh[u] + kh - 1) < (unsigned)H;
       const uint32_t voff =
           ok ? (uint32_t)((((long long)(r_pix[u] + (kh - 1) * W)) * a.x_ld + cc * 32 + lchunk * 8) * 2) : kOOB;

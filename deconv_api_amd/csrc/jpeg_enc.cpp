@@ -540,4 +540,77 @@ std::vector<std::string> encode_data_urls(const uint8_t* rgb, int B, int H, int 
   return out;
 }
 
+// Request side: the payload of a data URL (text between the first and second comma, the
+// reference's uri.split(',')[1]) base64-decoded the way CPython's non-strict a2b_base64 does it
+// (base64.b64decode(s), validate=False): characters outside the alphabet are skipped, a '=' that
+// completes a quad (at least two data characters before it) ends the input, and a quad left open
+// at the end is an error. Returns false with CPython's message on error.
+bool data_url_b64decode(const char* uri, size_t n, std::string& out, std::string& err) {
+  static const struct Table {
+    int8_t v[256];
+    Table() {
+      for (int i = 0; i < 256; ++i) v[i] = -1;
+      const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+      for (int i = 0; i < 64; ++i) v[(uint8_t)a[i]] = (int8_t)i;
+    }
+  } T;
+  const char* c1 = static_cast<const char*>(std::memchr(uri, ',', n));
+  if (c1 == nullptr) {
+    err = "not a data URL";
+    return false;
+  }
+  const char* p = c1 + 1;
+  const char* end = uri + n;
+  if (const char* c2 = static_cast<const char*>(std::memchr(p, ',', (size_t)(end - p)))) end = c2;
+  out.resize((size_t)(end - p) / 4 * 3 + 3);
+  uint8_t* o = reinterpret_cast<uint8_t*>(&out[0]);
+  int quad = 0, pads = 0;
+  long long ndata = 0;
+  uint32_t left = 0;
+  bool stop = false;
+  while (p < end && !stop) {
+    // fast path: whole quads of alphabet characters (the common, clean payload)
+    while (quad == 0 && end - p >= 4) {
+      const int a = T.v[(uint8_t)p[0]], b = T.v[(uint8_t)p[1]], c = T.v[(uint8_t)p[2]], d = T.v[(uint8_t)p[3]];
+      if ((a | b | c | d) < 0) break;
+      const uint32_t w = ((uint32_t)a << 18) | ((uint32_t)b << 12) | ((uint32_t)c << 6) | (uint32_t)d;
+      o[0] = (uint8_t)(w >> 16);
+      o[1] = (uint8_t)(w >> 8);
+      o[2] = (uint8_t)w;
+      o += 3;
+      p += 4;
+      ndata += 4;
+      pads = 0;
+    }
+    if (p >= end) break;
+    const uint8_t ch = (uint8_t)*p++;
+    if (ch == '=') {
+      if (quad >= 2 && quad + ++pads >= 4) stop = true;  // a completed pad sequence ends the input
+      continue;
+    }
+    const int v = T.v[ch];
+    if (v < 0) continue;
+    pads = 0;
+    ++ndata;
+    switch (quad) {
+      case 0: left = (uint32_t)v; quad = 1; break;
+      case 1: *o++ = (uint8_t)((left << 2) | (uint32_t)(v >> 4)); left = (uint32_t)v & 0xF; quad = 2; break;
+      case 2: *o++ = (uint8_t)((left << 4) | (uint32_t)(v >> 2)); left = (uint32_t)v & 0x3; quad = 3; break;
+      default: *o++ = (uint8_t)((left << 6) | (uint32_t)v); quad = 0; break;
+    }
+  }
+  out.resize((size_t)(o - reinterpret_cast<uint8_t*>(&out[0])));
+  if (stop) return true;
+  if (quad == 1) {
+    err = "Invalid base64-encoded string: number of data characters (" + std::to_string(ndata) +
+          ") cannot be 1 more than a multiple of 4";
+    return false;
+  }
+  if (quad != 0) {
+    err = "Incorrect padding";
+    return false;
+  }
+  return true;
+}
+
 }  // namespace dvjpeg

@@ -17,6 +17,10 @@ std::string data_url(const std::string& jpeg, const std::string& prefix);
 std::vector<std::string> encode_data_urls(const uint8_t* rgb, int B, int H, int W, int quality,
                                           const std::string& prefix, int threads);
 
+// payload of a data URL (between the first and second comma) -> bytes, with CPython's non-strict
+// base64.b64decode semantics and error messages; false + err on error (call with the GIL released)
+bool data_url_b64decode(const char* uri, size_t n, std::string& out, std::string& err);
+
 // Everything the GPU encoder (jpeg_gpu.hip) needs, laid out as its kernels read it: quantizer
 // reciprocals in the AAN DCT's transposed coefficient layout, the zig-zag source map, and the
 // Annex K Huffman codes (DC: 12 symbols, AC: 256) for luma (0) / chroma (1).

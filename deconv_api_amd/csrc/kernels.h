@@ -179,9 +179,11 @@ int stem_dgrad_fused_launch(const uint16_t* gy, const uint16_t* mask, const uint
                             const StemDgradGeom& g, int dtype, hipStream_t s);
 // GPU baseline JPEG encode of B same-size RGB images (jpeg_gpu.hip): entropy-coded scans (restart
 // marker after every MCU row, no header/EOI) packed back to back into `packed` at off[0..B];
-// `tables` = a device copy of dvjpeg::GpuTables, `ws` = jpeg_gpu_ws_bytes(B, H, W) of workspace
+// `tables` = a device copy of dvjpeg::GpuTables, `ws` = jpeg_gpu_ws_bytes(B, H, W) of workspace,
+// `packed` >= B * jpeg_gpu_out_cap(H, W) bytes; W <= jpeg_gpu_max_width()
 long long jpeg_gpu_ws_bytes(int B, int H, int W);
-void jpeg_gpu_caps(int H, int W, long long* raw_words, long long* out_cap);
+long long jpeg_gpu_out_cap(int H, int W);
+int jpeg_gpu_max_width();
 int jpeg_gpu_launch(const uint8_t* rgb, int B, int H, int W, const void* tables, void* ws, uint8_t* packed,
                     long long* off, hipStream_t s);
 // row softmax (fp32 [M][N])

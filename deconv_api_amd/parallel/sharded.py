@@ -51,6 +51,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..codec.image import gpu_jpeg_fits
 from ..utils.faults import FaultInjector
 from ..utils.logging import get_logger
 from .dist import DistInfo, shard_sizes
@@ -348,7 +349,7 @@ class ShardedRunner:
             return ("host", mos[:n].numpy())
         if st is not None and self.ring is not None:  # reuse the staging ring's slot + stream
             st.n = n
-            if self.cfg is None or self.cfg.gpu_jpeg:  # JPEG on rank 0's GPU: only scans cross PCIe
+            if (self.cfg is None or self.cfg.gpu_jpeg) and gpu_jpeg_fits(mos.shape[2]):  # only scans cross PCIe
                 q = self.cfg.jpeg_quality if self.cfg is not None else 95
                 return ("staged", self.ring.copy_back_jpeg(st, mos, q))
             return ("staged", self.ring.copy_back(st, mos))

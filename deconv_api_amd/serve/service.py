@@ -29,7 +29,7 @@ import torch
 
 from .. import ops
 from ..codec import CodecPool, encode_data_url, encode_data_urls, read_data_url
-from ..codec.image import gpu_data_urls
+from ..codec.image import gpu_data_urls, gpu_jpeg_fits
 from ..runtime.staging import GpuScans
 from ..config import Config
 from ..engine.deconvnet import DeconvNet, UnknownLayerError
@@ -346,7 +346,7 @@ class DeconvService:
             x = torch.empty(n, S, S, 8, dtype=torch.bfloat16, device=self.device)
             st = self.ring.stage(images, x)
             res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
-        if self.cfg.gpu_jpeg:  # JPEG on the device: only the scans cross PCIe
+        if self.cfg.gpu_jpeg and gpu_jpeg_fits(res.mosaic.shape[2]):  # JPEG on the device: only scans cross PCIe
             return ("staged", self.ring.copy_back_jpeg(st, res.mosaic, self.cfg.jpeg_quality))
         return ("staged", self.ring.copy_back(st, res.mosaic))
 

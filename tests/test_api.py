@@ -312,3 +312,35 @@ def test_scale_sweep_efficiency_and_parsing():
     assert rows[0]["efficiency"] == 1.0 and rows[1]["efficiency"] == 0.95 and rows[2]["efficiency"] is None
     assert sw.bench_cmd(2, type("A", (), dict(steps=3, warmup=1, device="cpu", tiny=True, batch=0))())[1:3] == \
         ["-m", "torch.distributed.run"]
+
+
+def test_native_data_url_b64decode_matches_python():
+    """csrc/jpeg_enc.cpp:data_url_b64decode == base64.b64decode(uri.split(',')[1]) (non-strict:
+    junk skipped, a completed pad ends the input) with the same error messages, on fuzzed payloads."""
+    import base64 as b64
+    import binascii
+
+    lib = _native_or_skip()
+    rng = np.random.default_rng(0)
+    alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"
+    pool = alpha * 3 + "==== \n\t!-_.:;"
+    cases = ["YQ==", "YQ==YQ==", "YQ=", "YQ", "Y", "YW Jj!", "YW=Jj", "=YWJj", "YQ=a=", "YWJjZA===",
+             "YWJjZA", "YQ===", "Y===", "YWI=YQ", "YW=JjZA=", "YW=JjZA==", ""]
+    cases += ["".join(rng.choice(list(pool), int(rng.integers(0, 40)))) for _ in range(3000)]
+    cases += [b64.b64encode(rng.bytes(int(n))).decode() for n in rng.integers(0, 5000, 50)]
+    for payload in cases:
+        for uri in ("data:image/png;base64," + payload, "x," + payload + ",tail,more"):
+            try:
+                want, werr = b64.b64decode(uri.split(",")[1]), None
+            except (binascii.Error, ValueError) as e:
+                want, werr = None, str(e)
+            try:
+                got, gerr = lib.data_url_b64decode(uri), None
+            except ValueError as e:
+                got, gerr = None, str(e)
+            assert (got, gerr) == (want, werr), (uri, got, gerr, want, werr)
+    from deconv_api_amd.codec.image import ImageDecodeError, read_data_url
+
+    for bad in ("no comma here", "data:x;base64,YQ=", "data:x;base64,Y"):
+        with pytest.raises(ImageDecodeError):
+            read_data_url(bad)

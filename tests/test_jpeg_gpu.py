@@ -70,3 +70,25 @@ def test_gpu_jpeg_data_urls(native_lib):
         dec = ci.parse_result_data_url(u)
         ref = ci.parse_result_data_url(ci.encode_data_url(im, 95))  # the host encoder's response
         assert dec.shape == (448, 448, 3) and _psnr(dec, ref) > 38.0, (b, _psnr(dec, ref))
+
+
+def test_gpu_jpeg_many_segments_and_width_limit(native_lib):
+    """> 1024 segments in one batch (the offsets kernel's chunked scan) and the width limit."""
+    from PIL import Image
+
+    from deconv_api_amd.codec import image as ci
+
+    B, H, W = 40, 448, 448
+    imgs = _images(B, H, W, 11)
+    packed, off = ci.encode_gpu(torch.from_numpy(imgs).cuda(), 95)
+    off_h = off.cpu()
+    assert int(off_h[0]) == 0 and bool((off_h[1:] > off_h[:-1]).all())
+    packed_h = packed[: int(off_h[-1])].cpu()
+    for b in (0, 1, 38, 39):
+        got = np.asarray(Image.open(io.BytesIO(ci.gpu_jpeg_bytes(packed_h, off_h, b, H, W, 95))).convert("RGB"))
+        ref = np.asarray(Image.open(io.BytesIO(ci.encode_jpeg(imgs[b], 95))).convert("RGB"))
+        assert _psnr(got, ref) > 38.0, (b, _psnr(got, ref))
+    wmax = native_lib.jpeg_gpu_max_width()
+    assert ci.gpu_jpeg_fits(wmax) and not ci.gpu_jpeg_fits(wmax + 1)
+    with pytest.raises(RuntimeError):
+        ci.encode_gpu(torch.zeros(1, 16, wmax + 16, 3, dtype=torch.uint8, device="cuda"))
