@@ -50,29 +50,43 @@ __global__ void __launch_bounds__(256) stem_dgrad_fused_kernel(const uint16_t* _
   const int oh_lo = floor_div(ih0 + g.pad - (KH - 1), S), ow_lo = floor_div(iw0 + g.pad - (KW - 1), S);
 
   // ---- 1. stage the dy window (rows r = wr * CN + wc <-> pixel (oh_lo + wr, ow_lo + wc)) and B ----
-  for (int ci = tid; ci < SD_MROWS * (SD_C / 8); ci += 256) {
-    const int r = ci >> 3, ch = ci & 7;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (r < RN * CN) {
-      const int oh = oh_lo + r / CN, ow = ow_lo + r % CN;
-      if ((unsigned)oh < (unsigned)g.OH && (unsigned)ow < (unsigned)g.OW) {
-        const long long o = (((long long)n * g.OH + oh) * g.OW + ow) * SD_C + ch * 8;
-        v = *reinterpret_cast<const uint4*>(gy + o);
-        if (mask != nullptr) {  // backward through the conv's ReLU: keep dy where y > 0
-          const uint4 m = *reinterpret_cast<const uint4*>(mask + o);
-          v.x = mask_pos_pk(v.x, m.x);
-          v.y = mask_pos_pk(v.y, m.y);
-          v.z = mask_pos_pk(v.z, m.z);
-          v.w = mask_pos_pk(v.w, m.w);
-        }
-      }
+  // Every load of the window, mask and B is issued before the first LDS store (fully unrolled, loads
+  // at clamped addresses, validity as a predicate): with a load -> store pair per loop iteration the
+  // compiler waited for each load before the next was issued, i.e. ~13 serial memory round trips
+  // per workgroup (411 us per call at 32 x 512^2, profiles/kstats_c5_r3_before.txt).
+  constexpr int A_IT = SD_MROWS * (SD_C / 8) / 256, B_IT = (JP * (SD_C / 8) + 255) / 256;
+  uint4 av[A_IT], mv[A_IT], bv[B_IT];
+#pragma unroll
+  for (int it = 0; it < A_IT; ++it) {
+    const int ci = tid + it * 256, r = ci >> 3, ch = ci & 7;
+    const int oh = oh_lo + r / CN, ow = ow_lo + r % CN;
+    const bool ok = r < RN * CN && (unsigned)oh < (unsigned)g.OH && (unsigned)ow < (unsigned)g.OW;
+    const long long o = ok ? (((long long)n * g.OH + oh) * g.OW + ow) * SD_C + ch * 8 : 0;
+    av[it] = *reinterpret_cast<const uint4*>(gy + o);
+    if (mask != nullptr) mv[it] = *reinterpret_cast<const uint4*>(mask + o);
+    if (!ok) av[it] = make_uint4(0u, 0u, 0u, 0u);
+  }
+#pragma unroll
+  for (int it = 0; it < B_IT; ++it) {
+    const int ci = min(tid + it * 256, JP * (SD_C / 8) - 1), r = ci >> 3, ch = ci & 7;
+    bv[it] = *reinterpret_cast<const uint4*>(wb + (long long)r * g.w_ld + ch * 8);
+  }
+#pragma unroll
+  for (int it = 0; it < A_IT; ++it) {
+    const int ci = tid + it * 256, r = ci >> 3, ch = ci & 7;
+    uint4 v = av[it];
+    if (mask != nullptr) {  // backward through the conv's ReLU: keep dy where y > 0
+      v.x = mask_pos_pk(v.x, mv[it].x);
+      v.y = mask_pos_pk(v.y, mv[it].y);
+      v.z = mask_pos_pk(v.z, mv[it].z);
+      v.w = mask_pos_pk(v.w, mv[it].w);
     }
     *reinterpret_cast<uint4*>(As + r * (SD_C * 2) + ((ch ^ (r & 7)) << 4)) = v;
   }
-  for (int ci = tid; ci < JP * (SD_C / 8); ci += 256) {
-    const int r = ci >> 3, ch = ci & 7;
-    *reinterpret_cast<uint4*>(Bs + r * (SD_C * 2) + ((ch ^ (r & 7)) << 4)) =
-        *reinterpret_cast<const uint4*>(wb + (long long)r * g.w_ld + ch * 8);
+#pragma unroll
+  for (int it = 0; it < B_IT; ++it) {
+    const int ci = tid + it * 256, r = ci >> 3, ch = ci & 7;
+    if (ci < JP * (SD_C / 8)) *reinterpret_cast<uint4*>(Bs + r * (SD_C * 2) + ((ch ^ (r & 7)) << 4)) = bv[it];
   }
   __syncthreads();
 
@@ -116,7 +130,14 @@ __global__ void __launch_bounds__(256) stem_dgrad_fused_kernel(const uint16_t* _
   __syncthreads();
 
   // ---- 3. col2im from LDS: each dx pixel gathers its taps (same order as col2im_kernel) ----
-  for (int p = tid; p < SD_TH * SD_TW; p += 256) {
+  // Pixels are dealt by stride-S parity class: wave w owns the pixels with (ih % S, iw % S) = class w
+  // (S * S == 4 waves), so every lane of a wave walks the same tap subset (no divergent tap loop)
+  static_assert(S * S == 4 || S == 1, "parity-class assignment needs S*S == 4 waves");
+  for (int q = lane; q < SD_TH * SD_TW / 4; q += 64) {
+    const int py = S == 1 ? 0 : (wave / S), px = S == 1 ? 0 : (wave % S);
+    const int cw_ = SD_TW / S;  // class columns per tile row
+    const int p = S == 1 ? (wave * (SD_TH * SD_TW / 4) + q)
+                         : ((q / cw_) * S + py) * SD_TW + (q % cw_) * S + px;
     const int ih = ih0 + p / SD_TW, iw = iw0 + p % SD_TW;
     if (ih >= g.H || iw >= g.W) continue;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
