@@ -25,6 +25,7 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dv {
 
@@ -771,16 +772,22 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
 
 // ---------------------------------------------------------------------------------------------
 // KW3: 3x3 / stride 1 / pad 1 forward conv, 256 x 256 tile, where the three kw taps of a kernel row
-// share ONE staged A tile. Output rows are pixels in natural (n, oh, ow) order, so the kw-tap input
-// pixel of output row r is the kw=1 input pixel of output row r + kw - 1: one A tile of 258 rows
-// (output rows m0-1 .. m0+256, each row's kw=1 pixel of input row oh + kh - 1) serves all three
-// taps through a row shift of the fragment reads; the two rows per image row where the shift crosses
-// the image border (ow = 0 for kw = 0, ow = W-1 for kw = 2) are zeroed in registers (the conv's zero
-// padding). A K step is (kernel row kh, 32-channel chunk): A 258 x 64 B + B 3 x 256 x 64 B, i.e.
-// 1.47x fewer staged bytes per FLOP than the plain implicit GEMM (which stages A once per tap), for
-// the 256/512-channel layers whose DMA kernel moves ~9.6 TB/s of staging at 1.1-1.28 PF/s.
-// LDS rows are 64 B with the 16-B chunk XOR-swizzled by bit 2 of the row (q ^ 2((row >> 2) & 1)):
-// conflict-free ds_read_b128 fragment reads for ANY 16-row base (the shifted A reads).
+// share ONE staged A tile. A K step is (kernel row kh, 32-channel chunk): the A tile holds the
+// kernel-row-kh input pixels of the tile's output rows, B the three kw sub-tiles of the weights
+// (A ~17-19 KB + B 3 x 256 x 64 B per step: 1.47x fewer staged bytes per FLOP than the plain
+// implicit GEMM, which stages A once per tap).
+//
+// Zero-padded slot layout: the A tile is staged in *padded* pixel coordinates, W + 2 slots per
+// image row ([0, pixel 0 .. pixel W-1, 0]), so output row r's kw tap is simply slot(r) + kw - 1
+// and the conv's left/right zero padding are real zero slots (the DMA's out-of-range offset
+// writes zeros). A 256-row tile touching b image-row boundaries stages 258 + 2b slots (<= 384 for
+// W >= 5, host check). The round-1..2 layout staged 258 unpadded rows and zeroed the border rows
+// of the A fragments in registers: 64 v_cndmask per wave per K step, each sub-step's MFMAs
+// waiting on ALL its fragment reads first. Now every A fragment address is a per-lane constant
+// (FM x 3 VGPRs, one v_add each per step for the stage offset; LDS: B0 | B1 | A0 | A1).
+// LDS rows are 64 B with the 16-B chunk XOR-swizzled by bit 2 of the slot (q ^ 2((slot >> 2) & 1)):
+// conflict-free ds_read_b128 fragment reads for 16 consecutive slots at any base (a fragment that
+// spans an image-row boundary skips two slots: at most 2-way on one lane group).
 namespace {
 __device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; }
 }  // namespace
@@ -795,13 +802,12 @@ template <int DT, int EPI, int BN_ = 256>
 __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
   constexpr int BN = BN_, BM = 256, NW = 8;
   constexpr int WN = BN == 256 ? 4 : 2, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
-  constexpr int A_I = 3;                   // A DMA instructions (16 rows each) per wave: 384 >= 258 rows
+  constexpr int A_I = 3;                   // A DMA instructions (16 slots each) per wave: 384 slots
   constexpr int B_I = 3 * BN / 16 / NW;    // B: 3 kw sub-tiles x BN rows (6 / 3 per wave)
   constexpr int A_BYTES = A_I * NW * 1024, B_BYTES = 3 * BN * 64;
-  constexpr int STAGE = A_BYTES + B_BYTES;  // 72 / 48 KiB
-  static_assert(BM * BN * 2 <= 2 * STAGE, "C tile must fit in the operand stages");
+  static_assert(BM * BN * 2 <= 2 * (A_BYTES + B_BYTES), "C tile must fit in the operand stages");
   typedef typename Vec8<DT>::type v8;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * (A_BYTES + B_BYTES)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -809,7 +815,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_n = wgid % tiles_n, tile_m = wgid / tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int H = a.H, W = a.W, C = a.C, HW = a.H * a.W;
+  const int H = a.H, W = a.W, C = a.C, HW = a.H * a.W, Wp = a.W + 2;
 
   const int n_base = (m0 < a.M ? m0 : a.M - 1) / HW;
   const long long img_elems = (long long)HW * a.x_ld;
@@ -818,38 +824,38 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
       make_rsrc(a.x + (long long)n_base * img_elems, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
 
-  // DMA lanes: 16 rows x 4 chunks per instruction; row group bases are multiples of 16
+  // padded coordinate of output row m (global image row R = m / W, W + 2 slots per row)
+  auto padded = [&](int m) {
+    const int R = m / W;
+    return R * Wp + 1 + (m - R * W);
+  };
+  const int P0 = padded(m0) - 1;                    // slot 0: the left neighbour of row m0
+  const int nslots = padded(m0 + BM - 1) - P0 + 2;  // through the right neighbour of row m0 + 255
+
+  // DMA lanes: 16 slots x 4 chunks per instruction; slot group bases are multiples of 16
   const int lrow = lane >> 2;
   const int lchunk = (lane & 3) ^ kw3_swz(lrow);
   int r_pix[A_I], r_oh[A_I];
 #pragma unroll
   for (int u = 0; u < A_I; ++u) {
-    const int s = (u * NW + wave) * 16 + lrow;  // staged row <-> output row m0 - 1 + s
-    const int m = m0 - 1 + s;
-    const int n = m >= 0 ? m / HW : -1;
-    const bool valid = s < BM + 2 && m >= 0 && m < a.M && n >= n_base;
-    const int rem = m - n * HW;
-    const int oh = rem / W;
-    r_pix[u] = valid ? (n - n_base) * HW + rem : 0;
+    const int t = (u * NW + wave) * 16 + lrow;
+    const int P = P0 + t;
+    const int R = P / Wp, c = P - R * Wp;
+    const int m = R * W + c - 1;
+    const bool valid = t < nslots && c > 0 && c <= W && m < a.M;  // else a zero slot
+    const int n = R / H, oh = R - n * H;
+    r_pix[u] = valid ? (n - n_base) * HW + oh * W + c - 1 : 0;
     r_oh[u] = valid ? oh : -(1 << 28);
-  }
-  // A-fragment rows whose kw = 0 / kw = 2 neighbour lies in the zero padding
-  uint32_t left = 0, right = 0;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int ow = (m0 + wm * FM * 16 + i * 16 + (lane & 15)) % W;
-    left |= (ow == 0 ? 1u : 0u) << i;
-    right |= (ow == W - 1 ? 1u : 0u) << i;
   }
   const int nch = C / 32;
   const int nsteps = 3 * nch;
   auto issue = [&](int step, int buf) {
     const int kh = step / nch, cc = step - kh * nch;
-    uint8_t* As = smem + buf * STAGE;
-    uint8_t* Bs = As + A_BYTES;
+    uint8_t* As = smem + 2 * B_BYTES + buf * A_BYTES;
+    uint8_t* Bs = smem + buf * B_BYTES;
 #pragma unroll
     for (int u = 0; u < A_I; ++u) {
-      if ((u * NW + wave) * 16 >= BM + 2) continue;  // staged rows past the tile's BM + 2 are never read
+      if ((u * NW + wave) * 16 >= nslots) continue;  // slots past the tile's last are never read
       const bool ok = (unsigned)(r_oh[u] + kh - 1) < (unsigned)H;
       const uint32_t voff =
           ok ? (uint32_t)((((long long)(r_pix[u] + (kh - 1) * W)) * a.x_ld + cc * 32 + lchunk * 8) * 2) : kOOB;
@@ -874,27 +880,39 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
   const int arow0 = wm * FM * 16 + (lane & 15);
   const int brow0 = wn * FN * 16 + (lane & 15);
   const int bswz = ((q ^ kw3_swz(brow0)) << 4);  // brow0 + 16 j: same bit 2
+  // per-lane LDS byte addresses: A fragments (stage 0; stage 1 = + A_BYTES) and the B base of each
+  // stage; opaque so each stays ONE VGPR (the compiler otherwise re-splits them into base + swizzle
+  // pairs: 2 VALU per fragment read and 241 VGPRs)
+  int aaddr[FM][3];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int s1 = padded(m0 + arow0 + i * 16) - P0;  // the kw = 1 slot of this lane's row
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int sl = s1 + kw - 1;
+      aaddr[i][kw] = 2 * B_BYTES + sl * 64 + ((q ^ kw3_swz(sl)) << 4);
+      asm volatile("" : "+v"(aaddr[i][kw]));
+    }
+  }
+  int baddr[2];
+  baddr[0] = brow0 * 64 + bswz;
+  baddr[1] = baddr[0] + B_BYTES;
+  asm volatile("" : "+v"(baddr[0]), "+v"(baddr[1]));
 
   issue(0, 0);
   for (int k = 0; k < nsteps; ++k) {
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
-    const uint8_t* As = smem + (k & 1) * STAGE;
-    const uint8_t* Bs = As + A_BYTES;
+    const int aoff = (k & 1) * A_BYTES;
+    const uint8_t* Bs = smem + baddr[k & 1];
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       v8 bf[FN], af[FM];
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bf[j] = *reinterpret_cast<const v8*>(Bs + kw * (BN * 64) + (brow0 + j * 16) * 64 + bswz);
+      for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const v8*>(Bs + kw * (BN * 64) + j * 1024);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int sr = arow0 + i * 16 + kw;
-        af[i] = *reinterpret_cast<const v8*>(As + sr * 64 + ((q ^ kw3_swz(sr)) << 4));
-        if ((kw == 0 && ((left >> i) & 1)) || (kw == 2 && ((right >> i) & 1)))
-          af[i] = __builtin_bit_cast(v8, make_uint4(0u, 0u, 0u, 0u));
-      }
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(smem + aoff + aaddr[i][kw]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -934,8 +952,9 @@ static int kw3_try(const ConvArgs& a, hipStream_t s) {
   if constexpr (AMODE != CONV_A_FWD || EPI == CONV_E_POOL) {
     return -4;
   } else {
+    // W >= 5: a 256-row tile crosses <= 51 image-row boundaries, 258 + 2 x 51 = 360 <= 384 slots
     if (kw3_mode() == 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH ||
-        a.W != a.OW || a.C % 32 || a.mask || a.ws || a.OCpad % BN || (long long)a.Kpad < 9LL * a.C)
+        a.W != a.OW || a.W < 5 || a.C % 32 || a.mask || a.ws || a.OCpad % BN || (long long)a.Kpad < 9LL * a.C)
       return -4;
     const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / BN;
     const long long nwg = (long long)tiles_m * tiles_n;
