@@ -89,19 +89,13 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
 // MASK: backward through a ReLU: A elements are kept only where mask (same layout and pixel
 // stride as x) is > 0. The mask tile is DMA'd into LDS next to the A tile with the same offsets
 // and applied to each A fragment in registers right before its MFMAs.
-// KS2: in-workgroup K split. Two groups of WM x WN waves share the C tile; group g computes the
-// 32-deep sub-step g of every BK=64 tile, and group 1's partial sums are added into group 0's
-// through LDS before the epilogue. Each wave then owns a (16*FM) x (16*FN) = 128 x 64 tile where
-// a plain 8-wave layout would own 64 x 64: 12 instead of 16 fragment reads per 32 MFMAs, for the
-// 128- and 64-output-channel layers whose 256 x 128 / 512 x 64 tiles are LDS-read bound.
 // The workgroup body: output tile ``wgid`` (row-major over tiles_n column tiles) of problem ``a``,
 // K slice ky of nky. Shared by the one-problem kernel below and the grouped kernel
 // (conv_dma_group_kernel), whose workgroups each look their problem up in a table.
 template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED,
-          bool MASK = false, bool FRAGPIPE = false, bool KS2 = false>
+          bool MASK = false, bool FRAGPIPE = false>
 __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, int wgid, int ky, int nky) {
-  constexpr int NW = WM * WN * (KS2 ? 2 : 1);
-  static_assert(!KS2 || (BK == 64 && !MASK), "KS2: BK=64 (one 32-deep sub-step per group), no mask");
+  constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16;
   constexpr int BN = WN * FN * 16;
   constexpr int ROWB = BK * 2;              // LDS bytes per row
@@ -121,9 +115,7 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kg = KS2 ? wave / (WM * WN) : 0;  // K group (KS2)
-  const int wl = KS2 ? wave - kg * (WM * WN) : wave;
-  const int wm = wl / WN, wn = wl % WN;
+  const int wm = wave / WN, wn = wave % WN;
   const int tile_n = wgid % tiles_n;
   const int tile_m = wgid / tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
@@ -318,22 +310,6 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
     if (kt + STAGES - 1 < nk) issue(k0 + kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const uint8_t* As = smem + cur * STAGE;
     const uint8_t* Bs = As + A_BYTES + M_BYTES;
-    if constexpr (KS2) {
-      typedef typename Vec8<DT>::type v8;
-      const int swk = ((kg * 4 + (lane >> 4)) ^ rx) << 4;
-      v8 af[FM], bf[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const v8*>(Bs + (b_row0 + j * 16) * ROWB + swk);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(As + (a_row0 + i * 16) * ROWB + swk);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bf[j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      continue;
-    }
     if constexpr (FRAGPIPE && !MASK) {
       // all fragments of a 32-K sub-step are read up front, and the next sub-step's reads are
       // issued before this sub-step's MFMAs (register double buffer), so LDS latency hides
@@ -384,29 +360,8 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
     }
   }
 
-  if constexpr (KS2) {  // group 1's partial sums -> group 0 (lane-linear 16-B slots, conflict-free)
-    static_assert(WM * WN * FM * FN * 64 * 16 <= STAGES * STAGE, "KS2 reduction must fit in the stages");
-    f32x4* red = reinterpret_cast<f32x4*>(smem) + (wl * FM * FN) * 64 + lane;
-    __syncthreads();  // every wave is done reading the operand stages
-    if (kg == 1) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) red[(i * FN + j) * 64] = acc[i][j];
-    }
-    __syncthreads();
-    if (kg == 0) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] += red[(i * FN + j) * 64];
-    }
-    __syncthreads();  // the epilogue may reuse the stages
-  }
-
   // ---- epilogue ----
   if (a.ws != nullptr) {  // split-K partial: raw fp32 sums to ws[split][row][OCpad]
-    if (kg != 0) return;
     float* ws = a.ws + (long long)ky * a.M * a.OCpad;
     const int row_l = (lane >> 4) * 4, col_l = lane & 15;
 #pragma unroll
@@ -425,12 +380,11 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
   if constexpr (EPI == CONV_E_BF16) {
     if (a.vec_epi) {
       static_assert(BM * BN * 2 <= STAGES * STAGE, "C tile must fit in the operand stages");
-      if constexpr (!KS2) __syncthreads();  // every wave is done reading the operand stages
-      epilogue_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid, kg == 0);
+      __syncthreads();  // every wave is done reading the operand stages
+      epilogue_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
       return;
     }
   }
-  if (kg != 0) return;
   if constexpr (EPI == CONV_E_BF16) {
     if (a.res || a.emask) {
       epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
@@ -444,9 +398,9 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
 }
 
 template <int DT, int WM, int WN, int FM, int FN, int BK, int STAGES, int AMODE, int EPI, bool CALIGNED,
-          bool MASK = false, bool FRAGPIPE = false, bool KS2 = false>
-__global__ void __launch_bounds__(WM * WN * (KS2 ? 128 : 64)) conv_dma_kernel(const ConvArgs a, int tiles_n) {
-  conv_dma_body<DT, WM, WN, FM, FN, BK, STAGES, AMODE, EPI, CALIGNED, MASK, FRAGPIPE, KS2>(
+          bool MASK = false, bool FRAGPIPE = false>
+__global__ void __launch_bounds__(WM * WN * 64) conv_dma_kernel(const ConvArgs a, int tiles_n) {
+  conv_dma_body<DT, WM, WN, FM, FN, BK, STAGES, AMODE, EPI, CALIGNED, MASK, FRAGPIPE>(
       a, tiles_n, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y, gridDim.y);
 }
 
@@ -790,19 +744,23 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
 // spans an image-row boundary skips two slots: at most 2-way on one lane group).
 namespace {
 __device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; }
+// staged A slots per workgroup: 8 waves x 16 x A_I >= BM + 2 + 2 x (row boundaries), host-checked
+constexpr int kw3_a_i(int bm) { return bm == 256 ? 3 : 5; }
 }  // namespace
 
-// BN_: 256 (8 waves of 128 x 64) or 128 (8 waves of 64 x 64) output channels per workgroup.
+// BM_ x BN_: 256 x 256 (8 waves of 128 x 64) or 512 x 128 (8 waves of 128 x 64: the same per-wave
+// MFMA:LDS-read ratio and FLOPs per K step as 256 x 256, for 128-channel outputs; the round-1..2
+// 256 x 128 tile ran 8 waves of 64 x 64 at MFMA util 0.35, profiles/pmc_c2_r3.txt).
 // (Measured and removed, round 3: issuing the next step's DMAs in three parts between the kw
 // sub-steps' fragment reads and MFMAs instead of all right after the barrier: config 2 fell from
 // 6.85-7.03k to 5.80-5.83k img/s, profiles/bench_c2_r3_ab.txt. Equal within noise and removed:
 // static priority for waves 4-7 instead of the per-sub-step flips, a 320-row M tile, and the DMAs
 // issued behind the first sub-step's fragment reads, profiles/kw3_variants_r3.txt.)
-template <int DT, int EPI, int BN_ = 256>
+template <int DT, int EPI, int BN_ = 256, int BM_ = 256>
 __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
-  constexpr int BN = BN_, BM = 256, NW = 8;
-  constexpr int WN = BN == 256 ? 4 : 2, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
-  constexpr int A_I = 3;                   // A DMA instructions (16 slots each) per wave: 384 slots
+  constexpr int BN = BN_, BM = BM_, NW = 8;
+  constexpr int WN = BN / 64, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
+  constexpr int A_I = kw3_a_i(BM);         // A DMA instructions (16 slots each) per wave
   constexpr int B_I = 3 * BN / 16 / NW;    // B: 3 kw sub-tiles x BN rows (6 / 3 per wave)
   constexpr int A_BYTES = A_I * NW * 1024, B_BYTES = 3 * BN * 64;
   static_assert(BM * BN * 2 <= 2 * (A_BYTES + B_BYTES), "C tile must fit in the operand stages");
@@ -947,30 +905,31 @@ static int kw3_mode() {
   return e ? std::atoi(e) : 1;
 }
 
-template <int DT, int AMODE, int EPI, int BN = 256>
+template <int DT, int AMODE, int EPI, int BN = 256, int BM = 256>
 static int kw3_try(const ConvArgs& a, hipStream_t s) {
   if constexpr (AMODE != CONV_A_FWD || EPI == CONV_E_POOL) {
     return -4;
   } else {
-    // W >= 5: a 256-row tile crosses <= 51 image-row boundaries, 258 + 2 x 51 = 360 <= 384 slots
     if (kw3_mode() == 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH ||
-        a.W != a.OW || a.W < 5 || a.C % 32 || a.mask || a.ws || a.OCpad % BN || (long long)a.Kpad < 9LL * a.C)
+        a.W != a.OW || a.W < 1 || a.C % 32 || a.mask || a.ws || a.OCpad % BN || (long long)a.Kpad < 9LL * a.C)
       return -4;
-    const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / BN;
+    // zero-padded slots of a BM-row tile: BM + 2 + 2 x (image-row boundaries, <= (BM - 1) / W + 1)
+    if (BM + 2 + 2 * ((BM - 1) / a.W + 1) > kw3_a_i(BM) * 8 * 16) return -4;  // W >= 5 (256), >= 9 (512)
+    const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.OCpad / BN;
     const long long nwg = (long long)tiles_m * tiles_n;
     if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
     // (a B-fragment double buffer across the kw sub-steps measured equal and was removed,
     // profiles/layers_r1_kw3_{nofp,on}.txt)
-    hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
+    hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN, BM>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
     return (int)hipGetLastError();
   }
 }
 
 template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int EPI, bool MASK = false,
-          bool FP = false, bool KS2 = false>
+          bool FP = false>
 static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
-  constexpr int NT = WM * WN * (KS2 ? 128 : 64);
+  constexpr int NT = WM * WN * 64;
   const int tiles_m = (a.M + BM - 1) / BM;
   const int tiles_n = a.OCpad / BN;
   const long long nwg = (long long)tiles_m * tiles_n;
@@ -978,40 +937,19 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   const bool aligned = (a.C % BK) == 0;
   const dim3 grid((unsigned)nwg, (unsigned)(a.ws ? a.ksplit : 1));
   if (aligned)
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK, FP, KS2>), grid,
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, true, MASK, FP>), grid,
                        dim3(NT), 0, s, a, tiles_n);
   else
-    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP, KS2>), grid,
+    hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP>), grid,
                        dim3(NT), 0, s, a, tiles_n);
   return (int)hipGetLastError();
 }
 
-// DV_DMA_VARIANT: 0 (default) 2-stage BK64 except 256x128 (3-stage); 1: all 2-stage BK64;
-// 2: BK32 x 4-stage rings for 256x256 and 512x64; 3: 128x256 3-stage for OC%256;
-// 4: register double-buffered fragments + s_setprio around MFMA runs (default for 256x256; v1
-// there selects the plain fragment loop) (A/B testing). Measured and removed: 4-wave 256x128 /
-// 128x256 workgroups (BK=32 x 3 stages, 72 KiB -> 2 per CU) on the 256/512-channel layers ran at
-// 0.53-0.72 PF/s vs 0.99-1.28 (profiles/layers_r1_dmav{0,5,6}.txt): 1.5x the staged bytes per FLOP.
-static int dma_variant() {
-  static int v = [] {
-    const char* e = std::getenv("DV_DMA_VARIANT");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
-// DV_KS2=1 enables the in-workgroup K split (KS2) on the 256 x 128 and 512 x 64 tiles (A/B only).
-// Measured slower on every VGG16 layer it applies to (profiles/layers_r1_ks2_{off,on}.txt, e.g.
-// block2_conv2.down 0.72 -> 0.68 PF/s): these tiles are bound by the A-operand DMA stream (~9 TB/s
-// L2 -> LDS for both tile shapes), not by LDS fragment reads, so it stays off.
-static bool ks2_on() {
-  static bool v = [] {
-    const char* e = std::getenv("DV_KS2");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
+// Measured and removed (rounds 1-3, profiles/layers_r1_dmav{0,5,6}.txt, layers_r1_ks2_{off,on}.txt,
+// layers_r1_pipeline.txt): BK32 x 4-stage rings on 256x256 / 512x64, all-2-stage rings, 4-wave
+// 256x128 / 128x256 workgroups (0.53-0.72 vs 0.99-1.28 PF/s: 1.5x the staged bytes per FLOP), and
+// the in-workgroup K split (two wave groups per C tile, partial sums through LDS: the 256x128 /
+// 512x64 tiles are bound by the A-operand DMA stream, not by LDS fragment reads).
 static int num_cus() {
   static int n = [] {
     int dev = 0, cu = 256;
@@ -1081,9 +1019,7 @@ template <int DT, int AMODE, int EPI>
 static int dma_bn(const ConvArgs& a, hipStream_t s) {
   if (g_cfg > 0) return dma_forced<DT, AMODE, EPI>(a, s, g_cfg);
   if (const int c = auto_cfg(a)) return dma_forced<DT, AMODE, EPI>(a, s, c);
-  // measured (profiles/layers_r1_pipeline.txt): BK=32 x 4-stage rings lose to 2-stage BK=64 on the
-  // 256x256 and 512x64 tiles; the 3-stage BK=64 ring wins slightly on 256x128.
-  const int v = DT == DT_BF16 ? dma_variant() : 0;  // A/B variants are bf16-only
+  // (the 3-stage BK=64 ring wins slightly on 256x128; 2 stages elsewhere)
   const long long cus = num_cus();
   auto nwg = [&](int BM, int BN) { return (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN); };
   if (a.OCpad % 256 == 0 && a.OC > 128) {
@@ -1091,11 +1027,7 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
       const int rc = kw3_try<DT, AMODE, EPI>(a, s);
       if (rc != -4) return rc;
     }
-    if constexpr (DT == DT_BF16) {
-      if (v == 2) return dma_cfg<DT, 2, 4, 8, 4, 32, 4, AMODE, EPI>(a, s);
-      if (v == 1 && nwg(256, 256) >= cus) return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI>(a, s);
-    }
-    if (v == 3 || (nwg(256, 256) < cus && nwg(128, 256) >= cus))
+    if (nwg(256, 256) < cus && nwg(128, 256) >= cus)
       return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
     if (nwg(256, 256) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
     {  // 3x3 s1 p1 forward: the three kw taps share one staged A tile
@@ -1106,25 +1038,15 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
     return dma_cfg<DT, 2, 4, 8, 4, 64, 2, AMODE, EPI, false, true>(a, s);
   }
   if (a.OCpad % 128 == 0 && a.OC > 64) {
-    if constexpr (DT == DT_BF16) {
-      if (v == 1) return dma_cfg<DT, 4, 2, 4, 4, 64, 2, AMODE, EPI>(a, s);
-      if (v == 4 && nwg(256, 128) >= cus) return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI, false, true>(a, s);
-    }
-    if (kw3_mode() == 2 || nwg(256, 128) >= cus) {  // 3x3 s1 p1 forward: shared-kw-tap 256 x 128 tile
-      const int rc = kw3_try<DT, AMODE, EPI, 128>(a, s);
+    if (kw3_mode() == 2 || nwg(512, 128) >= cus) {  // 3x3 s1 p1 forward: shared-kw-tap 512 x 128 tile
+      const int rc = kw3_try<DT, AMODE, EPI, 128, 512>(a, s);
       if (rc != -4) return rc;
     }
     if (nwg(256, 128) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
-    if (ks2_on()) return dma_cfg<DT, 2, 2, 8, 4, 64, 3, AMODE, EPI, false, false, true>(a, s);  // 256 x 128, KS2
     return dma_cfg<DT, 4, 2, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 256 x 128
   }
   if (a.OCpad % 64 == 0 && a.OC > 16) {
-    if constexpr (DT == DT_BF16) {
-      if (v == 2) return dma_cfg<DT, 8, 1, 4, 4, 32, 4, AMODE, EPI>(a, s);
-      if (v == 4 && nwg(512, 64) >= cus) return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI, false, true>(a, s);
-    }
     if (nwg(512, 64) < cus) return dma_cfg<DT, 8, 1, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 256 x 64
-    if (ks2_on()) return dma_cfg<DT, 4, 1, 8, 4, 64, 2, AMODE, EPI, false, false, true>(a, s);  // 512 x 64, KS2
     return dma_cfg<DT, 8, 1, 4, 4, 64, 2, AMODE, EPI>(a, s);  // 512 x 64
   }
   if (a.OCpad % 16 == 0) {
@@ -1145,7 +1067,7 @@ static int dma_mask_bn(const ConvArgs& a, hipStream_t s) {
   return -3;
 }
 
-// Tile dims the default (DV_DMA_VARIANT=0) selection above picks, for split-K planning.
+// Tile dims the default selection above picks, for split-K planning.
 static void dma_tile_dims(const ConvArgs& a, bool mask, int& BM, int& BN) {
   const long long cus = num_cus();
   auto nwg = [&](int bm, int bn) { return (long long)((a.M + bm - 1) / bm) * (a.OCpad / bn); };

@@ -26,7 +26,11 @@ namespace {
 constexpr int TH = 8, TW = 32;             // output tile: 8 waves x (1 row x 32 px)
 constexpr int IH = TH + 2, IW = TW + 2;    // halo tile
 constexpr int C64 = 64;                    // input channels
-constexpr int PIXB = C64 * 2 + 16;         // 144 B per halo pixel: 9 bank slots (coprime with 16)
+// 160 B per halo pixel (10 bank slots): conflict-free ds_read_b128 fragment reads of 16 consecutive
+// pixels at any base, chunk q or q + 4 (tools/lds_bank_check.py). The round-1..2 144-B pitch (9
+// slots) was 2-way on every lane group: SQ_LDS_BANK_CONFLICT / IDX_ACTIVE 0.40 on the v2 unpool
+// kernel (profiles/pmc_c2_r3.txt).
+constexpr int PIXB = C64 * 2 + 32;
 constexpr int KW9 = 9 * C64;               // K = 576
 constexpr int WROWB = KW9 * 2;             // 1152 B per weight row (72 chunks)
 constexpr int HALO_CH = IH * IW * 8;       // 16-B chunks per halo (4896)
@@ -222,7 +226,7 @@ namespace {
 constexpr int V2_PH = TH / 2 + 2, V2_PW = TW / 2 + 2;   // pooled halo (6 x 18)
 constexpr int V2_TASKS = V2_PH * V2_PW * 8;              // 16-B pooled chunks per tile (864)
 constexpr int V2_PER_T = (V2_TASKS + 511) / 512;         // 2
-constexpr int V2_A = IH * IW * PIXB;                     // 48960
+constexpr int V2_A = IH * IW * PIXB;                     // 54400
 constexpr int V2_C = TH * TW * 128;                      // 32768: bf16 output tile staging
 }  // namespace
 
@@ -959,23 +963,41 @@ __global__ void __launch_bounds__(256) conv3x3_c8_stream_kernel(const ConvArgs a
                                                                  0, 0, 0);
         }
       }
-      // C[channel][px]: lane (px = fi*16 + col, kq) holds channels j*16 + kq*4 + r, r = 0..3
+      // C[channel][px]: lane (px = fi*16 + col, kq) holds channels j*16 + kq*4 + r, r = 0..3. A
+      // v_permlane16_swap per dword of each block pair (j, j+1) gathers 8 consecutive channels per
+      // lane (row kq: block j + (kq & 1), channels (kq >> 1) * 8 + 0..7): one 16-B store per pair
+      // instead of two 8-B ones (the layer is store-issue bound: dwordx2 stores issue at half the
+      // bytes per instruction, MI355X_MICROARCH T21). All lanes swap; only the stores are guarded.
 #pragma unroll
       for (int fi = 0; fi < 2; ++fi) {
         const int ox = x0 + fi * 16 + col;
-        if (!FULL && ox >= W) continue;
-        uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + (((long long)n * H + y) * W + ox) * a.out_ld;
+        uint32_t pk[4][2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int oc = j * 16 + kq * 4;
-          if (!FULL && oc >= a.OC) continue;
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             v[r] = acc[fi][j][r] + bias[j][r];
             if (a.relu) v[r] = fmaxf(v[r], 0.f);
           }
-          *reinterpret_cast<uint2*>(orow + oc) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+          pk[j][0] = pack_bf2(v[0], v[1]);
+          pk[j][1] = pack_bf2(v[2], v[3]);
+        }
+#pragma unroll
+        for (int jp = 0; jp < 4; jp += 2)
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {  // odd rows of pk[jp] <-> even rows of pk[jp + 1]
+            const auto sw = __builtin_amdgcn_permlane16_swap(pk[jp][d], pk[jp + 1][d], false, false);
+            pk[jp][d] = sw[0];
+            pk[jp + 1][d] = sw[1];
+          }
+        if (!FULL && ox >= W) continue;
+        uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + (((long long)n * H + y) * W + ox) * a.out_ld;
+#pragma unroll
+        for (int jp = 0; jp < 4; jp += 2) {
+          const int oc = (jp + (kq & 1)) * 16 + (kq >> 1) * 8;
+          if (!FULL && oc >= a.OC) continue;
+          *reinterpret_cast<uint4*>(orow + oc) = make_uint4(pk[jp][0], pk[jp][1], pk[jp + 1][0], pk[jp + 1][1]);
         }
       }
     }
@@ -985,9 +1007,9 @@ __global__ void __launch_bounds__(256) conv3x3_c8_stream_kernel(const ConvArgs a
 
 int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s) {
   if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.C != 8 || a.x_ld != 8 || a.relu_in ||
-      a.OC > 64 || a.OCpad != 64 || a.OC % 4 != 0 || a.H != a.OH || a.W != a.OW || a.accumulate || a.mask ||
-      a.Kpad < 96 || a.out_ld % 4 != 0 || a.dtype != DT_BF16 || a.res || a.emask ||
-      (reinterpret_cast<uintptr_t>(a.out) & 7))
+      a.OC > 64 || a.OCpad != 64 || a.OC % 8 != 0 || a.H != a.OH || a.W != a.OW || a.accumulate || a.mask ||
+      a.Kpad < 96 || a.out_ld % 8 != 0 || a.dtype != DT_BF16 || a.res || a.emask ||
+      (reinterpret_cast<uintptr_t>(a.out) & 15))
     return -4;
   const long long nwg = (long long)a.N * ((a.W + S8_W - 1) / S8_W);
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;

@@ -2,6 +2,8 @@
 
 bf16 inputs/weights are rounded identically on both sides, so the only differences are fp32
 accumulation order and the final bf16 rounding of the GPU output."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -152,9 +154,8 @@ def test_conv_first_layer_stream(native_lib, N, H, W, OC):
 
 @pytest.mark.parametrize("N,H,W,C,OC", [(6, 112, 112, 128, 128), (11, 112, 112, 128, 64), (5, 115, 121, 64, 128),
                                         (21, 56, 56, 256, 256)])
-def test_conv_large_m_ks2_tiles(native_lib, conv_impl, N, H, W, C, OC):
-    """Large-M launches (>= one 256x128 / 512x64 tile per CU; with DV_KS2=1 in the environment the
-    in-workgroup K-split variants, with DV_DMA_VARIANT=5/6 the 4-wave 256-channel tiles): bf16 vector
+def test_conv_large_m_tiles(native_lib, conv_impl, N, H, W, C, OC):
+    """Large-M launches (>= one 256x128 / 512x64 tile per CU): bf16 vector
     epilogue, f32 epilogue, fused pool+switch and the transposed dgrad."""
     g = torch.Generator().manual_seed(21)
     x = torch.randn(N, H, W, C, generator=g)
@@ -873,3 +874,25 @@ def test_deconv_tail_fused(native_lib, N, H, W, div):
     a, b = got.flatten().double().cpu(), two.flatten().double().cpu()
     assert float(a @ b / (a.norm() * b.norm())) > 0.9999
     assert _rel(got, two) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,W", [(3, 64, 64), (2, 60, 70)])
+def test_conv_c8_stream_first_layer(native_lib, N, H, W):
+    """VGG16 block1_conv1 shape (8-channel padded RGB -> 64, 3x3 s1 p1, ReLU) on the row-streaming
+    kernel (conv3x3_c8_stream_kernel: full 4-row / 32-px strips and the ragged-edge path), whose
+    epilogue gathers 8 consecutive channels per lane with v_permlane16_swap for 16-B stores; vs
+    the fp32 reference, and vs the generic path (DV_NO_C8_STREAM)."""
+    g = torch.Generator().manual_seed(61)
+    x = torch.rand(N, H, W, 8, generator=g) * 2 - 1
+    x[..., 3:] = 0
+    cw = _cw(64, 8)
+    ref = ops.conv2d(_bf(x), cw, relu=True)
+    xd, cwd = _bf(x).to(torch.bfloat16).to(DEV), cw.to_device(DEV)
+    got = ops.conv2d(xd, cwd, relu=True)
+    assert got.shape == (N, H, W, 64) and _rel(got, ref) < 1e-2
+    os.environ["DV_NO_C8_STREAM"] = "1"
+    try:
+        alt = ops.conv2d(xd, cwd, relu=True)
+    finally:
+        del os.environ["DV_NO_C8_STREAM"]
+    assert _rel(got, alt) < 1e-2
