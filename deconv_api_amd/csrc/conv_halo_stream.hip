@@ -345,13 +345,18 @@ __device__ __forceinline__ int h16_swz(int p) { return ((p >> 2) & 1) << 1; }
 constexpr int HU_PI = 2, HU_CI = 1;           // pooled-value / code DMA instructions per wave and chunk
 constexpr int HU_PBUF = HU_PI * 4 * 1024, HU_CBUF = HU_CI * 4 * 1024;
 
-template <int DT, int OCT, bool POOL, bool UNPOOL>
+// TPS (taps per K step): 1, or 3 for 64-channel outputs (!UNPOOL): a step is one kernel row (three
+// taps, 48 MFMAs per wave between barriers instead of 16), the weight slot holds the row's three
+// taps, and a 2-slot ring with the next step's weights issued right after the barrier (prefetch
+// distance one 48-MFMA step) keeps 72 KiB of LDS -> 2 workgroups per CU.
+template <int DT, int OCT, bool POOL, bool UNPOOL, int TPS = 1>
 __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+  static_assert(TPS == 1 || (TPS == 3 && OCT == 64 && !UNPOOL), "3-tap steps: 64 output channels, no unpool");
   constexpr int FN = OCT / 16;                // output-channel blocks
-  constexpr int BI = OCT / 64;                // weight DMA instructions per wave and step (OCT*64 B / 4 KiB)
-  constexpr int BSLOT = OCT * 64;
-  constexpr int RING = 3;
-  constexpr int STEPS_PER_CHUNK = 9;
+  constexpr int BI = OCT / 64 * TPS;          // weight DMA instructions per wave and step (TPS*OCT*64 B / 4 KiB)
+  constexpr int BSLOT = OCT * 64 * TPS;
+  constexpr int RING = TPS == 1 ? 3 : 2;
+  constexpr int STEPS_PER_CHUNK = 9 / TPS;
   constexpr int HI = UNPOOL ? HU_PI + HU_CI : H16_HI;  // input DMA instructions per wave and chunk
   typedef typename Vec8<DT>::type v8;
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * H16_HBUF + RING * BSLOT + (UNPOOL ? HU_PBUF + HU_CBUF : 0)];
@@ -408,12 +413,13 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
       hoff[u] = ok ? (uint32_t)((((long long)y * W + x) * a.x_ld + ch * 8) * 2) : HS_OOB;
     }
   }
+  // weight DMA u of a step: tap (kw) u / (OCT / 64) of the step's row, rows ((u % (OCT/64)) * 4 + wave) * 16 ..
   uint32_t woff[BI];
 #pragma unroll
   for (int u = 0; u < BI; ++u) {
-    const int s = (u * 4 + wave) * 64 + lane;
+    const int s = ((u % (OCT / 64)) * 4 + wave) * 64 + lane;
     const int r = s >> 2, ch = (s & 3) ^ h16_swz(s >> 2);
-    woff[u] = (uint32_t)(((long long)r * a.Kpad + ch * 8) * 2);
+    woff[u] = (uint32_t)(((long long)r * a.Kpad + (u / (OCT / 64)) * C + ch * 8) * 2);
   }
   const int nch = C / 32;
   const int nsteps = nch * STEPS_PER_CHUNK;
@@ -460,9 +466,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
       *reinterpret_cast<uint4*>(hd + p * 64 + ((ch ^ h16_swz(p)) << 4)) = v;
     }
   };
-  auto issue_w = [&](int k) {
+  auto issue_w = [&](int k) {  // step k = (chunk c, tap t) or, TPS = 3, (chunk c, kernel row t)
     const int c = k / STEPS_PER_CHUNK, t = k - STEPS_PER_CHUNK * (k / STEPS_PER_CHUNK);
-    const uint32_t add = k < nsteps ? (uint32_t)((t * C + c * 32) * 2) : HS_OOB;
+    const uint32_t add = k < nsteps ? (uint32_t)((t * TPS * C + c * 32) * 2) : HS_OOB;
     uint8_t* dst = ring + (k % RING) * BSLOT;
 #pragma unroll
     for (int u = 0; u < BI; ++u)
@@ -487,6 +493,42 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
     expand(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before readers by step 0's barrier
   }
+  if constexpr (TPS == 3) {
+    // step k = (chunk c, kernel row kh): weights W(k) -> slot k % 2, issued at step k - 1 right after
+    // its barrier, BEFORE that step's halo(c + 1) DMAs (kh == 0), so the wait for W(k) leaves the
+    // younger halo in flight at kh == 1 and drains it at kh == 2 (two steps to land)
+    issue_w(0);
+    for (int c = 0; c < nch; ++c) {
+      const uint8_t* hb = halo + (c & 1) * H16_HBUF;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int k = c * 3 + kh;
+        if (kh == 1) hs_wait<HI>();
+        else hs_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        issue_w(k + 1);
+        if (kh == 0) issue_halo(c + 1, (c + 1) & 1);
+        const uint8_t* wb = ring + (k % RING) * BSLOT + wrd;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          v8 wf[FN], pf[4];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) wf[j] = *reinterpret_cast<const v8*>(wb + kw * OCT * 64 + j * 16 * 64);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int p = (4 * wave + i + kh) * H16_HW + px + kw;
+            pf[i] = *reinterpret_cast<const v8*>(hb + p * 64 + ((q ^ h16_swz(p)) << 4));
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(wf[j], pf[i], acc[i][j]);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      }
+    }
+  } else {
   issue_w(0);
   issue_w(1);
   for (int c = 0; c < nch; ++c) {
@@ -527,6 +569,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
       }
     }
   }
+  }  // TPS == 1
   hs_wait<0>();
 
   // epilogue: lane = pixel (tile row 4 wave + i, column px); register r of block j = channel 16j + 4q + r
@@ -670,7 +713,8 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
     const long long n16 = (long long)a.N * t16x * t16y;
     if (n16 <= 0 || n16 > 0x7fffffffLL) return -2;
     const dim3 g16((unsigned)n16), b16(256);
-#define HS16(DT_, OCT_, POOL_) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_, OCT_, POOL_, false>), g16, b16, 0, s, a, t16x, t16y)
+#define HS16(DT_, OCT_, POOL_)                                                                               \
+  hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_, OCT_, POOL_, false, OCT_ == 64 ? 3 : 1>), g16, b16, 0, s, a, t16x, t16y)
     if (pool) {
       if (a.OCpad == 128) HS16(DT_BF16, 128, true);
       else HS16(DT_BF16, 64, true);
