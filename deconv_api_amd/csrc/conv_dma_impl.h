@@ -118,7 +118,7 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
   const int wm = wave / WN, wn = wave % WN;
   const int tile_n = wgid % tiles_n;
   const int tile_m = wgid / tiles_n;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int m0 = a.m_base + tile_m * BM, n0 = tile_n * BN;
   const int H = a.H, W = a.W, C = a.C;
 
   // ---- tile base image: every A source offset is relative to it (32-bit voffsets) ----
@@ -772,7 +772,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
   const int wm = wave / WN, wn = wave % WN;
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_n = wgid % tiles_n, tile_m = wgid / tiles_n;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int m0 = a.m_base + tile_m * BM, n0 = tile_n * BN;
   const int H = a.H, W = a.W, C = a.C, HW = a.H * a.W, Wp = a.W + 2;
 
   const int n_base = (m0 < a.M ? m0 : a.M - 1) / HW;
@@ -905,8 +905,9 @@ static int kw3_mode() {
   return e ? std::atoi(e) : 1;
 }
 
+// tiles_m_limit > 0: launch only the first tiles_m_limit row tiles (kw3_split's full rounds)
 template <int DT, int AMODE, int EPI, int BN = 256, int BM = 256>
-static int kw3_try(const ConvArgs& a, hipStream_t s) {
+static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
   if constexpr (AMODE != CONV_A_FWD || EPI == CONV_E_POOL) {
     return -4;
   } else {
@@ -915,7 +916,10 @@ static int kw3_try(const ConvArgs& a, hipStream_t s) {
       return -4;
     // zero-padded slots of a BM-row tile: BM + 2 + 2 x (image-row boundaries, <= (BM - 1) / W + 1)
     if (BM + 2 + 2 * ((BM - 1) / a.W + 1) > kw3_a_i(BM) * 8 * 16) return -4;  // W >= 5 (256), >= 9 (512)
-    const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.OCpad / BN;
+    if (a.m_base != 0) return -4;
+    int tiles_m = (a.M + BM - 1) / BM;
+    if (tiles_m_limit > 0 && tiles_m_limit < tiles_m) tiles_m = tiles_m_limit;
+    const int tiles_n = a.OCpad / BN;
     const long long nwg = (long long)tiles_m * tiles_n;
     if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
     // (a B-fragment double buffer across the kw sub-steps measured equal and was removed,
@@ -930,7 +934,7 @@ template <int DT, int WM, int WN, int FM, int FN, int BK, int ST, int AMODE, int
 static int dma_cfg(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   constexpr int NT = WM * WN * 64;
-  const int tiles_m = (a.M + BM - 1) / BM;
+  const int tiles_m = (a.M - a.m_base + BM - 1) / BM;
   const int tiles_n = a.OCpad / BN;
   const long long nwg = (long long)tiles_m * tiles_n;
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
@@ -943,6 +947,25 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((conv_dma_kernel<DT, WM, WN, FM, FN, BK, ST, AMODE, EPI, false, MASK, FP>), grid,
                        dim3(NT), 0, s, a, tiles_n);
   return (int)hipGetLastError();
+}
+
+// KW3 256 x 256 runs one workgroup per CU (144 KiB of LDS), so a grid of R.f rounds pays a whole
+// round for its fraction f (block5 at B*K = 1024: 1568 tiles = 6.125 rounds; at B = 256: 392 =
+// 1.53). Split: the full rounds as KW3, the last partial round's rows as a tail launch of 128 x 128
+// DMA tiles (4x the workgroups, 2 per CU) starting at row m_base. Same stream, in order.
+template <int DT, int AMODE, int EPI>
+static int kw3_split(const ConvArgs& a, hipStream_t s, long long cus) {
+  const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / 256;
+  const long long nwg = (long long)tiles_m * tiles_n;
+  const long long full = nwg / cus, rem = nwg % cus;
+  const long long main_m = full * cus / tiles_n;  // row tiles of the full rounds
+  if (full < 1 || rem == 0 || (full * cus) % tiles_n != 0 || main_m >= tiles_m)
+    return kw3_try<DT, AMODE, EPI>(a, s);
+  const int rc = kw3_try<DT, AMODE, EPI>(a, s, (int)main_m);
+  if (rc != 0) return rc;  // -4 (unsupported) before anything launched, or a launch error
+  ConvArgs t = a;
+  t.m_base = (int)(main_m * 256);
+  return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(t, s);  // 128 x 128 tail
 }
 
 // Measured and removed (rounds 1-3, profiles/layers_r1_dmav{0,5,6}.txt, layers_r1_ks2_{off,on}.txt,
@@ -1031,7 +1054,7 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
       return dma_cfg<DT, 2, 4, 4, 4, 64, 3, AMODE, EPI>(a, s);  // 128 x 256, 3-stage
     if (nwg(256, 256) < cus) return dma_cfg<DT, 4, 2, 2, 4, 64, 2, AMODE, EPI>(a, s);  // 128 x 128
     {  // 3x3 s1 p1 forward: the three kw taps share one staged A tile
-      const int rc = kw3_try<DT, AMODE, EPI>(a, s);
+      const int rc = kw3_split<DT, AMODE, EPI>(a, s, cus);
       if (rc != -4) return rc;
     }
     // 256 x 256 with register double-buffered fragments: +3% on the big VGG layers (profiles/)

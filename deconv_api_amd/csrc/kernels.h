@@ -39,6 +39,8 @@ struct ConvArgs {
   int KH, KW, stride, pad_h, pad_w;
   int K, Kpad;
   int M;                  // GEMM rows = N*OH*OW
+  int m_base;             // LDS-DMA / KW3 launches: first GEMM row of tile 0 (a tail launch after a
+                          //   full-round one, conv_dma_impl.h:kw3_split); 0 otherwise
   int relu, relu_in, accumulate;
   int dtype;              // 16-bit storage dtype of x/w/mask/16-bit out: 0 bf16, 1 fp16
   const uint16_t* res;    // optional residual (LDS-DMA FWD, 16-bit out): out = [ReLU](acc + bias + res)

@@ -896,3 +896,26 @@ def test_conv_c8_stream_first_layer(native_lib, N, H, W):
     finally:
         del os.environ["DV_NO_C8_STREAM"]
     assert _rel(got, alt) < 1e-2
+
+
+def test_conv_kw3_tail_split(native_lib):
+    """KW3 grid of 1.05 rounds (135 row tiles x 2 on 256 CUs): the full round runs as KW3 and the
+    last partial round's rows as a 128x128 DMA tail launch from row m_base (kw3_split); vs the
+    plain DMA kernel (DV_KW3=0) and, on a slice, the fp32 reference."""
+    g = torch.Generator().manual_seed(67)
+    N, H, W, C, OC = 44, 28, 28, 256, 512
+    x = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16)
+    cw = _cw(OC, C)
+    xd, cwd = x.to(DEV), cw.to_device(DEV)
+    got = ops.conv2d(xd, cwd, relu=True)
+    os.environ["DV_KW3"] = "0"
+    try:
+        alt = ops.conv2d(xd, cwd, relu=True)
+    finally:
+        del os.environ["DV_KW3"]
+    assert _rel(got, alt) < 1e-2
+    tail = slice(N - 3, N)  # the tail launch's images (rows >= 128 x 256)
+    ref = ops.conv2d(x[tail].float(), cw, relu=True)
+    assert _rel(got[tail], ref) < 1e-2
+    ref0 = ops.conv2d(x[:2].float(), cw, relu=True)
+    assert _rel(got[:2], ref0) < 1e-2
