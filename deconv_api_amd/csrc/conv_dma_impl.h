@@ -731,21 +731,25 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
 // (A ~17-19 KB + B 3 x 256 x 64 B per step: 1.47x fewer staged bytes per FLOP than the plain
 // implicit GEMM, which stages A once per tap).
 //
-// Zero-padded slot layout: the A tile is staged in *padded* pixel coordinates, W + 2 slots per
-// image row ([0, pixel 0 .. pixel W-1, 0]), so output row r's kw tap is simply slot(r) + kw - 1
-// and the conv's left/right zero padding are real zero slots (the DMA's out-of-range offset
-// writes zeros). A 256-row tile touching b image-row boundaries stages 258 + 2b slots (<= 384 for
-// W >= 5, host check). The round-1..2 layout staged 258 unpadded rows and zeroed the border rows
-// of the A fragments in registers: 64 v_cndmask per wave per K step, each sub-step's MFMAs
-// waiting on ALL its fragment reads first. Now every A fragment address is a per-lane constant
-// (FM x 3 VGPRs, one v_add each per step for the stage offset; LDS: B0 | B1 | A0 | A1).
+// Zero-padded slot layout: the A tile is staged in *padded* pixel coordinates, W + 8 slots per
+// image row ([0 x 4, pixel 0 .. pixel W-1, 0 x 4]), so output row r's kw tap is simply
+// slot(r) + kw - 1 and the conv's left/right zero padding are real zero slots (the DMA's
+// out-of-range offset writes zeros). Eight pad slots make consecutive output rows across an image
+// row boundary 9 slots apart, i.e. the same slot index mod 8 as adjacent rows, so a 16-row fragment
+// read that spans a boundary is as conflict-free as one that does not (with 2 pad slots, as first
+// built this round, KW3 ran at SQ_LDS_BANK_CONFLICT / IDX_ACTIVE 0.19). A 256-row tile touching b
+// image-row boundaries stages 258 + 8b slots (<= 512: W >= 9, host check; 160 KiB of LDS). The
+// round-1..2 layout staged 258 unpadded rows and zeroed the border rows of the A fragments in
+// registers: 64 v_cndmask per wave per K step, each sub-step's MFMAs waiting on ALL its fragment
+// reads first. Now every A fragment address is a per-lane constant (FM x 3 VGPRs, one v_add each
+// per step for the stage offset; LDS: B0 | B1 | A0 | A1).
 // LDS rows are 64 B with the 16-B chunk XOR-swizzled by bit 2 of the slot (q ^ 2((slot >> 2) & 1)):
-// conflict-free ds_read_b128 fragment reads for 16 consecutive slots at any base (a fragment that
-// spans an image-row boundary skips two slots: at most 2-way on one lane group).
+// conflict-free ds_read_b128 fragment reads for 16 slots of consecutive indices mod 8 at any base.
 namespace {
 __device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; }
-// staged A slots per workgroup: 8 waves x 16 x A_I >= BM + 2 + 2 x (row boundaries), host-checked
-constexpr int kw3_a_i(int bm) { return bm == 256 ? 3 : 5; }
+// staged A slots per workgroup: 8 waves x 16 x A_I >= BM + 2 + 8 x (row boundaries), host-checked
+constexpr int kw3_a_i(int bm) { return bm == 256 ? 4 : 5; }
+constexpr int kKw3Pad = 8;  // zero slots between image rows: a row jump is +9 slots = +1 (mod 8)
 }  // namespace
 
 // BM_ x BN_: 256 x 256 (8 waves of 128 x 64) or 512 x 128 (8 waves of 128 x 64: the same per-wave
@@ -773,7 +777,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_n = wgid % tiles_n, tile_m = wgid / tiles_n;
   const int m0 = a.m_base + tile_m * BM, n0 = tile_n * BN;
-  const int H = a.H, W = a.W, C = a.C, HW = a.H * a.W, Wp = a.W + 2;
+  const int H = a.H, W = a.W, C = a.C, HW = a.H * a.W, Wp = a.W + kKw3Pad;
 
   const int n_base = (m0 < a.M ? m0 : a.M - 1) / HW;
   const long long img_elems = (long long)HW * a.x_ld;
@@ -782,10 +786,12 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
       make_rsrc(a.x + (long long)n_base * img_elems, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
 
-  // padded coordinate of output row m (global image row R = m / W, W + 2 slots per row)
+  // padded coordinate of output row m (global image row R = m / W, W + 8 slots per row: 4 zero
+  // slots on each side, so consecutive output rows across a row boundary sit 9 slots apart, the
+  // same slot index mod 8 as adjacent ones: the bit-2 swizzle stays conflict-free for them)
   auto padded = [&](int m) {
     const int R = m / W;
-    return R * Wp + 1 + (m - R * W);
+    return R * Wp + kKw3Pad / 2 + (m - R * W);
   };
   const int P0 = padded(m0) - 1;                    // slot 0: the left neighbour of row m0
   const int nslots = padded(m0 + BM - 1) - P0 + 2;  // through the right neighbour of row m0 + 255
@@ -799,10 +805,11 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
     const int t = (u * NW + wave) * 16 + lrow;
     const int P = P0 + t;
     const int R = P / Wp, c = P - R * Wp;
-    const int m = R * W + c - 1;
-    const bool valid = t < nslots && c > 0 && c <= W && m < a.M;  // else a zero slot
+    const int px = c - kKw3Pad / 2;
+    const int m = R * W + px;
+    const bool valid = t < nslots && px >= 0 && px < W && m < a.M;  // else a zero slot
     const int n = R / H, oh = R - n * H;
-    r_pix[u] = valid ? (n - n_base) * HW + oh * W + c - 1 : 0;
+    r_pix[u] = valid ? (n - n_base) * HW + oh * W + px : 0;
     r_oh[u] = valid ? oh : -(1 << 28);
   }
   const int nch = C / 32;
@@ -914,8 +921,8 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
     if (kw3_mode() == 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH ||
         a.W != a.OW || a.W < 1 || a.C % 32 || a.mask || a.ws || a.OCpad % BN || (long long)a.Kpad < 9LL * a.C)
       return -4;
-    // zero-padded slots of a BM-row tile: BM + 2 + 2 x (image-row boundaries, <= (BM - 1) / W + 1)
-    if (BM + 2 + 2 * ((BM - 1) / a.W + 1) > kw3_a_i(BM) * 8 * 16) return -4;  // W >= 5 (256), >= 9 (512)
+    // zero-padded slots of a BM-row tile: BM + 2 + 8 x (image-row boundaries, <= (BM - 1) / W + 1)
+    if (BM + 2 + kKw3Pad * ((BM - 1) / a.W + 1) > kw3_a_i(BM) * 8 * 16) return -4;  // W >= 9 (256), >= 35 (512)
     if (a.m_base != 0) return -4;
     int tiles_m = (a.M + BM - 1) / BM;
     if (tiles_m_limit > 0 && tiles_m_limit < tiles_m) tiles_m = tiles_m_limit;
