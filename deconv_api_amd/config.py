@@ -33,8 +33,11 @@ class Config:
     top: int = 8                          # find_top_filters default (app/deepdream.py:369)
     mode: str = "all"                     # visualize_mode (app/main.py:64)
     jpeg_quality: int = 95                # OpenCV imencode default (app/main.py:73)
-    max_batch: int = 64                   # request batcher
-    batch_timeout_ms: float = 4.0
+    # request batcher. Sweep at 128 in-process clients (profiles/latency_r3_batch_sweep.txt):
+    # 16 / 2 ms 2858 req/s (p50 41 ms) vs 64 / 2 ms 1989 (p50 59 ms) - small batches keep more of
+    # them in flight through decode -> GPU -> encode; the engine still does ~5.7k img/s at B = 16
+    max_batch: int = 16
+    batch_timeout_ms: float = 2.0
     max_queue: int = 4096                 # backpressure: 503 beyond this many pending requests
     request_timeout_s: float = 120.0
     codec_workers: int = 8                # decode threads (PIL releases the GIL while decoding)

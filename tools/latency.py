@@ -126,10 +126,11 @@ def main():
     ap.add_argument("--requests", type=int, default=256)
     ap.add_argument("--img", type=int, default=320, help="client image side (resized to 224 on GPU)")
     ap.add_argument("--sample", action="store_true", help="sample Python stacks during the last load run")
-    ap.add_argument("--timeout-ms", type=float, default=2.0, help="batcher straggler wait while the GPU is busy")
+    ap.add_argument("--timeout-ms", type=float, default=Config.batch_timeout_ms,
+                    help="batcher straggler wait while the GPU is busy")
     ap.add_argument("--chunk", type=int, default=16, help="images per encode+deliver chunk")
     ap.add_argument("--codec-workers", type=int, default=16)
-    ap.add_argument("--max-batch", type=int, default=64)
+    ap.add_argument("--max-batch", type=int, default=Config.max_batch)
     ap.add_argument("--switch-us", type=int, default=500)
     ap.add_argument("--enc-workers", type=int, default=2)
     ap.add_argument("--enc-threads", type=int, default=8)
