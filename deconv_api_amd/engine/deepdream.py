@@ -545,21 +545,27 @@ class TiledDeepDream(DeepDream):
             self._tile_apply(st, it)
 
     def _stage_shifts(self, st) -> None:
-        """This octave's random roll table -> the device, without a host sync: through a pinned
-        buffer of the octave's own state (a pageable H2D copy blocks the host until the stream
+        """This octave's random roll table -> the device, without a host sync: through pinned
+        buffers of the octave's own state (a pageable H2D copy blocks the host until the stream
         drains; one shared pinned buffer would make octave k+1 wait for octave k's upload, which
-        queues behind octave k-1's replay)."""
+        queues behind octave k-1's replay). Two buffers per state, used alternately: reusing one
+        waits for this shape's previous upload, which sits behind the whole previous dream batch
+        on the stream, so the host could not run more than one batch ahead
+        (``host_enqueue_s`` 0.087 s of a 0.30 s config-5 batch)."""
         shifts = torch.randint(-self.tile // 2, self.tile // 2 + 1, (self.s.iterations, 2), generator=self.gen)
-        pin = getattr(st, "shift_pin", None)
-        if pin is None or pin.shape != shifts.shape:
-            pin = st.shift_pin = torch.empty(shifts.shape, dtype=torch.int32, pin_memory=True)
-            st.shift_ev = None
-        if st.shift_ev is not None:
-            st.shift_ev.synchronize()  # this shape's previous upload (the previous dream batch)
-        pin.copy_(shifts)
-        st.shifts.copy_(pin, non_blocking=True)
-        st.shift_ev = torch.cuda.Event()
-        st.shift_ev.record()
+        pins = getattr(st, "shift_pins", None)
+        if pins is None or pins[0].shape != shifts.shape:
+            pins = st.shift_pins = [torch.empty(shifts.shape, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            st.shift_evs = [None, None]
+            st.shift_i = 0
+        i = st.shift_i
+        st.shift_i ^= 1
+        if st.shift_evs[i] is not None:
+            st.shift_evs[i].synchronize()  # this buffer's previous upload (two dream batches ago)
+        pins[i].copy_(shifts)
+        st.shifts.copy_(pins[i], non_blocking=True)
+        st.shift_evs[i] = torch.cuda.Event()
+        st.shift_evs[i].record()
 
     def _capture(self, fn) -> torch.cuda.CUDAGraph:
         g = torch.cuda.CUDAGraph()
