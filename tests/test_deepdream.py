@@ -549,7 +549,9 @@ def test_gpu_tiled_collective_octave_captured(native_lib):
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "tools/tiled_collective.py"],
                        cwd=root, env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
+    # on failure keep the child's error lines (the watchdog message precedes a long frame dump)
+    why = [ln for ln in r.stderr.splitlines() if "rror" in ln or "what()" in ln or "abort" in ln.lower()]
+    assert r.returncode == 0, "\n".join(why[:40]) + "\n...\n" + r.stderr[-2000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["backend"] == "nccl" and out["collective"] is True, out
     assert out["octave_graph"] is True and out["step_graphs"] is False, out
