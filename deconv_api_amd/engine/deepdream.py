@@ -29,6 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from ..ops import native
+from ..runtime.capture import capture, drain_collective
 from ..utils.logging import get_logger
 from ..ops.autograd import loss_tap, premasked_grads, sumsq_core
 
@@ -223,10 +224,7 @@ class DeepDream:
                 for _ in range(2):  # warm up allocator / autograd on a side stream before capture
                     self._fused_step(st)
             torch.cuda.current_stream(self.device).wait_stream(s)
-            st.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(st.graph):
-                for _ in range(steps):
-                    self._fused_step(st)
+            st.graph, _ = capture(lambda: [self._fused_step(st) for _ in range(steps)])
         st.steps = steps
         self._cache_put(key, st)
         return st
@@ -252,9 +250,7 @@ class DeepDream:
             for _ in range(2):  # warm up allocator / autograd on a side stream before capture
                 self._step(x, done)
         torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            loss = self._step(x, done)
+        g, loss = capture(lambda: self._step(x, done))
         self._cache_put(key, (g, x, done, loss))
         return self._graphs[key]
 
@@ -458,9 +454,7 @@ class TiledDeepDream(DeepDream):
             for _ in range(2):
                 self._tile_grad(bx, shift, plan, grad, loss)
         torch.cuda.current_stream(x.device).wait_stream(st)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._tile_grad(bx, shift, plan, grad, loss)
+        g, _ = capture(lambda: self._tile_grad(bx, shift, plan, grad, loss))
         self._tgraphs[key] = (g, bx, shift, grad, loss)
         return self._tgraphs[key]
 
@@ -568,10 +562,7 @@ class TiledDeepDream(DeepDream):
         st.shift_evs[i].record()
 
     def _capture(self, fn) -> torch.cuda.CUDAGraph:
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            fn()
-        return g
+        return capture(fn)[0]
 
     def _gradient_ascent_fused(self, x: torch.Tensor) -> torch.Tensor:
         import torch.distributed as dist
@@ -586,11 +577,14 @@ class TiledDeepDream(DeepDream):
             # warm up on a side stream (autograd / allocator), restore the image, capture the octave
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
+            work = None
             with torch.cuda.stream(s):
                 self._tile_compute(st, 0)
                 if coll:  # the collective's communicator is set up outside the capture
-                    dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
+                    work = dist.all_gather_into_tensor(st.packs.view(-1), st.pack, async_op=True)
             torch.cuda.current_stream(self.device).wait_stream(s)
+            if coll:  # retire the eager warm-up collective before the capture opens
+                drain_collective(work, self.device)
             if not coll or CAPTURE_COLLECTIVE:
                 # the whole octave, all-gathers included (RCCL collectives are graph-capturable):
                 # one replay per octave instead of `iterations` replays + eager collectives

@@ -9,6 +9,7 @@ from typing import Dict, Tuple
 
 import torch
 
+from ..runtime.capture import capture
 from .deconvnet import DeconvNet
 
 BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
@@ -39,11 +40,9 @@ class GraphedDeconv:
             for _ in range(2):  # warm up kernels/allocator off the capture stream
                 self.engine.run(x, layer, k=self.k, mode=self.mode)
         torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        # thread-local: the service's completion thread keeps synchronizing on earlier batches'
-        # events while the worker captures a new (layer, bucket) graph
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            res = self.engine.run(x, layer, k=self.k, mode=self.mode)
+        # thread-local (runtime/capture.py): the service's completion thread keeps synchronizing on
+        # earlier batches' events while the worker captures a new (layer, bucket) graph
+        g, res = capture(lambda: self.engine.run(x, layer, k=self.k, mode=self.mode))
         return g, x, res
 
     def get(self, layer: str, B: int):

@@ -193,7 +193,11 @@ class StagingRing:
         st.ev_comp1.record(cur)
         host_off = torch.empty(n + 1, dtype=torch.int64, pin_memory=True)
         self.back_stream.wait_event(st.ev_comp1)
+        # both device blocks are read on back_stream after this function returns: without
+        # record_stream the compute stream's pool could hand `off` to the next batch before the
+        # D2H below ran (corrupt scan offsets)
         packed.record_stream(self.back_stream)
+        off.record_stream(self.back_stream)
         with torch.cuda.stream(self.back_stream):
             host_off.copy_(off, non_blocking=True)
             st.ev_back1 = torch.cuda.Event(enable_timing=True)

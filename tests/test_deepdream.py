@@ -556,3 +556,62 @@ def test_gpu_tiled_collective_octave_captured(native_lib):
     assert out["backend"] == "nccl" and out["collective"] is True, out
     assert out["octave_graph"] is True and out["step_graphs"] is False, out
     assert out["equal"] is True, out
+
+
+@pytest.mark.gpu
+def test_gpu_capture_while_other_thread_polls_events(native_lib):
+    """Every DeepDream capture is thread-local (runtime/capture.py): octave graphs (untiled and
+    tiled) are captured while a second thread loops on Event.record/query/synchronize on its own
+    stream - what the RCCL watchdog and the deconv service's completion thread do. In torch's
+    default global mode those calls invalidate the capture (round-3 intermittent abort)."""
+    import threading
+
+    stop = threading.Event()
+    polls = [0]
+    errors = []
+
+    def poller():
+        try:
+            s = torch.cuda.Stream()
+            buf = torch.zeros(1 << 16, device="cuda")
+            while not stop.is_set():
+                with torch.cuda.stream(s):
+                    buf.add_(1.0)
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+                ev.query()
+                ev.synchronize()
+                polls[0] += 1
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    inc = InceptionV3(0).build("cuda")
+    res = ResNet50(0).build("cuda", torch.float16)
+    xi = (torch.rand(2, 120, 120, 3, generator=torch.Generator().manual_seed(21)) * 2 - 1).cuda()
+    xr = (torch.rand(2, 200, 260, 3, generator=torch.Generator().manual_seed(22)) * 2 - 1).cuda()
+    si = DreamSettings(iterations=3, octaves=2, max_loss=None)
+    sr = DreamSettings(layers=dict(RESNET_LAYERS), octaves=2, iterations=3, max_loss=None)
+    want_i = DeepDream(inc, si, use_graphs=False).run(xi)
+    want_r = TiledDeepDream(res, sr, tile=128, seed=4, use_graphs=False).run(xr)
+    torch.cuda.synchronize()
+    t = threading.Thread(target=poller, daemon=True)
+    t.start()
+    try:
+        while polls[0] < 10 and not errors:  # the poller is running before the first capture opens
+            pass
+        before = polls[0]
+        ddi = DeepDream(inc, si, use_graphs=True)
+        got_i = ddi.run(xi)
+        ddr = TiledDeepDream(res, sr, tile=128, seed=4, use_graphs=True)
+        got_r = ddr.run(xr)
+        torch.cuda.synchronize()
+        during = polls[0] - before
+    finally:
+        stop.set()
+        t.join(timeout=30)
+    assert not errors, errors
+    assert during > 0
+    assert all(st.graph is not None for st in ddi._graphs.values())
+    assert all(st.graph is not None for st in ddr._tgraphs.values())
+    assert (got_i - want_i).abs().max() < 1e-3
+    assert _cos(got_r - xr, want_r - xr) > 0.99

@@ -37,12 +37,15 @@ def _compare(model, B, hw, layers, seed=0):
         rg = gpu.backward(st_g, idx).cpu()
         rc = cpu.backward(st_c, idx.cpu())
         assert rg.shape == rc.shape == (B, 4, hw, hw, 3)
+        cs = []
         for b in range(B):
             for k in range(4):
                 if idx[b, k] < 0:
                     continue
                 c = _cos(rg[b, k], rc[b, k])
+                cs.append(c)
                 assert c > 0.98, (layer, b, k, c)
+        print(f"loose-cos {hw} {layer} min {min(cs):.5f} median {sorted(cs)[len(cs) // 2]:.5f}")
 
 
 def test_engine_small_all_targets(native_lib, small_specs):

@@ -153,3 +153,63 @@ def test_visualize_all_layers_k8_parity(engines, target):
             assert c >= 0.999, (target, name, kk, c)
             checked += 1
     assert checked >= 8 * len(want_layers) // 2, checked
+
+
+# ---- strict FORWARD parity: the GPU's discrete decisions (switch codes, top-k) ----
+
+POOL_CONVS = [("block1_conv2", "block1_conv1"), ("block2_conv2", "block2_conv1"), ("block3_conv3", "block3_conv2"),
+              ("block4_conv3", "block4_conv2"), ("block5_conv3", "block5_conv2")]
+
+
+@pytest.fixture(scope="module")
+def cpu_bf16w(native_lib):
+    """CPU fp32 engine on the bf16-ROUNDED weights the GPU uses: per layer, only accumulation order
+    and the output rounding differ between the two."""
+    m = VGG16.random(0, include_top=False)
+    sd = {k: (v.to(torch.bfloat16).float() if v.is_floating_point() else v) for k, v in m.state_dict().items()}
+    return DeconvNet(VGG16.from_state_dict(sd, specs=m.specs).build("cpu", torch.float32)), \
+        DeconvNet(VGG16.from_state_dict(sd, specs=m.specs).build("cuda", torch.bfloat16))
+
+
+@pytest.mark.parametrize("conv,prev", POOL_CONVS)
+def test_strict_forward_switch_codes(cpu_bf16w, x3, conv, prev):
+    """Each fused conv + 2x2 max-pool epilogue, fed the CPU forward's own (bf16-rounded) input of
+    that layer: GPU switch codes == the fp32 CPU first-max codes on >= 99.9 % of the windows whose
+    best and second-best differ by more than 1 % (all-zero windows, exact ties, must give code 0
+    on both: first max in row-major order, app/deepdream.py:170-187)."""
+    cpu, gpu = cpu_bf16w
+    xc = x3.float().cpu()
+    stc = cpu.forward(xc, prev, fuse_pools=False, keep_all=True)
+    inp = stc.outputs[prev].to(torch.bfloat16)
+    act = ops.conv2d(inp.float(), cpu.rt.convs[conv].fwd, relu=True)  # [N, H, W, C] fp32
+    _, want = ops.maxpool2x2(act)
+    _, got = ops.conv2d(inp.cuda(), gpu.rt.convs[conv].fwd, relu=True, epilogue="pool")
+    got = got.cpu()
+    assert got.shape == want.shape
+    N, H, W, C = act.shape
+    win = act.reshape(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 5, 2, 4).reshape(N, H // 2, W // 2, C, 4)
+    top2 = win.topk(2, dim=-1).values
+    zero = top2[..., 0] == 0
+    clear = (top2[..., 0] - top2[..., 1]) > 1e-2 * top2[..., 0]
+    assert torch.equal(got[zero], want[zero]) and not bool(got[zero].any())
+    agree = float((got[clear] == want[clear]).double().mean())
+    assert int(clear.sum()) > 0.2 * clear.numel(), (conv, int(clear.sum()))
+    assert agree >= 0.999, (conv, agree, int(clear.sum()))
+
+
+@pytest.mark.parametrize("layer", ["block1_pool", "block3_conv3", "block4_pool", "block5_conv3"])
+def test_strict_forward_topk(cpu_bf16w, x3, layer):
+    """Top-4 filter selection from the whole bf16 GPU forward vs the fp32 CPU forward on the same
+    input: every GPU-selected filter's CPU channel sum is within 2 % of the CPU's 4th best, and the
+    sets are equal whenever the CPU's 4th and 5th sums are more than 2 % apart."""
+    cpu, gpu = cpu_bf16w
+    st = gpu.forward(x3, layer)
+    idx, _ = gpu.select_filters(st.out, 4)
+    sums = ops.channel_sum(cpu.forward(x3.float().cpu(), layer).out)
+    for b in range(x3.shape[0]):
+        srt = torch.sort(sums[b], descending=True).values
+        got = sums[b, idx[b].long().cpu()]
+        assert float(got.min()) >= float(srt[3]) * 0.98, (layer, b, idx[b].tolist())
+        if float(srt[3] - srt[4]) > 0.02 * float(srt[3]):
+            want = set(torch.topk(sums[b], 4).indices.tolist())
+            assert set(idx[b].tolist()) == want, (layer, b, idx[b].tolist(), sorted(want))
