@@ -750,6 +750,7 @@ __device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; 
 // staged A slots per workgroup: 8 waves x 16 x A_I >= BM + 2 + 8 x (row boundaries), host-checked
 constexpr int kw3_a_i(int bm) { return bm == 256 ? 4 : 5; }
 constexpr int kKw3Pad = 8;  // zero slots between image rows: a row jump is +9 slots = +1 (mod 8)
+constexpr int kKw3DefaultVar = 0;
 }  // namespace
 
 // BM_ x BN_: 256 x 256 (8 waves of 128 x 64) or 512 x 128 (8 waves of 128 x 64: the same per-wave
@@ -760,7 +761,13 @@ constexpr int kKw3Pad = 8;  // zero slots between image rows: a row jump is +9 s
 // 6.85-7.03k to 5.80-5.83k img/s, profiles/bench_c2_r3_ab.txt. Equal within noise and removed:
 // static priority for waves 4-7 instead of the per-sub-step flips, a 320-row M tile, and the DMAs
 // issued behind the first sub-step's fragment reads, profiles/kw3_variants_r3.txt.)
-template <int DT, int EPI, int BN_ = 256, int BM_ = 256>
+// VAR (kw3_var(), DV_KW3_VAR): 0 = one read burst + 32 MFMAs per kw sub-step; 1 = fragment
+// pipeline: the next sub-step's B fragments are read into a second register set at the start of a
+// sub-step and each A fragment register is refilled with the next sub-step's fragment right after
+// its 4 MFMAs, so only the first sub-step of a K step waits for LDS reads; the next step's DMAs are
+// issued behind the first sub-step's reads. 8 / 9: ablations for tools/kw3_ab.py only (no
+// epilogue stores / no K loop): NOT correct outputs.
+template <int DT, int EPI, int BN_ = 256, int BM_ = 256, int VAR = 0>
 __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
   constexpr int BN = BN_, BM = BM_, NW = 8;
   constexpr int WN = BN / 64, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
@@ -865,12 +872,59 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
   asm volatile("" : "+v"(baddr[0]), "+v"(baddr[1]));
 
   issue(0, 0);
-  for (int k = 0; k < nsteps; ++k) {
+  const int nk = VAR == 9 ? 0 : nsteps;
+  for (int k = 0; k < nk; ++k) {
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
-    if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
     const int aoff = (k & 1) * A_BYTES;
     const uint8_t* Bs = smem + baddr[k & 1];
+    if constexpr (VAR == 1) {
+      v8 bA[FN], bB[FN], af[FM];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(smem + aoff + aaddr[i][0]);
+      if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
+      // kw = 0 (bA) while kw = 1 is read: B into bB up front, A into each af[i] after its MFMAs
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bB[j] = *reinterpret_cast<const v8*>(Bs + BN * 64 + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
+        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aaddr[i][1]);
+      }
+      // kw = 1 (bB) while kw = 2 is read into bA / af
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + 2 * BN * 64 + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bB[j], acc[i][j]);
+        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aaddr[i][2]);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
+      // pin that order (one pipeline, SyncID 0): hipcc otherwise sinks each prefetch down to its
+      // use and waits lgkmcnt(0) right after it
+      __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, FM * FN, 0);
+      continue;
+    }
+    if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       v8 bf[FN], af[FM];
@@ -887,6 +941,13 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
     }
   }
   wait_vm<0>();
+  if constexpr (VAR == 8) {  // ablation: keep the accumulators live, store nothing
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
 
   if constexpr (EPI == CONV_E_BF16) {
     if (a.vec_epi) {
@@ -905,11 +966,344 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
     epilogue<DT, FM, FN, EPI, false>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
 }
 
+// ---------------------------------------------------------------------------------------------
+// KW3P: persistent KW3 for plain 16-bit epilogues (no residual / emask / accumulate / unpool / split
+// output). tools/kw3_ab.py priced the non-persistent kernel's tile boundaries on the config-2 shapes:
+// without epilogue stores a launch runs 9-14 % faster (VAR 8) and prologue + epilogue alone are
+// 12-17 % of it (VAR 9). Every workgroup of a round reaches its epilogue at the same moment, so the
+// whole chip writes its C tiles (32 MB for 256 256 x 256 tiles) in one burst while no MFMA runs,
+// and the next round starts with every CU waiting for its first DMA. Here one workgroup per CU walks
+// tiles v = blockIdx.x, + gridDim.x, ... (XCD-remapped as before) and
+//   * the LAST K step of tile t issues step 0 of tile t + 1 (its gather state computed there), so
+//     the next tile's first operands land while this tile's last MFMAs and epilogue run;
+//   * the epilogue never touches LDS: each 16 x 16 accumulator block is transposed in registers by
+//     two DPP lane swaps (quad_perm [1,0,3,2], then [2,3,0,1]) so a lane holds 4 consecutive
+//     channels of one pixel, and goes out as one 8-B buffer store (rows past M: out-of-range
+//     offset, discarded);
+//   * those stores drain while tile t + 1's first K step computes (the wait at the end of that step
+//     is the first one that covers them).
+// Main loop: the VAR 1 fragment pipeline. Numerics equal the LDS-staged epilogue (same fp32 ops,
+// same rounding). Buffer parity follows a global step counter (odd step counts per tile).
+template <int DT, int BN_ = 256, int BM_ = 256, bool IL = false>
+__global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, int tiles_n, int ntiles) {
+  constexpr int BN = BN_, BM = BM_, NW = 8;
+  constexpr int WN = BN / 64, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
+  constexpr int A_I = kw3_a_i(BM);
+  constexpr int B_I = 3 * BN / 16 / NW;
+  constexpr int A_BYTES = A_I * NW * 1024, B_BYTES = 3 * BN * 64;
+  typedef typename Vec8<DT>::type v8;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * (A_BYTES + B_BYTES)];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int H = a.H, W = a.W, C = a.C, HW = a.H * a.W, Wp = a.W + kKw3Pad;
+  const long long img_elems = (long long)HW * a.x_ld;
+  const long long x_total = (long long)a.N * img_elems;
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
+  const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out, (uint64_t)a.out_elems * 2);
+  const int lrow = lane >> 2;
+  const int lchunk = (lane & 3) ^ kw3_swz(lrow);
+  const int q = lane >> 4;
+  const int arow0 = wm * FM * 16 + (lane & 15);
+  const int brow0 = wn * FN * 16 + (lane & 15);
+  int baddr0 = brow0 * 64 + ((q ^ kw3_swz(brow0)) << 4);  // stage 1: + B_BYTES
+  asm volatile("" : "+v"(baddr0));
+  const int nch = C / 32;
+  const int nsteps = 3 * nch;
+
+  auto padded = [&](int m) {
+    const int R = m / W;
+    return R * Wp + kKw3Pad / 2 + (m - R * W);
+  };
+
+  // ---- gather state of the tile whose DMAs are being issued ----
+  int m0 = 0, n0 = 0, P0 = 0, nslots = 0;
+  // per A slot: (pixel index relative to the tile's first image) << 12 | output row oh, or ~0 for a
+  // zero slot (host: H < 4096 and 2 HW + BM < 2^19); one VGPR per slot instead of two
+  uint32_t r_po[A_I];
+  __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, 16);
+  auto setup = [&](int v) {
+    const int wgid = xcd_remap(v, ntiles);
+    const int tile_n = wgid % tiles_n, tile_m = wgid / tiles_n;
+    m0 = a.m_base + tile_m * BM;
+    n0 = tile_n * BN;
+    const int n_base = (m0 < a.M ? m0 : a.M - 1) / HW;
+    xr = make_rsrc(a.x + (long long)n_base * img_elems, (uint64_t)(x_total - (long long)n_base * img_elems) * 2);
+    P0 = padded(m0) - 1;
+    nslots = padded(m0 + BM - 1) - P0 + 2;
+#pragma unroll
+    for (int u = 0; u < A_I; ++u) {
+      const int t = (u * NW + wave) * 16 + lrow;
+      const int P = P0 + t;
+      const int R = P / Wp, c = P - R * Wp;
+      const int px = c - kKw3Pad / 2;
+      const int m = R * W + px;
+      const bool valid = t < nslots && px >= 0 && px < W && m < a.M;
+      const int n = R / H, oh = R - n * H;
+      r_po[u] = valid ? ((uint32_t)((n - n_base) * HW + oh * W + px) << 12) | (uint32_t)oh : ~0u;
+    }
+  };
+  auto issue = [&](int step, int buf) {
+    const int kh = step / nch, cc = step - kh * nch;
+    uint8_t* As = smem + 2 * B_BYTES + buf * A_BYTES;
+    uint8_t* Bs = smem + buf * B_BYTES;
+#pragma unroll
+    for (int u = 0; u < A_I; ++u) {
+      if ((u * NW + wave) * 16 >= nslots) continue;
+      const int oh = (int)(r_po[u] & 0xFFFu), pix = (int)(r_po[u] >> 12);
+      const bool ok = r_po[u] != ~0u && (unsigned)(oh + kh - 1) < (unsigned)H;
+      const uint32_t voff =
+          ok ? (uint32_t)((((long long)(pix + (kh - 1) * W)) * a.x_ld + cc * 32 + lchunk * 8) * 2) : kOOB;
+      dma16(xr, As + (u * NW + wave) * 1024, voff);
+    }
+#pragma unroll
+    for (int u = 0; u < B_I; ++u) {
+      const int vv = u * NW + wave;
+      const int kw = vv / (BN / 16), brow = (vv % (BN / 16)) * 16 + lrow;
+      const uint32_t voff =
+          (uint32_t)((((long long)(n0 + brow)) * a.Kpad + (kh * 3 + kw) * C + cc * 32 + lchunk * 8) * 2);
+      dma16(wr, Bs + vv * 1024, voff);
+    }
+  };
+
+  // IL: one DMA piece of step (kh, cc) into stage buf, branch-free (a piece that must not load
+  // reads out of range: zeros into a slot nobody reads), so it can sit between MFMA groups.
+  // Pieces 0 .. A_I - 1: A slot groups; A_I .. A_I + B_I - 1: B row groups.
+  auto piece = [&](int p, int kh, int cc, int buf, bool none) {
+    if (p < A_I) {
+      const int u = p;
+      const uint32_t po = r_po[u];
+      const int oh = (int)(po & 0xFFFu), pix = (int)(po >> 12);
+      const bool ok = !none && (u * NW + wave) * 16 < nslots && po != ~0u && (unsigned)(oh + kh - 1) < (unsigned)H;
+      const uint32_t off = (uint32_t)(((pix + (kh - 1) * W) * (int)a.x_ld + cc * 32 + lchunk * 8) * 2);
+      dma16(xr, smem + 2 * B_BYTES + buf * A_BYTES + (u * NW + wave) * 1024, ok ? off : kOOB);
+    } else {
+      const int vv = (p - A_I) * NW + wave;
+      const int kw = vv / (BN / 16), brow = (vv % (BN / 16)) * 16 + lrow;
+      const uint32_t off = (uint32_t)(((n0 + brow) * a.Kpad + (kh * 3 + kw) * C + cc * 32 + lchunk * 8) * 2);
+      dma16(wr, smem + buf * B_BYTES + vv * 1024, none ? kOOB : off);
+    }
+  };
+  constexpr int NP = A_I + B_I;  // DMA pieces per wave and K step
+  static_assert(NP <= 2 * FM, "the pieces ride in the first two kw sub-steps");
+
+  int v = blockIdx.x;
+  if (v >= ntiles) return;
+  setup(v);
+  issue(0, 0);
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  int g = 0;  // global K step counter: LDS stage parity
+  for (;;) {
+    const int cm0 = m0, cn0 = n0;
+    // per-lane A fragment addresses of this tile (stage 0; opaque: one VGPR each, as in KW3)
+    int aaddr[FM][3];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int s1 = padded(cm0 + arow0 + i * 16) - P0;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int sl = s1 + kw - 1;
+        aaddr[i][kw] = 2 * B_BYTES + sl * 64 + ((q ^ kw3_swz(sl)) << 4);
+        asm volatile("" : "+v"(aaddr[i][kw]));
+      }
+    }
+    auto aad = [&](int i, int kw) { return aaddr[i][kw]; };
+    const int vnext = v + (int)gridDim.x;
+    const bool more = vnext < ntiles;
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // one K step on stage `cur` (its DMAs landed and every wave passed the barrier); `nxt` issues
+    // the following step's DMAs behind the first fragment reads; ends with the wait + barrier that
+    // make the next step's stage readable
+    auto kstep = [&](int cur, auto nxt) {
+      const int aoff = cur * A_BYTES;
+      const uint8_t* Bs = smem + baddr0 + cur * B_BYTES;
+      v8 bA[FN], bB[FN], af[FM];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 0));
+      nxt();
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bB[j] = *reinterpret_cast<const v8*>(Bs + BN * 64 + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
+        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 1));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + 2 * BN * 64 + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bB[j], acc[i][j]);
+        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 2));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
+      __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, FM * FN, 0);
+      // my next-stage DMAs landed AND every fragment read of this stage returned (the barrier may
+      // be scheduled among the last MFMAs: with reads still in flight, another wave's next DMA
+      // into this stage could overwrite what they have not fetched yet)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    // IL form of kstep: the NP DMA pieces of the next step are issued one per A-fragment group of
+    // the kw = 0 (and kw = 1) sub-step, between MFMA groups, instead of all at once after the first
+    // reads (both waves of a SIMD issued them together, with the matrix pipe idle meanwhile)
+    auto kstep_il = [&](int cur, int nkh, int ncc, bool none) {
+      const int aoff = cur * A_BYTES;
+      const uint8_t* Bs = smem + baddr0 + cur * B_BYTES;
+      v8 bA[FN], bB[FN], af[FM];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 0));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bB[j] = *reinterpret_cast<const v8*>(Bs + BN * 64 + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
+        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 1));
+        if (i < NP) piece(i, nkh, ncc, cur ^ 1, none);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + 2 * BN * 64 + j * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bB[j], acc[i][j]);
+        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 2));
+        if (FM + i < NP) piece(FM + i, nkh, ncc, cur ^ 1, none);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
+      __builtin_amdgcn_sched_group_barrier(0x100, FN + FM + FN, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (i < NP) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (FM + i < NP) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, FM * FN, 0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    if constexpr (IL) {
+#pragma unroll 1
+      for (int k = 0; k + 1 < nsteps; ++k, ++g) {
+        const int kh = (k + 1) / nch;
+        kstep_il(g & 1, kh, k + 1 - kh * nch, false);
+      }
+      if (more) setup(vnext);
+      kstep_il(g & 1, 0, 0, !more);
+    } else {
+#pragma unroll 1
+      for (int k = 0; k + 1 < nsteps; ++k, ++g) kstep(g & 1, [&] { issue(k + 1, (g & 1) ^ 1); });
+      // the last step issues the next tile's first step (gather state computed before its fragments
+      // are live): those operands land behind this step's MFMAs, its trailing wait covers them, and
+      // the epilogue's stores below are younger than them
+      if (more) setup(vnext);
+      kstep(g & 1, [&] {
+        if (more) issue(0, (g & 1) ^ 1);
+      });
+    }
+    ++g;
+    // ---- epilogue: register transpose -> 8-B stores (no LDS, no barrier) ----
+    // lane roles (see the header; derived here, not kept live across the K loop): this lane stores
+    // row rsub of each 16-row block, 4 columns from csub
+    const int cl = lane & 15, ce = cl & 1, cu = (cl >> 1) & 1;
+    const int rsub = (lane >> 4) * 4 + ce * 2 + cu, csub = cl & ~3;
+    const bool pre_relu = a.relu != 0;
+    // (every bias load before the first store: a load issued behind stores would wait for them)
+    float bias[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bias[j] = a.bias ? a.bias[cn0 + wn * FN * 16 + j * 16 + cl] : 0.f;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int gcol = cn0 + wn * FN * 16 + j * 16 + cl;
+      const bool rl = pre_relu && relu_at(a, gcol);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        float f0 = acc[i][j][0] + bias[j], f1 = acc[i][j][1] + bias[j], f2 = acc[i][j][2] + bias[j],
+              f3 = acc[i][j][3] + bias[j];
+        if (rl) {
+          f0 = fmaxf(f0, 0.f);
+          f1 = fmaxf(f1, 0.f);
+          f2 = fmaxf(f2, 0.f);
+          f3 = fmaxf(f3, 0.f);
+        }
+        const uint32_t p0 = pack2<DT>(f0, f1), p1 = pack2<DT>(f2, f3);  // rows (r0, r1) / (r2, r3)
+        // swap with lane ^ 1: even lanes end with rows r0, r1 of columns (c, c + 1), odd lanes with r2, r3
+        const uint32_t keep = ce ? p1 : p0;
+        const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(ce ? p0 : p1), 0xB1, 0xF, 0xF, false);
+        const uint32_t lo = ce ? recv : keep, hi = ce ? keep : recv;
+        const uint32_t d0 = (lo & 0xFFFFu) | (hi << 16), d1 = (lo >> 16) | (hi & 0xFFFF0000u);
+        // swap with lane ^ 2: one row x 4 consecutive columns per lane
+        const uint32_t recv2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(cu ? d0 : d1), 0x4E, 0xF, 0xF, false);
+        const uint32_t w0 = cu ? recv2 : d0, w1 = cu ? d1 : recv2;
+        const int row = cm0 + wm * FM * 16 + i * 16 + rsub;
+        const int col = cn0 + wn * FN * 16 + j * 16 + csub;
+        const uint32_t off = row < a.M ? (uint32_t)(((long long)row * a.out_ld + col) * 2) : kOOB;
+        typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{w0, w1}, orr, (int)off, 0, 0);
+      }
+    }
+    if (!more) break;
+    v = vnext;
+  }
+}
+
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, cu = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cu = 256;
+    return cu > 0 ? cu : 256;
+  }();
+  return n;
+}
+
 // DV_KW3: 0 disables the shared-kw-tap kernel (A/B), 2 forces it for every eligible launch regardless
 // of the grid size (tests: small shapes with many image borders per tile). Read per launch.
 static int kw3_mode() {
   const char* e = std::getenv("DV_KW3");
   return e ? std::atoi(e) : 1;
+}
+// DV_KW3_VAR: the KW3 main-loop variant (conv_dma_kw3_kernel VAR; 8 / 9 are timing ablations that
+// produce wrong outputs, tools/kw3_ab.py only). Read per launch.
+static int kw3_var() {
+  const char* e = std::getenv("DV_KW3_VAR");
+  return e ? std::atoi(e) : kKw3DefaultVar;
 }
 
 // tiles_m_limit > 0: launch only the first tiles_m_limit row tiles (kw3_split's full rounds)
@@ -931,7 +1325,39 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
     if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
     // (a B-fragment double buffer across the kw sub-steps measured equal and was removed,
     // profiles/layers_r1_kw3_{nofp,on}.txt)
-    hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN, BM>), dim3((unsigned)nwg), dim3(512), 0, s, a, tiles_n);
+    const int var = kw3_var();
+    const dim3 grid((unsigned)nwg);
+    if constexpr (EPI == CONV_E_BF16) {
+      // persistent KW3P: plain 16-bit epilogue only (its register-transpose stores write exactly
+      // the C tile), output addressable by a 31-bit buffer offset, one workgroup per CU
+      // (IL, var 3: the pieces' 32-bit offset math needs the gather span and the weight matrix
+      // below 2^31 bytes)
+      if ((var == 2 || var == 3) && a.res == nullptr && a.emask == nullptr && !a.accumulate && a.ucode == nullptr &&
+          a.out2 == nullptr && a.OC == a.OCpad && a.OC % 4 == 0 && a.out_ld % 4 == 0 &&
+          a.out_elems * 2 < 0x7FFFFFF0LL && a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19) &&
+          (2LL * a.H * a.W + BM) * a.x_ld * 2 < 0x7FFFFFF0LL && (long long)a.OCpad * a.Kpad * 2 < 0x7FFFFFF0LL) {
+        const unsigned g = (unsigned)(nwg < (long long)num_cus() ? nwg : (long long)num_cus());
+        if (var == 3)
+          hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, true>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+        else
+          hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, false>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+        return (int)hipGetLastError();
+      }
+    }
+    if (var == 1 || var == 2 || var == 3) {
+      hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN, BM, 1>), grid, dim3(512), 0, s, a, tiles_n);
+      return (int)hipGetLastError();
+    }
+    if constexpr (DT == DT_BF16 && EPI == CONV_E_BF16) {
+      if (var == 8 || var == 9) {
+        if (var == 8)
+          hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN, BM, 8>), grid, dim3(512), 0, s, a, tiles_n);
+        else
+          hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN, BM, 9>), grid, dim3(512), 0, s, a, tiles_n);
+        return (int)hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN, BM, 0>), grid, dim3(512), 0, s, a, tiles_n);
     return (int)hipGetLastError();
   }
 }
@@ -980,14 +1406,6 @@ static int kw3_split(const ConvArgs& a, hipStream_t s, long long cus) {
 // 256x128 / 128x256 workgroups (0.53-0.72 vs 0.99-1.28 PF/s: 1.5x the staged bytes per FLOP), and
 // the in-workgroup K split (two wave groups per C tile, partial sums through LDS: the 256x128 /
 // 512x64 tiles are bound by the A-operand DMA stream, not by LDS fragment reads).
-static int num_cus() {
-  static int n = [] {
-    int dev = 0, cu = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cu = 256;
-    return cu > 0 ? cu : 256;
-  }();
-  return n;
-}
 
 // Tuning override (tools/tune_dma.py): force tile config `g_cfg` (> 0) and split-K factor
 // `g_ks` (> 0) for every DMA conv launch until reset to 0. Host-side globals, set between launches.

@@ -313,6 +313,16 @@ class DeepDream:
         return torch.cat(outs)
 
     def _run_one(self, x: torch.Tensor) -> torch.Tensor:
+        img = x
+        for img in self.octave_steps(x):
+            pass
+        return img
+
+    def octave_steps(self, x: torch.Tensor):
+        """Generator form of one (sub-)batch's dream: yields the image after each octave (its GPU
+        work enqueued, not necessarily finished). The multi-rank service drives a dream octave by
+        octave through this, polling each octave's completion under its failure deadlines and
+        letting other commands run between octaves (parallel/sharded.py)."""
         shapes = self.octave_shapes(x.shape[1], x.shape[2])
         original = x
         shrunk = resize(original, shapes[0])
@@ -324,7 +334,7 @@ class DeepDream:
             same = resize(original, hw)
             img = img + (same - upscaled)
             shrunk = resize(original, hw)
-        return img
+            yield img
 
     def dream_u8(self, img_u8: torch.Tensor) -> torch.Tensor:
         """uint8 RGB [B, H, W, 3] -> uint8 dreamed image."""
@@ -372,6 +382,12 @@ class TiledDeepDream(DeepDream):
         self.tile_graphs = use_graphs and self.device.type == "cuda"
         self._tgraphs: "OrderedDict[tuple, object]" = OrderedDict()
         self.tile_fused = FUSED_STEP and self.device.type == "cuda"
+        # coll_wait(work): how an EAGER collective of the tiled step is waited for. None: a blocking
+        # call. The multi-rank service sets a poll under its heartbeat / re-form deadlines
+        # (ShardedRunner._await), so a peer that dies mid-dream surfaces as PeerLost instead of a
+        # collective that never returns. (Collectives captured inside an octave graph are covered by
+        # polling the octave's completion event instead.)
+        self.coll_wait = None
 
     @staticmethod
     def _axis_tiles(L: int, tile: int):
@@ -528,14 +544,24 @@ class TiledDeepDream(DeepDream):
             return True
         return TILE_COLLECTIVE and self.info is not None and self.info.backend != "none"
 
-    def _tile_steps(self, st) -> None:
+    def _coll(self, fn, *args) -> None:
+        """An eager collective: blocking, or issued async and handed to ``coll_wait``."""
+        if self.coll_wait is None:
+            fn(*args)
+        else:
+            self.coll_wait(fn(*args, async_op=True))
+
+    def _tile_steps(self, st, capturing: bool = False) -> None:
         import torch.distributed as dist
 
         coll = self._collective(st)
         for it in range(self.s.iterations):
             self._tile_compute(st, it)
             if coll:
-                dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
+                if capturing:  # recorded into the octave graph: nothing to wait for here
+                    dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
+                else:
+                    self._coll(dist.all_gather_into_tensor, st.packs.view(-1), st.pack)
             self._tile_apply(st, it)
 
     def _stage_shifts(self, st) -> None:
@@ -584,12 +610,12 @@ class TiledDeepDream(DeepDream):
                     work = dist.all_gather_into_tensor(st.packs.view(-1), st.pack, async_op=True)
             torch.cuda.current_stream(self.device).wait_stream(s)
             if coll:  # retire the eager warm-up collective before the capture opens
-                drain_collective(work, self.device)
+                drain_collective(work, self.device, self.coll_wait)
             if not coll or CAPTURE_COLLECTIVE:
                 # the whole octave, all-gathers included (RCCL collectives are graph-capturable):
                 # one replay per octave instead of `iterations` replays + eager collectives
                 try:
-                    st.graph = self._capture(lambda: self._tile_steps(st))
+                    st.graph = self._capture(lambda: self._tile_steps(st, capturing=True))
                 except RuntimeError as e:  # capture of the collective refused: per-step graphs
                     if not coll:
                         raise
@@ -603,7 +629,7 @@ class TiledDeepDream(DeepDream):
         elif st.step_graph is not None:
             for it in range(self.s.iterations):
                 st.step_graph[it].replay()
-                dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
+                self._coll(dist.all_gather_into_tensor, st.packs.view(-1), st.pack)
                 self._tile_apply(st, it)
         else:
             self._tile_steps(st)
@@ -679,8 +705,8 @@ class TiledDeepDream(DeepDream):
                 shift.copy_(shifts[it])
                 self._tile_grad(x, shift, plan, grad, loss)
             if world > 1:
-                dist.all_reduce(grad)
-                dist.all_reduce(loss)
+                self._coll(dist.all_reduce, grad)
+                self._coll(dist.all_reduce, loss)
             g = grad / grad.abs().mean(dim=(1, 2, 3), keepdim=True).clamp_min(1e-7)
             if self.s.max_loss is not None:
                 done |= loss > self.s.max_loss * ntiles

@@ -36,6 +36,16 @@ rank 0 rebuild the group over the survivors (renumbered, new store prefix), and 
 commands ran on the old group is recomputed on the new world. A local error on rank 0 (bad input,
 kernel check) fails only that batch; it never degrades the group.
 
+``/deepdream`` across ranks runs as one ``dream`` command (broadcast of the images, every rank
+builds its octave generator) followed by one ``dream_oct`` command per octave. Each octave's work
+(its per-step pack all-gathers included, eager or captured in the octave graph) is polled to
+completion under the same deadlines as a collective: rank 0 checks the followers' heartbeats, a
+follower checks for a re-form announcement; eager collectives inside the tiled step are polled
+one by one (``TiledDeepDream.coll_wait``). A peer lost mid-dream re-forms the group and the dream
+restarts on the survivors (same seed: same rolls, same result up to rounding). The command lock is
+a FIFO lock released between octaves, so deconv batches (``POST /``) interleave with a long dream
+instead of waiting for all of it.
+
 What stays uncovered: a follower that hangs inside a kernel while still heartbeating (its thread
 keeps beating) is only caught by the collective deadline (``ack_timeout``), not by staleness.
 """
@@ -58,6 +68,65 @@ from .dist import DistInfo, shard_sizes
 from .elastic import Control, PeerLost
 
 log = get_logger("deconv_api_amd.sharded")
+
+
+class FairLock:
+    """Reentrant lock granted in arrival order (tickets). ``threading.RLock`` lets a thread that
+    releases and re-acquires in a loop (the dream, once per octave) starve a waiting one (the deconv
+    worker); here the waiter that arrived first gets the lock next."""
+
+    def __init__(self):
+        self._cv = threading.Condition(threading.Lock())
+        self._owner: Optional[int] = None
+        self._count = 0
+        self._next = 0
+        self._serving = 0
+
+    def acquire(self) -> bool:
+        me = threading.get_ident()
+        with self._cv:
+            if self._owner == me:
+                self._count += 1
+                return True
+            ticket = self._next
+            self._next += 1
+            while self._serving != ticket or self._owner is not None:
+                self._cv.wait()
+            self._owner, self._count = me, 1
+            return True
+
+    def release(self) -> None:
+        with self._cv:
+            if self._owner != threading.get_ident():
+                raise RuntimeError("FairLock released by a thread that does not hold it")
+            self._count -= 1
+            if self._count == 0:
+                self._owner = None
+                self._serving += 1
+                self._cv.notify_all()
+
+    def __enter__(self):
+        return self.acquire()
+
+    def __exit__(self, *exc):
+        self.release()
+
+
+class _EventWork:
+    """A recorded GPU event polled like an async collective's work object (``_await``)."""
+
+    def __init__(self, ev: torch.cuda.Event):
+        self.ev = ev
+
+    def is_completed(self) -> bool:
+        return self.ev.query()
+
+    def wait(self) -> None:
+        self.ev.synchronize()
+
+
+class _DreamRestart(Exception):
+    """The group was re-formed while a dream was between octaves: restart it on the new group."""
 
 
 @dataclass
@@ -84,8 +153,12 @@ class ShardedRunner:
         self.engine = engine
         self.cfg = cfg
         # one command (its store keys and collectives) at a time: the deconv worker and the
-        # /deepdream worker both drive the group
-        self._cmd_lock = threading.RLock()
+        # /deepdream worker both drive the group (FIFO: a dream releases it between octaves)
+        self._cmd_lock = FairLock()
+        self._did = 0  # dream ids
+        self._dreams: Dict[int, tuple] = {}  # follower: dream id -> (octave generator, octaves)
+        self.dream_restarts = 0
+        self._oct_count = 0  # dream octaves run by this process (fault injection)
         self._dream_tiled: Dict[tuple, object] = {}
         self._dream_nets: Dict[str, object] = {}
         self.info = info
@@ -264,6 +337,7 @@ class ShardedRunner:
 
     def _after_reform(self) -> None:
         self.slots = [None, None]
+        self._dreams.clear()
         for dd in self._dream_tiled.values():  # unit plans / packs / graphs were for the old world
             dd._tgraphs.clear()
             dd._plans.clear()
@@ -278,37 +352,87 @@ class ShardedRunner:
 
     def _dream_local(self, dd, x_u8: torch.Tensor, seed: int) -> torch.Tensor:
         dd.gen.manual_seed(seed)  # identical rolls on every rank
+        dd.coll_wait = None
         return dd.dream_u8(x_u8)
+
+    def _dream_octaves(self, dd, x_u8: torch.Tensor, seed: int, follower: bool):
+        """This rank's dream, one octave per ``next``: every eager collective of the tiled step is
+        polled under the failure deadlines; yields each octave's (enqueued) image."""
+        from ..engine.deepdream import inception_preprocess
+
+        dd.gen.manual_seed(seed)  # identical rolls on every rank
+        dd.coll_wait = lambda w: self._await(w, "dream collective", follower)
+        yield from dd.octave_steps(inception_preprocess(x_u8))
+
+    def _octave(self, run, follower: bool) -> torch.Tensor:
+        """Advance a dream by one octave and poll its completion (GPU: an event recorded behind the
+        octave's work, which holds its captured all-gathers) under the deadlines."""
+        self._oct_count += 1
+        img = next(run)
+        if img.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._await(_EventWork(ev), "dream octave", follower)
+        return img
 
     def dream(self, imgs: torch.Tensor, model: str, octaves: int, steps: int) -> np.ndarray:
         """rank 0: DeepDream of u8 [n, H, W, 3] tiled across every rank -> u8 [n, H, W, 3]. The
         images are broadcast (RCCL); each rank runs its share of the (tile, image) units and the
-        per-step pack all-gathers inside the tiled engine assemble every step on every rank."""
+        per-step pack all-gathers inside the tiled engine assemble every step on every rank. One
+        command per octave; the command lock is released between octaves. A peer lost at any point
+        re-forms the group and restarts the dream on the survivors."""
         assert self.info.rank == 0
         seed = (self.cfg.seed if self.cfg is not None else 0)
-        with self._cmd_lock:
-            while True:
-                if self.world == 1:
-                    dd = self._dream_engine(model, octaves, steps)
-                    return self._dream_local(dd, imgs.to(self.info.device), seed).cpu().numpy()
-                try:
-                    return self._dream_cmd(imgs, model, octaves, steps, seed)
-                except PeerLost as e:
-                    self._reform(e)
+        while True:
+            if self.world == 1:
+                with self._cmd_lock:
+                    if self.world == 1:
+                        dd = self._dream_engine(model, octaves, steps)
+                        return self._dream_local(dd, imgs.to(self.info.device), seed).cpu().numpy()
+                continue
+            try:
+                return self._dream_cmds(imgs, model, octaves, steps, seed)
+            except _DreamRestart:
+                self.dream_restarts += 1
 
-    def _dream_cmd(self, imgs: torch.Tensor, model: str, octaves: int, steps: int, seed: int) -> np.ndarray:
+    def _dream_cmds(self, imgs: torch.Tensor, model: str, octaves: int, steps: int, seed: int) -> np.ndarray:
+        from ..engine.deepdream import inception_deprocess
+
         ctl = self.ctl
         n, H, W, _ = imgs.shape
-        seq = ctl.post_cmd({"op": "dream", "model": model, "octaves": octaves, "steps": steps, "n": n, "H": H,
-                            "W": W, "seed": seed})
-        dd = self._dream_engine(model, octaves, steps)  # overlaps the followers' acks
-        x = imgs.to(self.info.device).contiguous()
-        ctl.wait_acks("ready", seq)
-        ctl.go("go1", seq)
-        self._await(dist.broadcast(x, src=0, async_op=True), "broadcast")
-        out = self._dream_local(dd, x, seed)
-        ctl.wait_acks("done", seq)
-        return out.cpu().numpy()
+        with self._cmd_lock:
+            if self.world == 1:
+                raise _DreamRestart()
+            epoch = ctl.epoch
+            did = self._did
+            self._did += 1
+            try:
+                seq = ctl.post_cmd({"op": "dream", "did": did, "model": model, "octaves": octaves, "steps": steps,
+                                    "n": n, "H": H, "W": W, "seed": seed})
+                dd = self._dream_engine(model, octaves, steps)  # overlaps the followers' acks
+                x = imgs.to(self.info.device).contiguous()
+                ctl.wait_acks("ready", seq)
+                ctl.go("go1", seq)
+                self._await(dist.broadcast(x, src=0, async_op=True), "broadcast")
+                run = self._dream_octaves(dd, x, seed, follower=False)
+            except PeerLost as e:
+                self._reform(e)
+                raise _DreamRestart() from e
+        img = None
+        for o in range(octaves):
+            with self._cmd_lock:  # released between octaves: deconv batches interleave
+                if ctl.epoch != epoch:  # another command re-formed the group meanwhile
+                    raise _DreamRestart()
+                try:
+                    seq = ctl.post_cmd({"op": "dream_oct", "did": did, "o": o})
+                    ctl.wait_acks("ready", seq)
+                    ctl.go("go1", seq)
+                    img = self._octave(run, follower=False)
+                    ctl.wait_acks("done", seq)
+                except PeerLost as e:
+                    self._reform(e)
+                    raise _DreamRestart() from e
+        return inception_deprocess(img).cpu().numpy()
 
     def _run_cmd(self, b: Batch) -> None:
         n = len(b.images)
@@ -420,10 +544,18 @@ class ShardedRunner:
                     x = torch.empty(msg["n"], msg["H"], msg["W"], 3, dtype=torch.uint8, device=dev)
                     self._await(dist.broadcast(x, src=0, async_op=True), "broadcast", True)
                     dd = self._dream_engine(msg["model"], msg["octaves"], msg["steps"])
-                    out = self._dream_local(dd, x, msg["seed"])
-                    if out.is_cuda:
-                        torch.cuda.current_stream(dev).synchronize()
+                    self._dreams.clear()  # one dream at a time (a restarted one replaces it)
+                    self._dreams[msg["did"]] = (self._dream_octaves(dd, x, msg["seed"], True), msg["octaves"])
+                    continue
+                if op == "dream_oct":
+                    run, octaves = self._dreams[msg["did"]]
+                    ctl.ack("ready", seq)
+                    self._go(ctl, "go1", seq)
+                    self.faults.at("octave", self._oct_count + 1)  # fault window: inside a dream
+                    self._octave(run, follower=True)
                     ctl.ack("done", seq)
+                    if msg["o"] + 1 == octaves:
+                        del self._dreams[msg["did"]]
                     continue
                 if op == "gather":
                     mos, ev = pending.pop(msg["b"])

@@ -31,11 +31,14 @@ def capture(fn: Callable[[], object], graph: Optional[torch.cuda.CUDAGraph] = No
     return g, out
 
 
-def drain_collective(work, device) -> None:
-    """Retire an eager (async_op=True) collective before a capture: wait for its work object on
-    the current stream, then synchronize the device so its end event has completed before the
-    capture opens (the watchdog may still hold the work; with thread-local capture its poll is
-    legal either way, and a completed event makes the poll trivially succeed)."""
+def drain_collective(work, device, wait=None) -> None:
+    """Retire an eager (async_op=True) collective before a capture: wait for its work object
+    (``wait(work)`` when given: the caller's polled wait under its failure deadlines), then
+    synchronize the device so its end event has completed before the capture opens (the watchdog
+    may still hold the work; with thread-local capture its poll is legal either way, and a
+    completed event makes the poll trivially succeed)."""
     if work is not None:
+        if wait is not None:
+            wait(work)
         work.wait()
     torch.cuda.synchronize(device)

@@ -7,6 +7,8 @@
   exit_ready@2   terminates right after acknowledging its 2nd batch, before entering the scatter
   exit_done@2    terminates right after acknowledging that its 2nd batch is computed, before the
                  gather (the two windows the ack protocol alone cannot close, parallel/sharded.py)
+  exit_octave@2  terminates when released into its 2nd DeepDream octave (the other ranks are
+                 then inside that octave's collectives)
 Batches are counted per process from 1.
 """
 from __future__ import annotations
@@ -41,7 +43,7 @@ def parse(spec: str) -> List[Fault]:
         if ":" in rest:
             rest, a = rest.split(":")
             arg = float(a)
-        if action not in ("raise", "hang", "exit", "exit_ready", "exit_done"):
+        if action not in ("raise", "hang", "exit", "exit_ready", "exit_done", "exit_octave"):
             raise ValueError(f"unknown fault action {action!r}")
         out.append(Fault(action, int(rest), arg, rank))
     return out

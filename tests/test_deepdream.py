@@ -587,7 +587,7 @@ def test_gpu_capture_while_other_thread_polls_events(native_lib):
 
     inc = InceptionV3(0).build("cuda")
     res = ResNet50(0).build("cuda", torch.float16)
-    xi = (torch.rand(2, 120, 120, 3, generator=torch.Generator().manual_seed(21)) * 2 - 1).cuda()
+    xi = (torch.rand(2, 150, 150, 3, generator=torch.Generator().manual_seed(21)) * 2 - 1).cuda()
     xr = (torch.rand(2, 200, 260, 3, generator=torch.Generator().manual_seed(22)) * 2 - 1).cuda()
     si = DreamSettings(iterations=3, octaves=2, max_loss=None)
     sr = DreamSettings(layers=dict(RESNET_LAYERS), octaves=2, iterations=3, max_loss=None)

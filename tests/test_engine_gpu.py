@@ -42,10 +42,13 @@ def _compare(model, B, hw, layers, seed=0):
             for k in range(4):
                 if idx[b, k] < 0:
                     continue
-                c = _cos(rg[b, k], rc[b, k])
-                cs.append(c)
-                assert c > 0.98, (layer, b, k, c)
-        print(f"loose-cos {hw} {layer} min {min(cs):.5f} median {sorted(cs)[len(cs) // 2]:.5f}")
+                cs.append(_cos(rg[b, k], rc[b, k]))
+        # two independent forwards (bf16 GPU vs fp32 CPU): near-tied switches may flip, so a floor per
+        # reconstruction plus a tighter median (measured round 4: min 0.988 / median >= 0.993 on the
+        # scaled net, min 0.992 / median 0.993 at 224^2)
+        med = sorted(cs)[len(cs) // 2]
+        print(f"loose-cos {hw} {layer} min {min(cs):.5f} median {med:.5f}")
+        assert min(cs) > 0.985 and med > 0.99, (layer, min(cs), med)
 
 
 def test_engine_small_all_targets(native_lib, small_specs):

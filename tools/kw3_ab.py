@@ -1,0 +1,88 @@
+"""A/B of the KW3 conv main-loop variants (csrc/conv_dma_impl.h, conv_dma_kw3_kernel VAR) on the
+config-2 launch shapes, interleaved in ONE process (cdna_hip_programming.md §5.4 rule 24).
+
+    python tools/kw3_ab.py --vars 0,1,2,8,9 --rounds 5 --reps 20
+
+VAR 0 / 1 / 2 (persistent KW3P) are real kernels (their outputs are compared bit for bit: the
+accumulation order is the same); 8 (no epilogue stores) and 9 (no K loop) are ablations that price the epilogue and the
+prologue + epilogue of a tile. Prints one JSON line per (case, variant) with the median and min
+time over rounds and the conv TF/s.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from deconv_api_amd import ops  # noqa: E402
+from deconv_api_amd.ops.conv import ConvWeights  # noqa: E402
+
+# config-2 KW3 launches (VGG16 block5_conv3 deconvnet, B = 256 images x K = 4 signals): name ->
+# (N, H, W, C, OC)
+CASES = {
+    "b5down": (1024, 14, 14, 512, 512),     # block5_conv{2,3}.down (x2 per step) and conv1.down (unpool-out)
+    "b4down": (1024, 28, 28, 512, 512),     # block4_conv{2,3}.down
+    "b4c1down": (1024, 28, 28, 512, 256),   # block4_conv1.down: 512 -> 256
+    "b3down": (1024, 56, 56, 256, 256),     # block3_conv{2,3}.down
+    "b3c1down": (1024, 56, 56, 256, 128),   # block3_conv1.down: 512 x 128 KW3 tile
+    "b4fwd": (256, 28, 28, 512, 512),       # block4_conv{2,3} forward
+    "b5fwd": (256, 14, 14, 512, 512),       # block5 forward (tail-split KW3)
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--vars", default="0,1,2,8,9")
+    ap.add_argument("--cases", default=",".join(CASES))
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    ops.native.load()
+    dev = torch.device("cuda", 0)
+    variants = [int(v) for v in a.vars.split(",")]
+    g = torch.Generator(device=dev).manual_seed(0)
+    for case in a.cases.split(","):
+        N, H, W, C, OC = CASES[case]
+        w = torch.randn(OC, C, 3, 3) / (3 * C ** 0.5)
+        cw = ConvWeights(w, None, "fwd").to_device(dev)
+        x = (torch.rand(N, H, W, C, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+        out = {v: torch.empty(N, H, W, OC, dtype=torch.bfloat16, device=dev) for v in variants}
+
+        def run(v):
+            os.environ["DV_KW3_VAR"] = str(v)
+            return ops.conv2d(x, cw, relu=True, use_bias=False, out=out[v])
+
+        for v in variants:  # warm up every variant (and check the real ones agree)
+            run(v)
+        torch.cuda.synchronize()
+        real = [v for v in variants if v < 8]
+        for v in real[1:]:
+            same = torch.equal(out[v], out[real[0]])
+            if not same:
+                d = (out[v].float() - out[real[0]].float()).abs().max().item()
+                print(json.dumps({"case": case, "var": v, "equal_to": real[0], "equal": False, "maxdiff": d}),
+                      flush=True)
+        times = {v: [] for v in variants}
+        for _ in range(a.rounds):
+            for v in variants:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.reps):
+                    run(v)
+                e1.record()
+                e1.synchronize()
+                times[v].append(e0.elapsed_time(e1) / a.reps)
+        fl = 2.0 * N * H * W * OC * 9 * C
+        for v in variants:
+            med = statistics.median(times[v])
+            print(json.dumps({"case": case, "var": v, "ms_median": round(med, 4), "ms_min": round(min(times[v]), 4),
+                              "tflops": round(fl / med / 1e9, 1)}), flush=True)
+    os.environ.pop("DV_KW3_VAR", None)
+
+
+if __name__ == "__main__":
+    main()
