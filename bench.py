@@ -69,6 +69,10 @@ def parse(argv=None):
     ap.add_argument("--breakdown", action="store_true", help="per-phase timing to stderr (extra syncs)")
     ap.add_argument("--no-copyback", action="store_true",
                     help="DIAGNOSTIC ONLY (not a benchmark number): skip the mosaics' copy to the host, to price it")
+    ap.add_argument("--emulate-gather-world", type=int, default=0,
+                    help="DIAGNOSTIC ONLY (not a benchmark number): every step also copies (N-1) x the step's "
+                         "mosaics device-to-device on a side stream, overlapping the next step, i.e. the HBM "
+                         "writes and CU time an N-rank all-gather of the mosaics costs each rank")
     ap.add_argument("--profile", nargs="?", const="trace", default=None, choices=["trace", "pmc"],
                     help="re-run under rocprofv3 and print a per-kernel table (trace) [+ PMC pass]")
     return ap.parse_args(argv)
@@ -237,12 +241,29 @@ def main(argv=None):
         if ev0 is not None:
             lat.append((ev0, back_done[slot]))
 
+    emu_n = max(0, args.emulate_gather_world - 1)
+    emu_stream = torch.cuda.Stream(dev) if (cuda and emu_n) else None
+    emu_dst = torch.empty(emu_n * B, 2 * S, 2 * S, 3, dtype=torch.uint8, device=dev) if emu_stream else None
+
+    def emulate_gather(mosaic):
+        """(N-1) mosaic-sized D2D copies on a side stream behind this step (what an N-rank all-gather
+        writes into each rank's HBM, and the copy kernels' CUs), overlapping the next step."""
+        ready = torch.cuda.Event()
+        ready.record()
+        emu_stream.wait_event(ready)
+        mosaic.record_stream(emu_stream)
+        with torch.cuda.stream(emu_stream):
+            for r in range(emu_n):
+                emu_dst[r * B:(r + 1) * B].copy_(mosaic)
+
     def step(i, ev0=None):
         ops.resize_preprocess(images, xbuf)
         hook = (COPY_AT, issue_copy) if cuda and COPY_AT else None
         res = eng.run(xbuf, args.layer, k=args.k, hook=hook)
         if cuda:
             issue_copy()  # no-op when the hook already issued step i-1's copy
+        if emu_stream is not None:
+            emulate_gather(res.mosaic)
         slot = i % 2
         if info.backend != "none" and not (JPEG and cuda):
             if pending[slot] is not None:
@@ -309,6 +330,8 @@ def main(argv=None):
     drain()
     if cuda:
         copy_stream.synchronize()
+    if emu_stream is not None:
+        emu_stream.synchronize()
     sync()
     pdist.barrier(info)
     sync()
@@ -352,6 +375,9 @@ def main(argv=None):
         line["data"] = "REHEARSAL: scaled VGG16 (width/8, 32px) on CPU - not a benchmark"
     if args.no_copyback:
         line["data"] = "DIAGNOSTIC: mosaics not copied back to the host - not a benchmark"
+    if emu_n:
+        line["data"] = f"DIAGNOSTIC: + {emu_n} mosaic-sized D2D copies per step (emulated {emu_n + 1}-rank all-gather)"
+        line["emulated_gather_bytes_per_step"] = int(emu_dst.numel())
     if info.is_main:
         print(json.dumps(line), flush=True)
     pdist.shutdown()

@@ -37,7 +37,13 @@ def main(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
                     help="16-bit storage / MFMA dtype (BASELINE config 5 is quoted in fp16)")
+    ap.add_argument("--virtual-world", type=int, default=0,
+                    help="tiled only: time ONE rank's share of a W-rank dream on this GPU (no collective; "
+                         "readiness sizing for config 5, not a dream result)")
+    ap.add_argument("--virtual-rank", type=int, default=0)
     a = ap.parse_args(argv)
+    if a.virtual_world:
+        return virtual_rank(a)
 
     info = pdist.init()
     dev = info.device
@@ -90,6 +96,64 @@ def main(argv=None):
                        "parallelism": f"{'tiles' if a.tile else 'dp'}{info.world}"},
         }), flush=True)
     pdist.shutdown()
+
+
+def virtual_rank(a) -> dict:
+    """Per-rank step time of a W-rank tiled dream, measured on one GPU: rank r's plan (its
+    (tile, image) units dealt round-robin, its pack slot, tile_update over W packs) runs every
+    octave without the all-gather. Prints per octave: units on this rank, ms per gradient step,
+    and the bytes one step's pack all-gather moves into every rank (W x pack)."""
+    from types import SimpleNamespace
+
+    dev = torch.device("cuda", 0)
+    ops.native.load()
+    dt = torch.float16 if a.dtype == "fp16" else torch.bfloat16
+    assert a.tile, "--virtual-world needs --tile"
+    if a.model == "inception_v3":
+        from deconv_api_amd.models.inception_v3 import InceptionV3
+
+        net = InceptionV3(0).build(dev, dt)
+        s = DreamSettings(octaves=a.octaves, iterations=a.steps)
+    else:
+        from deconv_api_amd.models.resnet50 import ResNet50
+
+        net = ResNet50(0).build(dev, dt)
+        s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=a.octaves, iterations=a.steps)
+    info = SimpleNamespace(world=a.virtual_world, rank=a.virtual_rank, backend="none", device=dev)
+    dd = TiledDeepDream(net, s, tile=a.tile, info=info, use_graphs=not a.no_graphs)
+    dd.virtual = True
+    g = torch.Generator(device=dev).manual_seed(7)
+    img = torch.randint(0, 256, (a.batch, a.size, a.size, 3), dtype=torch.uint8, device=dev, generator=g)
+    x = inception_preprocess(img)
+    for _ in range(a.warmup):
+        for _o in dd.octave_steps(x):
+            pass
+    torch.cuda.synchronize()
+    per_oct = {}
+    for _ in range(a.runs):
+        evs = [torch.cuda.Event(enable_timing=True)]
+        evs[0].record()
+        for _o in dd.octave_steps(x):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            evs.append(e)
+        torch.cuda.synchronize()
+        for i in range(len(evs) - 1):
+            per_oct.setdefault(i, []).append(evs[i].elapsed_time(evs[i + 1]))
+    shapes = dd.octave_shapes(a.size, a.size)
+    rows = []
+    for i, hw in enumerate(shapes):
+        st = dd._tgraphs[(a.batch, hw[0], hw[1])]
+        ms = sorted(per_oct[i])[len(per_oct[i]) // 2]
+        rows.append({"octave": list(hw), "tiles": st.ntiles, "units_this_rank": st.mine, "units_all": st.plan.shape[0],
+                     "ms_per_step": round(ms / a.steps, 3), "ms_octave": round(ms, 2),
+                     "allgather_bytes_per_step": int(st.packs.numel() * st.packs.element_size())})
+    out = {"virtual_world": a.virtual_world, "virtual_rank": a.virtual_rank, "model": a.model, "batch": a.batch,
+           "size": a.size, "tile": a.tile, "dtype": a.dtype, "octaves": rows,
+           "ms_per_dream_batch_compute": round(sum(r["ms_octave"] for r in rows), 1),
+           "note": "one rank's share, no collective: compute-only lower bound of a W-rank dream batch"}
+    print(json.dumps(out), flush=True)
+    return out
 
 
 def _tile_info(dd) -> dict:

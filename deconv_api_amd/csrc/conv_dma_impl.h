@@ -750,7 +750,7 @@ __device__ __forceinline__ int kw3_swz(int row) { return ((row >> 2) & 1) << 1; 
 // staged A slots per workgroup: 8 waves x 16 x A_I >= BM + 2 + 8 x (row boundaries), host-checked
 constexpr int kw3_a_i(int bm) { return bm == 256 ? 4 : 5; }
 constexpr int kKw3Pad = 8;  // zero slots between image rows: a row jump is +9 slots = +1 (mod 8)
-constexpr int kKw3DefaultVar = 0;
+constexpr int kKw3DefaultVar = 2;
 }  // namespace
 
 // BM_ x BN_: 256 x 256 (8 waves of 128 x 64) or 512 x 128 (8 waves of 128 x 64: the same per-wave
@@ -761,12 +761,9 @@ constexpr int kKw3DefaultVar = 0;
 // 6.85-7.03k to 5.80-5.83k img/s, profiles/bench_c2_r3_ab.txt. Equal within noise and removed:
 // static priority for waves 4-7 instead of the per-sub-step flips, a 320-row M tile, and the DMAs
 // issued behind the first sub-step's fragment reads, profiles/kw3_variants_r3.txt.)
-// VAR (kw3_var(), DV_KW3_VAR): 0 = one read burst + 32 MFMAs per kw sub-step; 1 = fragment
-// pipeline: the next sub-step's B fragments are read into a second register set at the start of a
-// sub-step and each A fragment register is refilled with the next sub-step's fragment right after
-// its 4 MFMAs, so only the first sub-step of a K step waits for LDS reads; the next step's DMAs are
-// issued behind the first sub-step's reads. 8 / 9: ablations for tools/kw3_ab.py only (no
-// epilogue stores / no K loop): NOT correct outputs.
+// VAR (kw3_var(), DV_KW3_VAR): 0 = this kernel; 2 (default) = the persistent KW3P kernel below for
+// plain epilogues (this kernel otherwise); 8 / 9: ablations for tools/kw3_ab.py only (no epilogue
+// stores / no K loop): NOT correct outputs.
 template <int DT, int EPI, int BN_ = 256, int BM_ = 256, int VAR = 0>
 __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int tiles_n) {
   constexpr int BN = BN_, BM = BM_, NW = 8;
@@ -878,52 +875,6 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
     __builtin_amdgcn_s_barrier();
     const int aoff = (k & 1) * A_BYTES;
     const uint8_t* Bs = smem + baddr[k & 1];
-    if constexpr (VAR == 1) {
-      v8 bA[FN], bB[FN], af[FM];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + j * 1024);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(smem + aoff + aaddr[i][0]);
-      if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
-      // kw = 0 (bA) while kw = 1 is read: B into bB up front, A into each af[i] after its MFMAs
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bB[j] = *reinterpret_cast<const v8*>(Bs + BN * 64 + j * 1024);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
-        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aaddr[i][1]);
-      }
-      // kw = 1 (bB) while kw = 2 is read into bA / af
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + 2 * BN * 64 + j * 1024);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bB[j], acc[i][j]);
-        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aaddr[i][2]);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
-      // pin that order (one pipeline, SyncID 0): hipcc otherwise sinks each prefetch down to its
-      // use and waits lgkmcnt(0) right after it
-      __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, FM * FN, 0);
-      continue;
-    }
     if (k + 1 < nsteps) issue(k + 1, (k + 1) & 1);
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
@@ -982,9 +933,16 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
 //     offset, discarded);
 //   * those stores drain while tile t + 1's first K step computes (the wait at the end of that step
 //     is the first one that covers them).
-// Main loop: the VAR 1 fragment pipeline. Numerics equal the LDS-staged epilogue (same fp32 ops,
-// same rounding). Buffer parity follows a global step counter (odd step counts per tile).
-template <int DT, int BN_ = 256, int BM_ = 256, bool IL = false>
+// Main loop: a fragment pipeline (the next kw sub-step's B fragments read into a second register
+// set, each A fragment register refilled with the next sub-step's fragment right after its 4
+// MFMAs; the order pinned by sched_group_barrier), so only a K step's first sub-step waits for LDS
+// reads. Numerics equal the LDS-staged epilogue (same fp32 ops, same rounding). Buffer parity
+// follows a global step counter (odd step counts per tile).
+// Measured (tools/kw3_ab.py, profiles/kw3_ab_r4.txt): 2-4 % faster per launch than KW3 on every
+// config-2 shape. Measured and removed: the fragment pipeline alone in the non-persistent kernel
+// (-2 % .. +2 %, noise) and the next step's DMA pieces issued one per MFMA group instead of all
+// after the first reads (-3 % .. +3 % vs this kernel, shape-dependent).
+template <int DT, int BN_ = 256, int BM_ = 256>
 __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, int tiles_n, int ntiles) {
   constexpr int BN = BN_, BM = BM_, NW = 8;
   constexpr int WN = BN / 64, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
@@ -1067,27 +1025,6 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
     }
   };
 
-  // IL: one DMA piece of step (kh, cc) into stage buf, branch-free (a piece that must not load
-  // reads out of range: zeros into a slot nobody reads), so it can sit between MFMA groups.
-  // Pieces 0 .. A_I - 1: A slot groups; A_I .. A_I + B_I - 1: B row groups.
-  auto piece = [&](int p, int kh, int cc, int buf, bool none) {
-    if (p < A_I) {
-      const int u = p;
-      const uint32_t po = r_po[u];
-      const int oh = (int)(po & 0xFFFu), pix = (int)(po >> 12);
-      const bool ok = !none && (u * NW + wave) * 16 < nslots && po != ~0u && (unsigned)(oh + kh - 1) < (unsigned)H;
-      const uint32_t off = (uint32_t)(((pix + (kh - 1) * W) * (int)a.x_ld + cc * 32 + lchunk * 8) * 2);
-      dma16(xr, smem + 2 * B_BYTES + buf * A_BYTES + (u * NW + wave) * 1024, ok ? off : kOOB);
-    } else {
-      const int vv = (p - A_I) * NW + wave;
-      const int kw = vv / (BN / 16), brow = (vv % (BN / 16)) * 16 + lrow;
-      const uint32_t off = (uint32_t)(((n0 + brow) * a.Kpad + (kh * 3 + kw) * C + cc * 32 + lchunk * 8) * 2);
-      dma16(wr, smem + buf * B_BYTES + vv * 1024, none ? kOOB : off);
-    }
-  };
-  constexpr int NP = A_I + B_I;  // DMA pieces per wave and K step
-  static_assert(NP <= 2 * FM, "the pieces ride in the first two kw sub-steps");
-
   int v = blockIdx.x;
   if (v >= ntiles) return;
   setup(v);
@@ -1168,76 +1105,15 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     };
-    // IL form of kstep: the NP DMA pieces of the next step are issued one per A-fragment group of
-    // the kw = 0 (and kw = 1) sub-step, between MFMA groups, instead of all at once after the first
-    // reads (both waves of a SIMD issued them together, with the matrix pipe idle meanwhile)
-    auto kstep_il = [&](int cur, int nkh, int ncc, bool none) {
-      const int aoff = cur * A_BYTES;
-      const uint8_t* Bs = smem + baddr0 + cur * B_BYTES;
-      v8 bA[FN], bB[FN], af[FM];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + j * 1024);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 0));
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bB[j] = *reinterpret_cast<const v8*>(Bs + BN * 64 + j * 1024);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
-        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 1));
-        if (i < NP) piece(i, nkh, ncc, cur ^ 1, none);
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bA[j] = *reinterpret_cast<const v8*>(Bs + 2 * BN * 64 + j * 1024);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bB[j], acc[i][j]);
-        af[i] = *reinterpret_cast<const v8*>(smem + aoff + aad(i, 2));
-        if (FM + i < NP) piece(FM + i, nkh, ncc, cur ^ 1, none);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32<DT>(af[i], bA[j], acc[i][j]);
-      __builtin_amdgcn_sched_group_barrier(0x100, FN + FM + FN, 0);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        if (i < NP) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        if (FM + i < NP) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, FM * FN, 0);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    };
-    if constexpr (IL) {
 #pragma unroll 1
-      for (int k = 0; k + 1 < nsteps; ++k, ++g) {
-        const int kh = (k + 1) / nch;
-        kstep_il(g & 1, kh, k + 1 - kh * nch, false);
-      }
-      if (more) setup(vnext);
-      kstep_il(g & 1, 0, 0, !more);
-    } else {
-#pragma unroll 1
-      for (int k = 0; k + 1 < nsteps; ++k, ++g) kstep(g & 1, [&] { issue(k + 1, (g & 1) ^ 1); });
-      // the last step issues the next tile's first step (gather state computed before its fragments
-      // are live): those operands land behind this step's MFMAs, its trailing wait covers them, and
-      // the epilogue's stores below are younger than them
-      if (more) setup(vnext);
-      kstep(g & 1, [&] {
-        if (more) issue(0, (g & 1) ^ 1);
-      });
-    }
+    for (int k = 0; k + 1 < nsteps; ++k, ++g) kstep(g & 1, [&] { issue(k + 1, (g & 1) ^ 1); });
+    // the last step issues the next tile's first step (gather state computed before its fragments
+    // are live): those operands land behind this step's MFMAs, its trailing wait covers them, and
+    // the epilogue's stores below are younger than them
+    if (more) setup(vnext);
+    kstep(g & 1, [&] {
+      if (more) issue(0, (g & 1) ^ 1);
+    });
     ++g;
     // ---- epilogue: register transpose -> 8-B stores (no LDS, no barrier) ----
     // lane roles (see the header; derived here, not kept live across the K loop): this lane stores
@@ -1330,23 +1206,13 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
     if constexpr (EPI == CONV_E_BF16) {
       // persistent KW3P: plain 16-bit epilogue only (its register-transpose stores write exactly
       // the C tile), output addressable by a 31-bit buffer offset, one workgroup per CU
-      // (IL, var 3: the pieces' 32-bit offset math needs the gather span and the weight matrix
-      // below 2^31 bytes)
-      if ((var == 2 || var == 3) && a.res == nullptr && a.emask == nullptr && !a.accumulate && a.ucode == nullptr &&
+      if (var == 2 && a.res == nullptr && a.emask == nullptr && !a.accumulate && a.ucode == nullptr &&
           a.out2 == nullptr && a.OC == a.OCpad && a.OC % 4 == 0 && a.out_ld % 4 == 0 &&
-          a.out_elems * 2 < 0x7FFFFFF0LL && a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19) &&
-          (2LL * a.H * a.W + BM) * a.x_ld * 2 < 0x7FFFFFF0LL && (long long)a.OCpad * a.Kpad * 2 < 0x7FFFFFF0LL) {
+          a.out_elems * 2 < 0x7FFFFFF0LL && a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19)) {
         const unsigned g = (unsigned)(nwg < (long long)num_cus() ? nwg : (long long)num_cus());
-        if (var == 3)
-          hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, true>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
-        else
-          hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, false>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+        hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
         return (int)hipGetLastError();
       }
-    }
-    if (var == 1 || var == 2 || var == 3) {
-      hipLaunchKernelGGL((conv_dma_kw3_kernel<DT, EPI, BN, BM, 1>), grid, dim3(512), 0, s, a, tiles_n);
-      return (int)hipGetLastError();
     }
     if constexpr (DT == DT_BF16 && EPI == CONV_E_BF16) {
       if (var == 8 || var == 9) {

@@ -539,7 +539,12 @@ class TiledDeepDream(DeepDream):
 
     def _collective(self, st) -> bool:
         """Whether the octave all-gathers the packs: several ranks, or DV_TILE_COLLECTIVE=1 with a
-        real 1-rank process group (the multi-rank code path, rehearsed on one GPU)."""
+        real 1-rank process group (the multi-rank code path, rehearsed on one GPU). ``virtual``
+        (bench_dream.py --virtual-world): this process times ONE rank's share of a W-rank octave
+        (its units, its pack, the update over W packs) without the collective; the result is not
+        a dream (the other ranks' packs stay zero)."""
+        if getattr(self, "virtual", False):
+            return False
         if st.world > 1:
             return True
         return TILE_COLLECTIVE and self.info is not None and self.info.backend != "none"

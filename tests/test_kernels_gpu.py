@@ -299,9 +299,8 @@ def test_conv_hs_unpool(native_lib, N, H, W, C, OC, div):
 @pytest.mark.parametrize("N,H,W,C,OC,dt", [(200, 28, 28, 32, 256, torch.bfloat16), (90, 14, 13, 96, 512, torch.bfloat16),
                                            (300, 20, 20, 64, 256, torch.float16), (120, 36, 36, 64, 128, torch.bfloat16)])
 def test_conv_kw3_persistent(native_lib, monkeypatch, N, H, W, C, OC, dt):
-    """Persistent KW3 (conv_dma_kw3p_kernel, DV_KW3_VAR=2, and =3 with the DMA pieces interleaved
-    between MFMA groups): several tiles per workgroup with a
-    partial last round, odd K-step counts (C = 32 / 96: the LDS stage parity runs across tiles),
+    """Persistent KW3 (conv_dma_kw3p_kernel, DV_KW3_VAR=2, the default): several tiles per workgroup
+    with a partial last round, odd K-step counts (C = 32 / 96: the LDS stage parity runs across tiles),
     image-row and image boundaries inside tiles, the 512 x 128 tile, a channel-slice output view;
     bias + ReLU and plain. Equal BIT FOR BIT to the LDS-staged KW3 epilogue (DV_KW3_VAR=0: same
     accumulation order, same rounding) and to the fp32 reference up to bf16 rounding."""
@@ -313,12 +312,12 @@ def test_conv_kw3_persistent(native_lib, monkeypatch, N, H, W, C, OC, dt):
     xd, cwd = x.to(DEV), cw.to_device(DEV, dt)
     for relu in (True, False):
         outs = {}
-        for var in ("0", "2", "3"):
+        for var in ("0", "2"):
             monkeypatch.setenv("DV_KW3_VAR", var)
             big = torch.full((N, H, W, OC + 8), 7.0, dtype=dt, device=DEV)
             outs[var] = ops.conv2d(xd, cwd, relu=relu, out=big[..., :OC])
             assert bool((big[..., OC:] == 7.0).all()), "wrote past the channel slice"
-        assert torch.equal(outs["0"], outs["2"]) and torch.equal(outs["0"], outs["3"]), relu
+        assert torch.equal(outs["0"], outs["2"]), relu
         ref = ops.conv2d(x[: min(N, 8)].float(), cw, relu=relu)
         assert _rel(outs["2"][: min(N, 8)], ref) < 1e-2
 

@@ -1,9 +1,9 @@
-"""A/B of the KW3 conv main-loop variants (csrc/conv_dma_impl.h, conv_dma_kw3_kernel VAR) on the
+"""A/B of the KW3 conv main-loop variants (csrc/conv_dma_impl.h, conv_dma_kw3_kernel / conv_dma_kw3p_kernel) on the
 config-2 launch shapes, interleaved in ONE process (cdna_hip_programming.md §5.4 rule 24).
 
-    python tools/kw3_ab.py --vars 0,1,2,8,9 --rounds 5 --reps 20
+    python tools/kw3_ab.py --vars 0,2,8,9 --rounds 5 --reps 20
 
-VAR 0 / 1 / 2 (persistent KW3P) are real kernels (their outputs are compared bit for bit: the
+VAR 0 (KW3) / 2 (persistent KW3P, the default) are real kernels (their outputs are compared bit for bit: the
 accumulation order is the same); 8 (no epilogue stores) and 9 (no K loop) are ablations that price the epilogue and the
 prologue + epilogue of a tile. Prints one JSON line per (case, variant) with the median and min
 time over rounds and the conv TF/s.
@@ -36,7 +36,7 @@ CASES = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--vars", default="0,1,2,8,9")
+    ap.add_argument("--vars", default="0,2,8,9")
     ap.add_argument("--cases", default=",".join(CASES))
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
