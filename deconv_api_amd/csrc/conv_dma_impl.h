@@ -743,6 +743,11 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
 // registers: 64 v_cndmask per wave per K step, each sub-step's MFMAs waiting on ALL its fragment
 // reads first. Now every A fragment address is a per-lane constant (FM x 3 VGPRs, one v_add each
 // per step for the stage offset; LDS: B0 | B1 | A0 | A1).
+// K step order: kh innermost (step = 3 cc + kh). The A tiles of kh = 0, 1, 2 for one channel chunk
+// are the same pixels shifted by one image row, so two of every three steps find their A rows in
+// L2 (the round-1..3 order, cc innermost, read a new 64-B chunk of every pixel each step): config-2
+// KW3 launches 0-4 % faster (tools/kw3_ab.py, profiles/kw3_ab_r4.txt; an ablation without the DMA
+// showed the A stream costing 4-13 % of a launch on the HBM-streamed 56^2 / 28^2 maps).
 // LDS rows are 64 B with the 16-B chunk XOR-swizzled by bit 2 of the slot (q ^ 2((slot >> 2) & 1)):
 // conflict-free ds_read_b128 fragment reads for 16 slots of consecutive indices mod 8 at any base.
 namespace {
@@ -819,7 +824,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
   const int nch = C / 32;
   const int nsteps = 3 * nch;
   auto issue = [&](int step, int buf) {
-    const int kh = step / nch, cc = step - kh * nch;
+    const int kh = step % 3, cc = step / 3;  // kh innermost (see the KW3 header)
     uint8_t* As = smem + 2 * B_BYTES + buf * A_BYTES;
     uint8_t* Bs = smem + buf * B_BYTES;
 #pragma unroll
@@ -1003,7 +1008,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
     }
   };
   auto issue = [&](int step, int buf) {
-    const int kh = step / nch, cc = step - kh * nch;
+    const int kh = step % 3, cc = step / 3;  // kh innermost (see the KW3 header)
     uint8_t* As = smem + 2 * B_BYTES + buf * A_BYTES;
     uint8_t* Bs = smem + buf * B_BYTES;
 #pragma unroll
