@@ -642,6 +642,44 @@ void dream_update(Tensor g, Tensor x, Tensor xin, Tensor gpart, Tensor lpart, Te
            "dream_update");
 }
 
+// DeepDream octave transition (engine/deepdream.py:DeepDream.octave_steps): y [N,Hd,Wd,3] fp32 = corner-aligned
+// bilinear resize of (a + b - c) (a, b, c [N,Hs,Ws,3] fp32; b, c optional); yin (optional) [N,Hd,Wd,8] 16-bit
+// network input.
+void octave_resize(Tensor a, c10::optional<Tensor> b, c10::optional<Tensor> c, Tensor y, c10::optional<Tensor> yin) {
+  check_cuda(a, "a");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  auto f3 = [](const Tensor& t) {
+    return t.scalar_type() == at::kFloat && t.is_contiguous() && t.dim() == 4 && t.size(3) == 3;
+  };
+  TORCH_CHECK(f3(a) && f3(y) && y.size(0) == a.size(0), "octave_resize: a, y fp32 [N,H,W,3] contiguous");
+  check_cuda(y, "y");
+  const float* bp = nullptr;
+  if (b && b->defined()) {
+    TORCH_CHECK(b->sizes() == a.sizes() && f3(*b), "octave_resize: b like a");
+    check_cuda(*b, "b");
+    bp = b->data_ptr<float>();
+  }
+  const float* cp = nullptr;
+  if (c && c->defined()) {
+    TORCH_CHECK(c->sizes() == a.sizes() && f3(*c), "octave_resize: c like a");
+    check_cuda(*c, "c");
+    cp = c->data_ptr<float>();
+  }
+  uint16_t* ip = nullptr;
+  int dt = dv::DT_BF16;
+  if (yin && yin->defined()) {
+    TORCH_CHECK(yin->dim() == 4 && yin->size(0) == y.size(0) && yin->size(1) == y.size(1) && yin->size(2) == y.size(2) &&
+                    yin->size(3) == 8 && yin->is_contiguous(),
+                "octave_resize: yin 16-bit [N,Hd,Wd,8] contiguous");
+    check_cuda(*yin, "yin");
+    dt = dt_of(*yin);
+    ip = reinterpret_cast<uint16_t*>(yin->data_ptr());
+  }
+  check_rc(dv::octave_resize_launch(a.data_ptr<float>(), bp, cp, y.data_ptr<float>(), ip, (int)a.size(0), (int)a.size(1),
+                                    (int)a.size(2), (int)y.size(1), (int)y.size(2), dt, cur_stream()),
+           "octave_resize");
+}
+
 // Tiled DeepDream step (engine/deepdream.py:TiledDeepDream). plan: int32 [units_total, 7] rows
 // {image, tile origin y, x, owned y0, y1, x0, x1 (tile-local)}, validated on the host when built;
 // shift: int32 [2] device (sy, sx). This rank's units are u = rank + k * world, k < xin.size(0).
@@ -1159,6 +1197,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tile_update", &tile_update, "tiled DeepDream: normalize + update the image from every rank's packs");
   m.def("tile_pack_elems", &tile_pack_elems);
   m.def("dream_update", &dream_update, "fused DeepDream normalize + update + next network input");
+  m.def("octave_resize", &octave_resize, "DeepDream octave transition: corner-aligned bilinear resize of (a + b - c)",
+        py::arg("a"), py::arg("b"), py::arg("c"), py::arg("y"), py::arg("yin") = py::none());
   m.def("stem_dgrad_fused", &stem_dgrad_fused, "fused GEMM + col2im input gradient of a 7x7/2 RGB stem conv");
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
   m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");

@@ -179,6 +179,50 @@ __global__ void __launch_bounds__(256) dream_update_kernel(const uint16_t* __res
   }
 }
 
+// ---- octave transition (engine/deepdream.py:DeepDream.octave_steps) ----
+// y[n] = bilinear resize, corner-aligned, of (a[n] + b[n] - c[n]) from [Hs, Ws, 3] to [Hd, Wd, 3] (fp32; b and c
+// optional, same shape as a: the dreamed image plus the octave's lost detail), with torch's upsample_bilinear2d index math (src = r * dst, r = (in-1)/(out-1) from the
+// host; i0 = floor, i1 = i0 + (i0 < in-1), lambda = src - i0), so it matches F.interpolate(align_corners=True)
+// to rounding. yin (optional) receives the same pixels in the 16-bit 8-channel network-input layout (channels
+// 3..7 zero), so an octave starts without copy/fill launches. One thread per output pixel.
+template <int DT>
+__global__ void __launch_bounds__(256) octave_resize_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                            const float* __restrict__ c, float* __restrict__ y, uint16_t* __restrict__ yin, int N,
+                                                            int Hs, int Ws, int Hd, int Wd, float rh, float rw) {
+  const long long total = (long long)N * Hd * Wd;
+  for (long long p = blockIdx.x * 256LL + threadIdx.x; p < total; p += (long long)gridDim.x * 256) {
+    const int ox = (int)(p % Wd);
+    const long long t = p / Wd;
+    const int oy = (int)(t % Hd), n = (int)(t / Hd);
+    const float sy = rh * (float)oy, sx = rw * (float)ox;
+    const int y0 = (int)sy, x0 = (int)sx;
+    const int dy = y0 < Hs - 1 ? Ws * 3 : 0, dx = x0 < Ws - 1 ? 3 : 0;
+    const float ly = sy - (float)y0, hy = 1.f - ly, lx = sx - (float)x0, hx = 1.f - lx;
+    const long long o = (((long long)n * Hs + y0) * Ws + x0) * 3;
+    float v[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const long long i00 = o + ch, i01 = i00 + dx, i10 = i00 + dy, i11 = i10 + dx;
+      float v00 = a[i00], v01 = a[i01], v10 = a[i10], v11 = a[i11];
+      if (b) {
+        v00 += b[i00];
+        v01 += b[i01];
+        v10 += b[i10];
+        v11 += b[i11];
+      }
+      if (c) {
+        v00 -= c[i00];
+        v01 -= c[i01];
+        v10 -= c[i10];
+        v11 -= c[i11];
+      }
+      v[ch] = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
+      y[p * 3 + ch] = v[ch];
+    }
+    if (yin) *reinterpret_cast<uint4*>(yin + p * 8) = uint4{pack2<DT>(v[0], v[1]), pack2<DT>(v[2], 0.f), 0u, 0u};
+  }
+}
+
 // ---- tiled DeepDream step (engine/deepdream.py:TiledDeepDream; BASELINE config 5) ----
 // Work units are (tile, image) pairs; unit u has plan row plan[u] = {image, tile origin y, x,
 // owned rect y0, y1, x0, x1 (tile-local, half-open)}. The image is rolled by shift = (sy, sx)
@@ -374,6 +418,20 @@ int dream_update_launch(const uint16_t* g, float* x, uint16_t* xin, float* gpart
     hipLaunchKernelGGL(dream_update_kernel<DT_BF16>, dim3(ub, (unsigned)N), dim3(256), 0, s, g, x, xin, gpart, gparts,
                        lpart, lcoef, L, lparts, N, done, loss, step, max_loss, HW);
   }
+  return (int)hipGetLastError();
+}
+
+int octave_resize_launch(const float* a, const float* b, const float* c, float* y, uint16_t* yin, int N, int Hs, int Ws, int Hd, int Wd,
+                         int dtype, hipStream_t s) {
+  if (N < 1 || Hs < 1 || Ws < 1 || Hd < 1 || Wd < 1) return -1;
+  const float rh = Hd > 1 ? (float)(Hs - 1) / (float)(Hd - 1) : 0.f;
+  const float rw = Wd > 1 ? (float)(Ws - 1) / (float)(Wd - 1) : 0.f;
+  const long long total = (long long)N * Hd * Wd;
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 256LL * 16);
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(octave_resize_kernel<DT_F16>, dim3(grid), dim3(256), 0, s, a, b, c, y, yin, N, Hs, Ws, Hd, Wd, rh, rw);
+  else
+    hipLaunchKernelGGL(octave_resize_kernel<DT_BF16>, dim3(grid), dim3(256), 0, s, a, b, c, y, yin, N, Hs, Ws, Hd, Wd, rh, rw);
   return (int)hipGetLastError();
 }
 

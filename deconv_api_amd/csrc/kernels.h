@@ -149,6 +149,10 @@ int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* i
 int dream_update_launch(const uint16_t* g, float* x, uint16_t* xin, float* gpart, int gparts, const float* lpart,
                         const float* lcoef, int L, int lparts, uint8_t* done, float* loss, float step, float max_loss,
                         int N, int H, int W, int dtype, hipStream_t s);
+// DeepDream octave transition: y = corner-aligned bilinear resize of (a + b - c) (fp32 NHWC, 3 channels; b, c may
+// be null), optionally also written as the 16-bit 8-channel network input yin
+int octave_resize_launch(const float* a, const float* b, const float* c, float* y, uint16_t* yin, int N, int Hs, int Ws, int Hd, int Wd,
+                         int dtype, hipStream_t s);
 // tiled DeepDream step: rolled tile gather -> owned-pixel pack (+ unit loss / sum|g| tail) ->
 // [all-gather of packs over ranks] -> update of the fp32 image straight from the packs
 int tile_gather_launch(const float* x, uint16_t* xin, const int* plan, const int* shift, int units, int rank, int world,

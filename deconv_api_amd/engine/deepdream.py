@@ -60,6 +60,9 @@ TILE_COLLECTIVE = os.environ.get("DV_TILE_COLLECTIVE", "0") == "1"
 # partial sums of squares come out of its loss-gradient kernel (one launch per loss layer, not two)
 FUSED_LOSS = os.environ.get("DV_DREAM_FUSED_LOSS", "1") != "0"
 LOSS_PARTS = 32
+# DV_DREAM_OCTAVE_RESIZE=0: octave transitions as F.interpolate + ATen adds (A/B); default: one
+# octave_resize HIP launch per transition writing the next octave's static inputs directly
+OCTAVE_RESIZE = os.environ.get("DV_DREAM_OCTAVE_RESIZE", "1") != "0"
 
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
 
@@ -254,6 +257,16 @@ class DeepDream:
         self._cache_put(key, (g, x, done, loss))
         return self._graphs[key]
 
+    def _ascend(self, st) -> None:
+        """The ``iterations`` fused steps on a state whose st.x / st.xin hold the octave's input."""
+        st.done.zero_()
+        if st.graph is None:
+            for _ in range(self.s.iterations):
+                self._fused_step(st)
+        else:
+            for _ in range(self.s.iterations // st.steps):
+                st.graph.replay()
+
     def gradient_ascent(self, x: torch.Tensor) -> torch.Tensor:
         B, H, W, _ = x.shape
         if self.fused:
@@ -262,13 +275,7 @@ class DeepDream:
                 st.x.copy_(x)
                 st.xin.zero_()
                 st.xin[..., :3].copy_(x)
-            st.done.zero_()
-            if st.graph is None:
-                for _ in range(self.s.iterations):
-                    self._fused_step(st)
-            else:
-                for _ in range(self.s.iterations // st.steps):
-                    st.graph.replay()
+            self._ascend(st)
             return st.x.clone()
         if self.use_graphs:
             g, gx, gdone, gloss = self._graph(B, (H, W))
@@ -323,6 +330,9 @@ class DeepDream:
         work enqueued, not necessarily finished). The multi-rank service drives a dream octave by
         octave through this, polling each octave's completion under its failure deadlines and
         letting other commands run between octaves (parallel/sharded.py)."""
+        if self.fused and x.is_cuda and OCTAVE_RESIZE:
+            yield from self._octave_steps_fused(x)
+            return
         shapes = self.octave_shapes(x.shape[1], x.shape[2])
         original = x
         shrunk = resize(original, shapes[0])
@@ -335,6 +345,44 @@ class DeepDream:
             img = img + (same - upscaled)
             shrunk = resize(original, hw)
             yield img
+
+    def _octave_steps_fused(self, x: torch.Tensor):
+        """``octave_steps`` on the fused GPU path: every octave transition is ONE octave_resize
+        launch (csrc/dream.hip) that resizes (dreamed image + lost detail) straight into the next
+        octave's static fp32 image and 16-bit network input, instead of F.interpolate x4, two ATen
+        adds and the copy/fill/clone around each octave's graph. The lost detail of octave o is
+        same_o - up_o with same_o = resize(x, s_o), up_o = resize(same_{o-1}, s_o) (0 for o = 0),
+        both enqueued ahead of the octave's replay. Intermediate yields are the octave's dreamed
+        image before its detail is re-injected (the detail rides on the next resize); the last
+        yield is the finished image, a fresh tensor."""
+        lib = native.lib()
+        shapes = self.octave_shapes(x.shape[1], x.shape[2])
+        x = x.contiguous()
+        B = x.shape[0]
+        dev = x.device
+
+        def resized(src, hw):
+            if tuple(hw) == tuple(src.shape[1:3]):
+                return src
+            dst = torch.empty(B, *hw, 3, device=dev)
+            lib.octave_resize(src, None, None, dst, None)
+            return dst
+
+        img = same = up = prev = None
+        for o, hw in enumerate(shapes):
+            st = self._fused_state(B, hw)
+            # the octave's input: x resized (octave 0) or the previous octave's image + its detail
+            lib.octave_resize(x if o == 0 else img, same, up, st.x, st.xin)
+            cur = resized(x, hw)
+            same, up = (None, None) if o == 0 else (cur, resized(prev, hw))
+            prev = cur
+            self._ascend(st)
+            img = st.x
+            if o + 1 < len(shapes):
+                yield img
+        out = torch.empty_like(img)
+        lib.octave_resize(img, same, up, out, None)
+        yield out
 
     def dream_u8(self, img_u8: torch.Tensor) -> torch.Tensor:
         """uint8 RGB [B, H, W, 3] -> uint8 dreamed image."""

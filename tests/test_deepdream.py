@@ -343,6 +343,55 @@ def test_gpu_fused_step_equals_unfused(native_lib):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("src,dst", [((108, 108), (152, 152)), ((213, 213), (299, 299)), ((37, 53), (20, 71)),
+                                     ((64, 64), (64, 64)), ((1, 5), (3, 1))])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gpu_octave_resize_matches_interpolate(native_lib, src, dst, dt):
+    """octave_resize (csrc/dream.hip) == F.interpolate(bilinear, align_corners=True) of (a + b - c), in fp32
+    on the GPU and against the fp64 CPU oracle; the 16-bit network-input copy is the rounded image with
+    channels 3..7 zero; an identity resize is exact."""
+    gen = torch.Generator().manual_seed(3)
+    a, b, c = (torch.randn(3, *src, 3, generator=gen) for _ in range(3))
+    want = deepdream_mod.resize((a + b - c).double(), dst).float()
+    y = torch.empty(3, *dst, 3, device="cuda")
+    yin = torch.full((3, *dst, 8), 7.0, dtype=dt, device="cuda")
+    native_lib.octave_resize(a.cuda(), b.cuda(), c.cuda(), y, yin)
+    # fp32 source positions (as torch's kernel): |error| <= slope x position ulp, ~1e-5 on these values
+    assert float((y.cpu() - want).abs().max()) < 2e-4
+    gpu_ref = deepdream_mod.resize((a + b - c).cuda(), dst)
+    assert float((y - gpu_ref).abs().max()) < 5e-5
+    assert torch.equal(yin[..., :3], y.to(dt)) and not yin[..., 3:].any()
+    y2 = torch.empty_like(y)
+    native_lib.octave_resize(a.cuda(), None, None, y2, None)
+    assert float((y2.cpu() - deepdream_mod.resize(a.double(), dst).float()).abs().max()) < 2e-4
+    if src == dst:
+        assert torch.equal(y2.cpu(), a)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_octaves_match_torch_octaves(native_lib):
+    """The fused octave loop (one octave_resize per transition, detail precomputed) == the torch octave loop
+    (F.interpolate + adds) around the same fused gradient ascent."""
+    net = InceptionV3(0).build("cuda")
+    x = (torch.rand(2, 220, 230, 3, generator=torch.Generator().manual_seed(8)) * 2 - 1).cuda()
+    for iters, max_loss in ((1, 1e-9), (2, None)):
+        dd = DeepDream(net, DreamSettings(iterations=iters, octaves=3, max_loss=max_loss), use_graphs=True)
+        dd.split = 1
+        got = dd.run(x)
+        shapes = dd.octave_shapes(220, 230)
+        img, shrunk = x, deepdream_mod.resize(x, shapes[0])
+        for hw in shapes:  # the generic loop of DeepDream.octave_steps
+            img = dd.gradient_ascent(deepdream_mod.resize(img, hw))
+            img = img + (deepdream_mod.resize(x, hw) - deepdream_mod.resize(shrunk, hw))
+            shrunk = deepdream_mod.resize(x, hw)
+        if max_loss is not None:  # no update: pure resize/detail arithmetic
+            assert float((got - img).abs().max()) < 1e-4
+        else:
+            # bf16-rounded network inputs (1-ulp differences of the resize grow through the steps)
+            assert _cos(got - x, img - x) > 0.99 and float((got - img).abs().max()) < 0.25
+
+
+@pytest.mark.gpu
 def test_gpu_split_batch_streams(native_lib):
     """A batch run as 2 concurrent sub-batches (own streams, own graphs) == the whole batch."""
     net = InceptionV3(0).build("cuda")
