@@ -876,7 +876,7 @@ def test_conv_two_destination_epilogue(native_lib, dt, N, H, C, OC, split, relu_
     assert bool((Yc[..., :40] == 7.0).all()) and bool((Yc[..., 40 + split:] == 7.0).all())  # untouched
 
 
-@pytest.mark.parametrize("N,H,W,div", [(4, 40, 48, 2), (2, 224, 224, 1), (8, 16, 96, 4)])
+@pytest.mark.parametrize("N,H,W,div", [(4, 40, 48, 2), (2, 224, 224, 1), (8, 16, 96, 4), (2, 42, 70, 2)])
 def test_deconv_tail_fused(native_lib, N, H, W, div):
     """Fused deconvnet tail (unpool -> 3x3 conv 64->64 -> ReLU -> per-tap products Z -> 9-tap
     shift-add -> ReLU, fp32 + per-image stats) vs its fp32 oracle with the same bf16 rounding points,
