@@ -947,11 +947,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
 // config-2 shape. Measured and removed: the fragment pipeline alone in the non-persistent kernel
 // (-2 % .. +2 %, noise) and the next step's DMA pieces issued one per MFMA group instead of all
 // after the first reads (-3 % .. +3 % vs this kernel, shape-dependent).
-// UC: max-unpool-out epilogue (a.ucode: the deconvnet's conv-downs that feed an unpooled map): each lane's 4
-// channels of one pixel go to the 4 positions of its 2x2 window, zeroed where the channel's switch code names
-// another position (the 32 code words of a tile's lane are loaded before its first store; 64-bit addressed
-// stores: the unpooled map can exceed 4 GiB).
-template <int DT, int BN_ = 256, int BM_ = 256, bool UC = false>
+template <int DT, int BN_ = 256, int BM_ = 256>
 __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, int tiles_n, int ntiles) {
   constexpr int BN = BN_, BM = BM_, NW = 8;
   constexpr int WN = BN / 64, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
@@ -968,7 +964,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
   const long long img_elems = (long long)HW * a.x_ld;
   const long long x_total = (long long)a.N * img_elems;
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (uint64_t)a.OCpad * a.Kpad * 2);
-  const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out, UC ? 16 : (uint64_t)a.out_elems * 2);  // UC: global stores
+  const __amdgpu_buffer_rsrc_t orr = make_rsrc(a.out, (uint64_t)a.out_elems * 2);
   const int lrow = lane >> 2;
   const int lchunk = (lane & 3) ^ kw3_swz(lrow);
   const int q = lane >> 4;
@@ -1134,19 +1130,6 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
     float bias[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) bias[j] = a.bias ? a.bias[cn0 + wn * FN * 16 + j * 16 + cl] : 0.f;
-    uint32_t ucd[UC ? FM : 1][UC ? FN : 1];
-    if constexpr (UC) {  // switch codes of this lane's (row, 4 columns) of every block
-      const int hw = a.OH * a.OW;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int row = cm0 + wm * FM * 16 + i * 16 + rsub;
-        const int rr = row < a.M ? row : a.M - 1;
-        const int nimg = rr / hw, rem = rr - nimg * hw;
-        const uint8_t* cb = a.ucode + ((long long)(nimg / a.ucode_div) * hw + rem) * a.OC + cn0 + wn * FN * 16 + csub;
-#pragma unroll
-        for (int j = 0; j < FN; ++j) ucd[i][j] = *reinterpret_cast<const uint32_t*>(cb + j * 16);
-      }
-    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int gcol = cn0 + wn * FN * 16 + j * 16 + cl;
@@ -1172,28 +1155,9 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
         const uint32_t w0 = cu ? recv2 : d0, w1 = cu ? d1 : recv2;
         const int row = cm0 + wm * FM * 16 + i * 16 + rsub;
         const int col = cn0 + wn * FN * 16 + j * 16 + csub;
-        if constexpr (UC) {
-          if (row < a.M) {
-            const int hw = a.OH * a.OW;
-            const int nimg = row / hw, rem = row - nimg * hw;
-            const int oh = rem / a.OW, ow = rem - oh * a.OW;
-            const long long ob = (((long long)nimg * 2 * a.OH + 2 * oh) * 2 * a.OW + 2 * ow) * a.out_ld + col;
-            const uint32_t cd = ucd[i][j];
-#pragma unroll
-            for (int pos = 0; pos < 4; ++pos) {
-              const uint32_t e = cd ^ ((uint32_t)pos * 0x01010101u);  // byte c == 0 <=> channel c's code is pos
-              const uint32_t m0 = ((e & 0xFFu) == 0u ? 0xFFFFu : 0u) | (((e >> 8) & 0xFFu) == 0u ? 0xFFFF0000u : 0u);
-              const uint32_t m1 = (((e >> 16) & 0xFFu) == 0u ? 0xFFFFu : 0u) | ((e >> 24) == 0u ? 0xFFFF0000u : 0u);
-              const long long po = ob + ((long long)(pos >> 1) * 2 * a.OW + (pos & 1)) * a.out_ld;
-              if (DV_BOUNDS(po, 4, a.out_elems, "kw3p unpool-out store"))
-                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.out) + po) = make_uint2(w0 & m0, w1 & m1);
-            }
-          }
-        } else {
-          const uint32_t off = row < a.M ? (uint32_t)(((long long)row * a.out_ld + col) * 2) : kOOB;
-          typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
-          __builtin_amdgcn_raw_buffer_store_b64(u32x2{w0, w1}, orr, (int)off, 0, 0);
-        }
+        const uint32_t off = row < a.M ? (uint32_t)(((long long)row * a.out_ld + col) * 2) : kOOB;
+        typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{w0, w1}, orr, (int)off, 0, 0);
       }
     }
     if (!more) break;
@@ -1215,11 +1179,6 @@ static int num_cus() {
 static int kw3_mode() {
   const char* e = std::getenv("DV_KW3");
   return e ? std::atoi(e) : 1;
-}
-// DV_KW3P_UNPOOL=0: unpool-out (ucode) epilogues on the non-persistent KW3 kernel (A/B). Read per launch.
-static bool kw3p_unpool_on() {
-  const char* e = std::getenv("DV_KW3P_UNPOOL");
-  return !(e && e[0] == '0');
 }
 // DV_KW3_VAR: the KW3 main-loop variant (conv_dma_kw3_kernel VAR; 8 / 9 are timing ablations that
 // produce wrong outputs, tools/kw3_ab.py only). Read per launch.
@@ -1252,15 +1211,11 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
     if constexpr (EPI == CONV_E_BF16) {
       // persistent KW3P: plain 16-bit epilogue only (its register-transpose stores write exactly
       // the C tile), output addressable by a 31-bit buffer offset, one workgroup per CU
-      if (var == 2 && a.res == nullptr && a.emask == nullptr && !a.accumulate && a.out2 == nullptr &&
-          a.OC == a.OCpad && a.OC % 4 == 0 && a.out_ld % 4 == 0 && a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19) &&
-          (a.ucode != nullptr ? kw3p_unpool_on() && a.ucode_div >= 1 && a.OH == a.H && a.OW == a.W
-                              : a.out_elems * 2 < 0x7FFFFFF0LL)) {
+      if (var == 2 && a.res == nullptr && a.emask == nullptr && !a.accumulate && a.ucode == nullptr &&
+          a.out2 == nullptr && a.OC == a.OCpad && a.OC % 4 == 0 && a.out_ld % 4 == 0 &&
+          a.out_elems * 2 < 0x7FFFFFF0LL && a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19)) {
         const unsigned g = (unsigned)(nwg < (long long)num_cus() ? nwg : (long long)num_cus());
-        if (a.ucode != nullptr)
-          hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, true>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
-        else
-          hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+        hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
         return (int)hipGetLastError();
       }
     }

@@ -322,32 +322,6 @@ def test_conv_kw3_persistent(native_lib, monkeypatch, N, H, W, C, OC, dt):
         assert _rel(outs["2"][: min(N, 8)], ref) < 1e-2
 
 
-@pytest.mark.parametrize("N,H,W,C,OC,div", [(8, 14, 14, 512, 512, 4), (6, 28, 28, 256, 128, 2), (5, 10, 12, 64, 256, 5),
-                                            (3, 56, 56, 128, 128, 1)])
-def test_conv_kw3p_unpool_out(native_lib, monkeypatch, N, H, W, C, OC, div):
-    """Unpool-out epilogue on the persistent KW3P kernel (the deconvnet's conv-downs feeding an unpooled map)
-    == the same epilogue on the non-persistent KW3 kernel (DV_KW3P_UNPOOL=0) bit for bit, == unpool of the
-    plain conv, nothing off the switch positions; tiles across image rows / images, the 512 x 128 tile, a
-    partial last round, code_div > 1."""
-    monkeypatch.setenv("DV_KW3", "2")
-    monkeypatch.setenv("DV_NO_SPLITK", "1")
-    g = torch.Generator().manual_seed(N * H + OC)
-    x = torch.relu(torch.randn(N, H, W, C, generator=g)).to(torch.bfloat16)
-    code = torch.randint(0, 4, (N // div, H, W, OC), generator=g, dtype=torch.uint8)
-    cw = _cw(OC, C, bias=False)
-    xd, cwd, cd = x.to(DEV), cw.to_device(DEV), code.to(DEV)
-    got = ops.conv2d(xd, cwd, relu=True, use_bias=False, unpool_out=cd, unpool_div=div)
-    monkeypatch.setenv("DV_KW3P_UNPOOL", "0")
-    old = ops.conv2d(xd, cwd, relu=True, use_bias=False, unpool_out=cd, unpool_div=div)
-    monkeypatch.delenv("DV_KW3P_UNPOOL")
-    assert got.shape == (N, 2 * H, 2 * W, OC)
-    assert torch.equal(got, old)
-    plain = ops.conv2d(xd, cwd, relu=True, use_bias=False)
-    want = ops.unpool_ref(plain, cd, div)
-    assert torch.equal(got, want)
-    assert ((got != 0) & (want == 0)).sum() == 0
-
-
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N,H,W,C,OC", [(5, 7, 7, 64, 256), (3, 14, 13, 96, 512), (2, 28, 28, 256, 256), (1, 9, 1, 32, 256),
                                         (4, 10, 9, 64, 128), (2, 56, 56, 256, 128)])
