@@ -89,25 +89,38 @@ __device__ __forceinline__ f32x4 mfma16x16x32(const typename Vec8<DT>::type& a, 
 
 // bf16 lane predicates on a packed pair (bits of two bf16 values in one u32)
 // (sign-bit / zero tests: valid for fp16 bit patterns too)
+// v_perm_b32 selectors 8 / 9 give 0xFF when bit 15 / 31 of the second source is set: the sign masks of both
+// halves in one permute, then one AND-NOT (2 VALU instead of ~6 compare/select)
 __device__ __forceinline__ uint32_t relu_bf2(uint32_t v) {
-  uint32_t lo = (v & 0x8000u) ? 0u : (v & 0xFFFFu);
-  uint32_t hi = (v & 0x80000000u) ? 0u : (v & 0xFFFF0000u);
-  return lo | hi;
+  return v & ~__builtin_amdgcn_perm(0u, v, 0x09090808u);
+}
+// Max-unpool switch select on one 16-B chunk: v = 8 16-bit channels, codes = their switch codes (byte c =
+// channel c's window position, 0..3); channels whose code != pos are zeroed. unpool_spread repeats each code
+// byte over its channel's two bytes (once per chunk); then per position ONE v_perm_b32(0, 0xFF << 8 pos, spread)
+// per dword maps every byte to 0xFF exactly where the code equals pos (selector bytes 0..3 index the constant)
+// and an AND applies it: 8 VALU per chunk and position instead of ~28 for per-byte compare/select (the unpool
+// expansions are VALU-bound: round 4 tail launch 4.27 -> 3.93 ms, profiles/bench_c2_r4_unpool_perm_ab.txt).
+__device__ __forceinline__ uint4 unpool_spread(uint2 codes) {
+  return make_uint4(__builtin_amdgcn_perm(0u, codes.x, 0x01010000u), __builtin_amdgcn_perm(0u, codes.x, 0x03030202u),
+                    __builtin_amdgcn_perm(0u, codes.y, 0x01010000u), __builtin_amdgcn_perm(0u, codes.y, 0x03030202u));
+}
+__device__ __forceinline__ uint4 unpool_pick_s(uint4 v, uint4 spread, uint32_t pos) {
+  const uint32_t K = 0xFFu << (8u * pos);
+  return make_uint4(v.x & __builtin_amdgcn_perm(0u, K, spread.x), v.y & __builtin_amdgcn_perm(0u, K, spread.y),
+                    v.z & __builtin_amdgcn_perm(0u, K, spread.z), v.w & __builtin_amdgcn_perm(0u, K, spread.w));
+}
+__device__ __forceinline__ uint4 unpool_pick(uint4 v, uint2 codes, uint32_t pos) {
+  return unpool_pick_s(v, unpool_spread(codes), pos);
 }
 // keep elements of v where the matching element of m is > 0
-__device__ __forceinline__ uint32_t mask_pos_bf2(uint32_t v, uint32_t m) {
-  uint32_t mlo = m & 0xFFFFu, mhi = m >> 16;
-  uint32_t lo = (mlo != 0u && !(mlo & 0x8000u)) ? (v & 0xFFFFu) : 0u;
-  uint32_t hi = (mhi != 0u && !(mhi & 0x8000u)) ? (v & 0xFFFF0000u) : 0u;
-  return lo | hi;
-}
-
 // keep the 16-bit elements of a where the matching element of m is > 0, 2 per u32, branch-free:
 // (m & 0x7FFF) + 0x7FFF sets bit 15 iff |m| != 0 (no carry across halves); & ~m clears negatives
+// (a sign-select v_perm_b32 in place of the multiply raised conv_pw's spills: 8-12 -> 12-17 VGPRs)
 __device__ __forceinline__ uint32_t mask_pos_pk(uint32_t a, uint32_t m) {
   const uint32_t pos = (((m & 0x7FFF7FFFu) + 0x7FFF7FFFu) & ~m) & 0x80008000u;
   return a & __umul24(pos >> 15, 0xFFFFu);
 }
+__device__ __forceinline__ uint32_t mask_pos_bf2(uint32_t v, uint32_t m) { return mask_pos_pk(v, m); }
 
 // Bijective XCD-aware workgroup remap (MI355X: 8 XCDs, consecutive dispatch ids go to
 // different XCDs). After the remap logically-adjacent tiles share an XCD (and its L2).

@@ -452,16 +452,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
         const uint4 pv = *reinterpret_cast<const uint4*>(pstage + sp * 64 + ch * 16);
         const uint2 cd = *reinterpret_cast<const uint2*>(cstage + sp * 32 + ch * 8);
         const uint32_t pos = (uint32_t)(((y & 1) << 1) | (x & 1));
-        const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
-        uint32_t ov[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t cw = e < 2 ? cd.x : cd.y;
-          const uint32_t c0 = (cw >> (16 * (e & 1))) & 0xFFu, c1 = (cw >> (16 * (e & 1) + 8)) & 0xFFu;
-          const uint32_t r = relu_bf2(pw[e]);  // sign-bit test: valid for fp16 bit patterns too
-          ov[e] = (c0 == pos ? r & 0xFFFFu : 0u) | (c1 == pos ? r & 0xFFFF0000u : 0u);
-        }
-        v = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+        // ReLU (sign-bit test: valid for fp16 bit patterns too), then the switch select
+        v = unpool_pick(make_uint4(relu_bf2(pv.x), relu_bf2(pv.y), relu_bf2(pv.z), relu_bf2(pv.w)), cd, pos);
       }
       *reinterpret_cast<uint4*>(hd + p * 64 + ((ch ^ h16_swz(p)) << 4)) = v;
     }

@@ -132,19 +132,7 @@ __global__ void __launch_bounds__(256, 2) conv_igemm_kernel(const ConvArgs a, in
             v = *reinterpret_cast<const uint4*>(a.x + pix * a.x_ld + c);
             const long long cpix = ((long long)(r_n[i] / a.code_div) * PH + ph) * PW + pw;
             const uint2 cd = *reinterpret_cast<const uint2*>(a.code + cpix * C + c);
-            const uint32_t sel = (uint32_t)(((ih & 1) << 1) | (iw & 1));
-            const uint32_t sel4 = sel * 0x01010101u;
-            // per-byte equality -> per-element keep masks
-            const uint32_t e0 = cd.x ^ sel4, e1 = cd.y ^ sel4;
-            auto keep2 = [](uint32_t e, int byte0) -> uint32_t {
-              uint32_t lo = ((e >> (8 * byte0)) & 0xFFu) == 0u ? 0xFFFFu : 0u;
-              uint32_t hi = ((e >> (8 * (byte0 + 1))) & 0xFFu) == 0u ? 0xFFFF0000u : 0u;
-              return lo | hi;
-            };
-            v.x &= keep2(e0, 0);
-            v.y &= keep2(e0, 2);
-            v.z &= keep2(e1, 0);
-            v.w &= keep2(e1, 2);
+            v = unpool_pick(v, cd, (uint32_t)(((ih & 1) << 1) | (iw & 1)));
           } else {
             const long long pix = ((long long)r_n[i] * H + ih) * W + iw;
             v = *reinterpret_cast<const uint4*>(a.x + pix * a.x_ld + c);

@@ -108,7 +108,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 4) conv_pw_kernel(const ConvArgs
       const int t = first + j * G;
       const int m0 = (t / tiles_n) * BM, n0 = (t - (t / tiles_n) * tiles_n) * BN;
       __syncthreads();  // every wave is done reading slot `cur`: it becomes the C staging buffer
-      epilogue_lds<DT, NT, BM, BN, FM, FN>(a, acc, smem + cur * STAGE, m0, n0, wm, wn, lane, tid, true);
+      // ucode known null (the launcher rejects it): the epilogue's max-unpool branch folds away
+      ConvArgs an = a;
+      an.ucode = nullptr;
+      epilogue_lds<DT, NT, BM, BN, FM, FN>(an, acc, smem + cur * STAGE, m0, n0, wm, wn, lane, tid, true);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

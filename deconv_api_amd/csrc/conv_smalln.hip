@@ -109,16 +109,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_c64_persist_kernel(const ConvA
         if constexpr (UNPOOL) {
           const int p = idx >> 3;
           const int iy = ld_y0 + p / IW, ix = ld_x0 + p % IW;
-          const uint32_t sel4 = (uint32_t)(((iy & 1) << 1) | (ix & 1)) * 0x01010101u;
-          const uint32_t e0 = rc[q].x ^ sel4, e1 = rc[q].y ^ sel4;
-          auto keep2 = [](uint32_t e, int b0) -> uint32_t {
-            return ((((e >> (8 * b0)) & 0xFFu) == 0u) ? 0xFFFFu : 0u) |
-                   ((((e >> (8 * (b0 + 1))) & 0xFFu) == 0u) ? 0xFFFF0000u : 0u);
-          };
-          v.x &= keep2(e0, 0);
-          v.y &= keep2(e0, 2);
-          v.z &= keep2(e1, 0);
-          v.w &= keep2(e1, 2);
+          v = unpool_pick(v, rc[q], (uint32_t)(((iy & 1) << 1) | (ix & 1)));
         }
         if (a.relu_in) {
           v.x = relu_bf2(v.x);
@@ -325,21 +316,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
         v.z = relu_bf2(v.z);
         v.w = relu_bf2(v.w);
       }
+      const uint4 sp = unpool_spread(rc[q]);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const int hy = 2 * py + (d >> 1) - y0, hx = 2 * px + (d & 1) - x0;
         if ((unsigned)hy >= (unsigned)IH || (unsigned)hx >= (unsigned)IW) continue;
-        const uint32_t sel4 = (uint32_t)d * 0x01010101u;
-        const uint32_t e0 = rc[q].x ^ sel4, e1 = rc[q].y ^ sel4;
-        auto keep2 = [](uint32_t e, int b0) -> uint32_t {
-          return ((((e >> (8 * b0)) & 0xFFu) == 0u) ? 0xFFFFu : 0u) |
-                 ((((e >> (8 * (b0 + 1))) & 0xFFu) == 0u) ? 0xFFFF0000u : 0u);
-        };
-        uint4 o;
-        o.x = v.x & keep2(e0, 0);
-        o.y = v.y & keep2(e0, 2);
-        o.z = v.z & keep2(e1, 0);
-        o.w = v.w & keep2(e1, 2);
+        const uint4 o = unpool_pick_s(v, sp, (uint32_t)d);
         *reinterpret_cast<uint4*>(As + (hy * IW + hx) * PIXB + c8 * 16) = o;
       }
     }

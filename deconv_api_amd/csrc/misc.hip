@@ -636,22 +636,11 @@ __global__ void __launch_bounds__(256) unpool2x2_vec_kernel(const uint16_t* __re
     }
     const long long cpix = ((n / code_div) * PH + ph) * PW + pw;
     const uint2 cd = *reinterpret_cast<const uint2*>(code + cpix * C + chunk * 8);
-    const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+    const uint4 sp = unpool_spread(cd);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const uint32_t sel4 = (uint32_t)s * 0x01010101u;
-      const uint32_t e0 = cd.x ^ sel4, e1 = cd.y ^ sel4;
-      uint32_t o[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t e = q < 2 ? e0 : e1;
-        const int b0 = (q & 1) * 2;
-        const uint32_t lo = ((e >> (8 * b0)) & 0xFFu) == 0u ? 0xFFFFu : 0u;
-        const uint32_t hi = ((e >> (8 * (b0 + 1))) & 0xFFu) == 0u ? 0xFFFF0000u : 0u;
-        o[q] = vw[q] & (lo | hi);
-      }
       const int h = 2 * ph + (s >> 1), w = 2 * pw + (s & 1);
-      *reinterpret_cast<uint4*>(out + ((n * H + h) * W + w) * C + chunk * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<uint4*>(out + ((n * H + h) * W + w) * C + chunk * 8) = unpool_pick_s(v, sp, (uint32_t)s);
     }
   }
 }
