@@ -51,8 +51,13 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// two floats -> one packed pair through a 2-vector conversion: ONE v_cvt_pk_bf16_f32 (the scalar casts
+// combined with a shift + or compile to two converts and two more VALU)
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 
 // ---- 16-bit storage dtype trait: DT 0 = bf16, DT 1 = fp16 (IEEE half) ----
@@ -69,8 +74,9 @@ __device__ __forceinline__ uint16_t from_f(float f) {
   else return __builtin_bit_cast(uint16_t, (_Float16)f);
 }
 template <int DT>
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return (uint32_t)from_f<DT>(lo) | ((uint32_t)from_f<DT>(hi) << 16);
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {  // v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32
+  if constexpr (DT == DT_BF16) return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
+  else return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, f16x2_t));
 }
 template <int DT>
 struct Vec8 {
