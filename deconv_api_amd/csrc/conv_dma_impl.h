@@ -255,8 +255,10 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
       ok = ok && kval;
       ok = ok && DV_BOUNDS((long long)n_base * img_elems + ((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch, 8,
                            a.x_elems, "conv_dma A gather");
+      // 32-bit offset math: the DMA offset is 32-bit anyway, and the 64-bit multiply it was truncated from cost
+      // ~4 more VALU per DMA in a K step that is issue-bound on the small GEMMs
       const uint32_t voff =
-          ok ? (uint32_t)((((long long)(r_off[j] + ih * W + iw)) * a.x_ld + ch) * 2) : kOOB;
+          ok ? ((uint32_t)(r_off[j] + ih * W + iw) * (uint32_t)a.x_ld + (uint32_t)ch) * 2u : kOOB;
       dma16(xr, As + (j * NW + wave) * 1024, voff);
       if constexpr (MASK) dma16(mr, As + A_BYTES + (j * NW + wave) * 1024, voff);
     }
@@ -266,7 +268,7 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
       const int grp = j * NW + wave;
       if (grp < B_GROUPS) {
         const int row = grp * RPI + lrow;
-        const uint32_t voff = (uint32_t)((((long long)(n0 + row)) * a.Kpad + kt * BK + lchunk * 8) * 2);
+        const uint32_t voff = ((uint32_t)(n0 + row) * (uint32_t)a.Kpad + (uint32_t)(kt * BK + lchunk * 8)) * 2u;
         if (DV_BOUNDS((long long)voff / 2, 8, (long long)a.OCpad * a.Kpad, "conv_dma B weights"))
           dma16(wr, Bs + grp * 1024, voff);
       }
@@ -832,7 +834,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
       if ((u * NW + wave) * 16 >= nslots) continue;  // slots past the tile's last are never read
       const bool ok = (unsigned)(r_oh[u] + kh - 1) < (unsigned)H;
       const uint32_t voff =
-          ok ? (uint32_t)((((long long)(r_pix[u] + (kh - 1) * W)) * a.x_ld + cc * 32 + lchunk * 8) * 2) : kOOB;
+          ok ? ((uint32_t)(r_pix[u] + (kh - 1) * W) * (uint32_t)a.x_ld + (uint32_t)(cc * 32 + lchunk * 8)) * 2u : kOOB;
       dma16(xr, As + (u * NW + wave) * 1024, voff);
     }
 #pragma unroll
@@ -840,7 +842,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
       const int v = u * NW + wave;  // kw sub-tile v >> 4, rows (v & 15) * 16 + lrow
       const int kw = v / (BN / 16), brow = (v % (BN / 16)) * 16 + lrow;
       const uint32_t voff =
-          (uint32_t)((((long long)(n0 + brow)) * a.Kpad + (kh * 3 + kw) * C + cc * 32 + lchunk * 8) * 2);
+          ((uint32_t)(n0 + brow) * (uint32_t)a.Kpad + (uint32_t)((kh * 3 + kw) * C + cc * 32 + lchunk * 8)) * 2u;
       dma16(wr, Bs + v * 1024, voff);
     }
   };
@@ -1017,7 +1019,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
       const int oh = (int)(r_po[u] & 0xFFFu), pix = (int)(r_po[u] >> 12);
       const bool ok = r_po[u] != ~0u && (unsigned)(oh + kh - 1) < (unsigned)H;
       const uint32_t voff =
-          ok ? (uint32_t)((((long long)(pix + (kh - 1) * W)) * a.x_ld + cc * 32 + lchunk * 8) * 2) : kOOB;
+          ok ? ((uint32_t)(pix + (kh - 1) * W) * (uint32_t)a.x_ld + (uint32_t)(cc * 32 + lchunk * 8)) * 2u : kOOB;
       dma16(xr, As + (u * NW + wave) * 1024, voff);
     }
 #pragma unroll
@@ -1025,7 +1027,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
       const int vv = u * NW + wave;
       const int kw = vv / (BN / 16), brow = (vv % (BN / 16)) * 16 + lrow;
       const uint32_t voff =
-          (uint32_t)((((long long)(n0 + brow)) * a.Kpad + (kh * 3 + kw) * C + cc * 32 + lchunk * 8) * 2);
+          ((uint32_t)(n0 + brow) * (uint32_t)a.Kpad + (uint32_t)((kh * 3 + kw) * C + cc * 32 + lchunk * 8)) * 2u;
       dma16(wr, Bs + vv * 1024, voff);
     }
   };
@@ -1155,7 +1157,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
         const uint32_t w0 = cu ? recv2 : d0, w1 = cu ? d1 : recv2;
         const int row = cm0 + wm * FM * 16 + i * 16 + rsub;
         const int col = cn0 + wn * FN * 16 + j * 16 + csub;
-        const uint32_t off = row < a.M ? (uint32_t)(((long long)row * a.out_ld + col) * 2) : kOOB;
+        const uint32_t off = row < a.M ? ((uint32_t)row * (uint32_t)a.out_ld + (uint32_t)col) * 2u : kOOB;
         typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{w0, w1}, orr, (int)off, 0, 0);
       }

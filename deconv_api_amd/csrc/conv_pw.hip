@@ -56,14 +56,14 @@ __global__ void __launch_bounds__(WM * WN * 64, 4) conv_pw_kernel(const ConvArgs
     for (int i = 0; i < A_I; ++i) {
       const int gm = m0 + (i * NW + wave) * RPI + lrow;
       const bool ok = gm < a.M && DV_BOUNDS((long long)gm * a.x_ld + ch, 8, a.x_elems, "conv_pw A");
-      dma16(xr, As + (i * NW + wave) * 1024, ok ? (uint32_t)(((long long)gm * a.x_ld + ch) * 2) : kOOB);
+      dma16(xr, As + (i * NW + wave) * 1024, ok ? ((uint32_t)gm * (uint32_t)a.x_ld + (uint32_t)ch) * 2u : kOOB);
     }
 #pragma unroll
     for (int i = 0; i < B_FULL + (B_REM ? 1 : 0); ++i) {
       const int grp = i * NW + wave;
       if (grp < B_GROUPS) {
         const int row = grp * RPI + lrow;
-        dma16(wr, Bs + grp * 1024, (uint32_t)((((long long)(n0 + row)) * a.Kpad + kt * BK + lchunk * 8) * 2));
+        dma16(wr, Bs + grp * 1024, ((uint32_t)(n0 + row) * (uint32_t)a.Kpad + (uint32_t)(kt * BK + lchunk * 8)) * 2u);
       }
     }
   };
