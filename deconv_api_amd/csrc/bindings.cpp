@@ -178,6 +178,9 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     need(*out_code, out_rows * a.OC, "out_code");
     a.out_code = reinterpret_cast<uint8_t*>(out_code->data_ptr());
     TORCH_CHECK(out.scalar_type() == dt, "pool out must have x's dtype");
+    const bool no_pool_t = std::getenv("DV_NO_POOL_T") != nullptr;  // A/B: the per-element pool stores (per call)
+    a.pool_t = !no_pool_t && a.OC % 4 == 0 && a.out_ld % 4 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0 &&
+               reinterpret_cast<uintptr_t>(a.out_code) % 4 == 0;
   } else if (epi == dv::CONV_E_F32) {
     TORCH_CHECK(out.scalar_type() == at::kFloat, "f32 epilogue needs fp32 out");
   } else {

@@ -462,8 +462,77 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
   }
 }
 
+// Pooled-max epilogue with 8-B stores: a lane's 4 accumulators are one 2x2 window of one channel (pool-major M
+// order), so the max / first-max code per (fragment, channel) comes out one value per lane; a 4 x 4 transpose
+// over each lane quad (two DPP swaps, as KW3P's epilogue) then gives every lane 4 consecutive channels of one
+// pooled pixel: one 8-B value store + one 4-B code store per 4 fragments instead of 4 two-byte + 4 one-byte
+// stores, each with its own 64-bit address. Needs FM % 4 == 0 and 4-aligned channel counts / strides (host).
+template <int DT, int FM, int FN>
+__device__ __forceinline__ void epilogue_pool_t(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw,
+                                                int lane) {
+  const int q = lane >> 4, cl = lane & 15, ce = cl & 1, cu = (cl >> 1) & 1, csub = cl & ~3, tsel = ce * 2 + cu;
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col0 = nw + j * 16;
+    const float bias = (a.bias && col0 + cl < a.OC) ? a.bias[col0 + cl] : 0.f;
+#pragma unroll
+    for (int ig = 0; ig < FM / 4; ++ig) {
+      float best[4];
+      uint32_t code[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int i = ig * 4 + t;
+        float b = -INFINITY;
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bias;
+          if (a.relu) v = fmaxf(v, 0.f);
+          v = to_f<DT>(from_f<DT>(v));
+          if (v > b) {
+            b = v;
+            c = (uint32_t)r;
+          }
+        }
+        best[t] = b;
+        code[t] = c;
+      }
+      // rows = the 4 fragments, columns = channels: lane (quad position tsel) ends with fragment ig*4 + tsel,
+      // channels csub .. csub + 3
+      auto tr = [&](uint32_t p0, uint32_t p1, uint32_t& w0, uint32_t& w1) {
+        const uint32_t keep = ce ? p1 : p0;
+        const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(ce ? p0 : p1), 0xB1, 0xF, 0xF, false);
+        const uint32_t lo = ce ? recv : keep, hi = ce ? keep : recv;
+        const uint32_t d0 = (lo & 0xFFFFu) | (hi << 16), d1 = (lo >> 16) | (hi & 0xFFFF0000u);
+        const uint32_t recv2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(cu ? d0 : d1), 0x4E, 0xF, 0xF, false);
+        w0 = cu ? recv2 : d0;
+        w1 = cu ? d1 : recv2;
+      };
+      uint32_t w0, w1, k0, k1;
+      tr(pack2<DT>(best[0], best[1]), pack2<DT>(best[2], best[3]), w0, w1);
+      tr(code[0] | (code[1] << 16), code[2] | (code[3] << 16), k0, k1);
+      const int rowb = mw + (ig * 4 + tsel) * 16 + q * 4;  // first M row of this lane's window
+      const int col = col0 + csub;
+      if (rowb >= a.M || col >= a.OC) continue;
+      const long long prow = rowb >> 2;
+      if (DV_BOUNDS(prow * a.out_ld + col, 4, a.out_elems, "conv_dma pool epilogue out")) {
+        *reinterpret_cast<uint2*>(out + prow * a.out_ld + col) = make_uint2(w0, w1);
+        *reinterpret_cast<uint32_t*>(a.out_code + prow * a.OC + col) =
+            (k0 & 0xFFu) | ((k0 >> 8) & 0xFF00u) | ((k1 & 0xFFu) << 16) | ((k1 >> 16) << 24);
+      }
+    }
+  }
+}
+
 template <int DT, int FM, int FN, int EPI, bool accum>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[FM][FN], int mw, int nw, int lane) {
+  if constexpr (EPI == CONV_E_POOL && FM % 4 == 0) {
+    if (a.pool_t) {
+      epilogue_pool_t<DT, FM, FN>(a, acc, mw, nw, lane);
+      return;
+    }
+  }
   const int row_l = (lane >> 4) * 4;
   const int col_l = lane & 15;
 #pragma unroll

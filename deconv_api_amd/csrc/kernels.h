@@ -66,6 +66,8 @@ struct ConvArgs {
   long long out2_elems;
   const uint16_t* w2;     // optional second-GEMM weights of a fused epilogue (conv3x3_unpool_z_launch: the
                           //   next conv-down's taps as a [32][64] matrix, row tap*3+c = W[c][tap][:])
+  int pool_t;             // host-checked (POOL epilogue): OC, out_ld % 4 == 0, out 8-B / out_code 4-B aligned ->
+                          //   the transposed pooled-max epilogue (conv_dma_impl.h:epilogue_pool_t)
 };
 
 // grouped LDS-DMA launch of up to kGroupMax independent problems (conv_dma.hip:conv_dma_group_launch)

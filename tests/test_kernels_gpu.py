@@ -106,6 +106,23 @@ def test_conv_pool_epilogue(native_lib):
     assert agree.float().mean() > 0.999
 
 
+@pytest.mark.parametrize("N,H,W,C,OC", [(2, 56, 56, 256, 256), (3, 28, 28, 512, 512), (2, 16, 14, 64, 128),
+                                        (3, 10, 14, 64, 192), (1, 12, 12, 32, 48)])
+def test_conv_pool_epilogue_transposed(native_lib, monkeypatch, N, H, W, C, OC):
+    """Pooled-max epilogue with DPP-transposed 8-B stores (epilogue_pool_t) == the per-element stores
+    (DV_NO_POOL_T=1) bit for bit, values and switch codes; partial channel blocks (OC 48) and M tails."""
+    monkeypatch.setenv("DV_NO_POOL_V3", "1")
+    monkeypatch.setenv("DV_NO_HS16", "1")
+    monkeypatch.setenv("DV_KW3", "0")
+    g = torch.Generator().manual_seed(N * H + OC)
+    x = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).to(DEV)
+    cwd = _cw(OC, C).to_device(DEV)
+    got_p, got_c = ops.conv2d(x, cwd, relu=True, epilogue="pool")
+    monkeypatch.setenv("DV_NO_POOL_T", "1")
+    ref_p, ref_c = ops.conv2d(x, cwd, relu=True, epilogue="pool")
+    assert torch.equal(got_p, ref_p) and torch.equal(got_c, ref_c)
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 112, 120), (1, 118, 112), (1, 224, 224)])
 def test_conv_pool_v3(native_lib, N, H, W):
     """64 -> 64 conv + fused pool at >= 112^2 maps (weight-resident halo kernel) vs the fp32 reference
