@@ -635,24 +635,39 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
                                              int n0, int wm, int wn, int lane, int tid, bool writer) {
   constexpr int CPR = BN / 8;                       // 16-B chunks per C-tile row
   constexpr int SWZ = (CPR < 8 ? CPR : 8) - 1;
-  const int row_l = (lane >> 4) * 4, col_l = lane & 15;
+  const int col_l = lane & 15;
   const bool pre_relu = a.relu && a.res == nullptr;
+  // C tile -> LDS: each 16 x 16 block's 4 rows x 1 column per lane are transposed within the lane quad
+  // (two DPP swaps, as the KW3P epilogue) to 1 row x 4 consecutive columns, written as ONE ds_write_b64
+  // (the per-element form was 4 converts, 4 address computations and 4 ds_write_b16 per block)
+  const int ce = col_l & 1, cu = (col_l >> 1) & 1;
+  const int rsub = (lane >> 4) * 4 + ce * 2 + cu, csub = col_l & ~3;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     if (!writer) break;
-    const int col = wn * FN * 16 + j * 16 + col_l;
-    const int gcol = n0 + col;
+    const int gcol = n0 + wn * FN * 16 + j * 16 + col_l;
     const float bias = (a.bias && gcol < a.OCpad) ? a.bias[gcol] : 0.f;
+    const bool rl = pre_relu && relu_at(a, gcol);
+    const int col = wn * FN * 16 + j * 16 + csub;
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * FM * 16 + i * 16 + row_l + r;
-        float v = acc[i][j][r] + bias;
-        if (pre_relu && relu_at(a, gcol)) v = fmaxf(v, 0.f);
-        *reinterpret_cast<uint16_t*>(smem + row * (BN * 2) + ((((col >> 3) ^ (row & SWZ))) << 4) + (col & 7) * 2) =
-            from_f<DT>(v);
+    for (int i = 0; i < FM; ++i) {
+      float f0 = acc[i][j][0] + bias, f1 = acc[i][j][1] + bias, f2 = acc[i][j][2] + bias, f3 = acc[i][j][3] + bias;
+      if (rl) {
+        f0 = fmaxf(f0, 0.f);
+        f1 = fmaxf(f1, 0.f);
+        f2 = fmaxf(f2, 0.f);
+        f3 = fmaxf(f3, 0.f);
       }
+      const uint32_t p0 = pack2<DT>(f0, f1), p1 = pack2<DT>(f2, f3);
+      const uint32_t keep = ce ? p1 : p0;
+      const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(ce ? p0 : p1), 0xB1, 0xF, 0xF, false);
+      const uint32_t lo = ce ? recv : keep, hi = ce ? keep : recv;
+      const uint32_t d0 = (lo & 0xFFFFu) | (hi << 16), d1 = (lo >> 16) | (hi & 0xFFFF0000u);
+      const uint32_t recv2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(cu ? d0 : d1), 0x4E, 0xF, 0xF, false);
+      const int row = wm * FM * 16 + i * 16 + rsub;
+      *reinterpret_cast<uint2*>(smem + row * (BN * 2) + ((((col >> 3) ^ (row & SWZ))) << 4) + (col & 7) * 2) =
+          make_uint2(cu ? recv2 : d0, cu ? d1 : recv2);
+    }
   }
   __syncthreads();
   uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
