@@ -143,8 +143,9 @@ int conv_pw_launch(const ConvArgs& a, hipStream_t s) {
   }
   const int tiles_n = a.OCpad / BN;
   const long long tiles_total = (long long)((a.M + BM - 1) / BM) * tiles_n;
-  // persistence pays once every CU walks several tiles
-  if (tiles_total < (min_tiles > 0 ? min_tiles : 4 * cus) || tiles_total > 0x7fffffffLL) return -4;
+  // persistence pays once every CU has a tile: round 4 (kernel without spills) moved the default from 4 to 1 tile
+  // per CU (config 5 +0.7 %, config 3 unchanged, profiles/dream_r4_pw_min_tiles.txt)
+  if (tiles_total < (min_tiles > 0 ? min_tiles : cus) || tiles_total > 0x7fffffffLL) return -4;
   const unsigned G = (unsigned)std::min<long long>(tiles_total, 2 * cus);
   if (BN == 128) {
     if (a.dtype == DT_F16)
