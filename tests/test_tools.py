@@ -1,5 +1,5 @@
 """CPU: the trace / layout analysis tools behind the committed profiles (tools/kstats.py,
-tools/kseq.py, tools/lds_bank_check.py) on synthetic inputs."""
+tools/kseq.py, tools/lds_bank_check.py, tools/spill_diff.py) on synthetic inputs."""
 import os
 import sqlite3
 import sys
@@ -56,3 +56,26 @@ def test_lds_bank_check_layouts():
     assert ways(lambda p, q: p * 64 + ((q ^ swz(p)) << 4)) == 1
     assert ways(lambda p, q: p * 160 + q * 16) == 1  # c64 halo pitch (round 3)
     assert ways(lambda p, q: p * 144 + q * 16) == 2  # the round-2 pitch
+
+
+def test_spill_diff_flags_regressions(tmp_path, capsys):
+    """tools/spill_diff.py reads -Rpass-analysis=kernel-resource-usage remarks and fails when any kernel of
+    the new build spills more VGPRs or uses more scratch than in the old one."""
+    import spill_diff
+
+    def remarks(path, rows):
+        with open(path, "w") as f:
+            for name, vgpr, spill, scratch in rows:
+                f.write(f"x.hip:1:1: remark: Function Name: {name} [-Rpass-analysis=kernel-resource-usage]\n")
+                f.write(f"x.hip:1:1: remark:     VGPRs: {vgpr} [-Rpass-analysis=kernel-resource-usage]\n")
+                f.write(f"x.hip:1:1: remark:     VGPRs Spill: {spill} [-Rpass-analysis=kernel-resource-usage]\n")
+                f.write(f"x.hip:1:1: remark:     ScratchSize [bytes/lane]: {scratch} [-Rpass-analysis=kernel-resource-usage]\n")
+
+    remarks(tmp_path / "o_u.txt", [("_Z1ak", 128, 8, 36), ("_Z1bk", 200, 0, 0)])
+    remarks(tmp_path / "n_u.txt", [("_Z1ak", 103, 0, 0), ("_Z1bk", 256, 0, 480)])
+    sys.argv = ["spill_diff", str(tmp_path / "o_{unit}.txt"), str(tmp_path / "n_{unit}.txt"), "u"]
+    assert spill_diff.main() == 1  # _Z1bk: 0 -> 480 B of scratch
+    out = capsys.readouterr().out
+    assert "worse 1, better 1" in out and "_Z1bk" in out
+    remarks(tmp_path / "n_u.txt", [("_Z1ak", 103, 0, 0), ("_Z1bk", 200, 0, 0)])
+    assert spill_diff.main() == 0
