@@ -47,7 +47,7 @@ from deconv_api_amd.runtime.streams import copy_stream as copy_stream_for
 # next step's first layers queued. Raw mosaics are copied right after their step is enqueued (the
 # copy costs ~0.2 % of the step: --no-copyback 7016 vs 6999 img/s, profiles/bench_c2_r3_copy_ab.txt).
 JPEG = os.environ.get("DV_BENCH_JPEG", "0") == "1"
-COPY_AT = "block3_conv1" if JPEG else ""
+COPY_AT = os.environ.get("DV_BENCH_COPY_AT", "block3_conv1" if JPEG else "")
 
 # the reference's implied end-to-end rate for layer=block5_conv3 is ~0.03-0.04 img/s
 # (CPU, one request at a time; a lower bound on its cost). We divide by the favourable 0.04.
