@@ -91,6 +91,44 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
     const int h = (int)(pq % g.H);
     const long long n = (long long)(pq / g.H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (KC == 3 && g.s == 2) {
+      // 3x3 / stride 2 (every InceptionV3 / ResNet-50 max pool): at most 2 x 2 windows contain
+      // (h, w), oh in {ohh - 1, ohh}; all 8 loads are issued (clamped to a real window) before the
+      // first use, and summed in the generic loop's (oh, ow) ascending order: bit-identical results
+      const int ohh = (h + g.pad) >> 1, owh = (w + g.pad) >> 1;
+      uint4 v[2][2];
+      uint2 ix[2][2];
+      uint32_t pos[2][2];
+      bool ok[2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int oh = ohh - 1 + a, kh = ((h + g.pad) & 1) + 2 - 2 * a;
+        const bool vh = oh >= 0 && oh < g.OH && kh < 3;
+        const int ohc = oh < 0 ? 0 : (oh >= g.OH ? g.OH - 1 : oh);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int ow = owh - 1 + b, kw = ((w + g.pad) & 1) + 2 - 2 * b;
+          ok[a][b] = vh && ow >= 0 && ow < g.OW && kw < 3;
+          const int owc = ow < 0 ? 0 : (ow >= g.OW ? g.OW - 1 : ow);
+          pos[a][b] = (uint32_t)(kh * 3 + kw);
+          const long long op = (n * g.OH + ohc) * g.OW + owc;
+          v[a][b] = *reinterpret_cast<const uint4*>(gy + op * g.y_ld + ch * 8);
+          ix[a][b] = *reinterpret_cast<const uint2*>(idx + op * g.C + ch * 8);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (!ok[a][b]) continue;
+          const uint32_t w4[4] = {v[a][b].x, v[a][b].y, v[a][b].z, v[a][b].w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t ie = ((e < 4 ? ix[a][b].x : ix[a][b].y) >> (8 * (e & 3))) & 0xFFu;
+            if (ie == pos[a][b]) acc[e] += to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+          }
+        }
+    } else {
     // windows containing (h, w): oh*s - pad <= h <= oh*s - pad + k - 1
     const int oh_lo = max(0, (h + g.pad - k + g.s) / g.s), oh_hi = min(g.OH - 1, (h + g.pad) / g.s);
     const int ow_lo = max(0, (w + g.pad - k + g.s) / g.s), ow_hi = min(g.OW - 1, (w + g.pad) / g.s);
@@ -111,6 +149,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
           if (ie == pos) acc[e] += to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
         }
       }
+    }
     }
     if (g.acc) {  // accumulate into the existing gradient (one pass instead of pool + add)
       const uint4 old = *reinterpret_cast<const uint4*>(gx + (long long)pix * g.x_ld + ch * 8);
@@ -293,7 +332,9 @@ static int pool_dt(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t
                    hipStream_t st) {
   const long long big = std::max((long long)g.N * g.OH * g.OW, (long long)g.N * g.H * g.W) * (g.C / 8) + 256LL * 32 * 256;
   const bool i32 = big < 0x7FFFFFFFLL;
-  if (g.k == 3 && i32) return pool_dt_k<DT, 3, int>(kind, dir, in, out, idx, g, st);
+  // DV_NO_POOL_S2=1: max-pool backward on the generic window loop instead of the unrolled 3x3 / s2 path (A/B)
+  static const bool no_s2 = std::getenv("DV_NO_POOL_S2") != nullptr;
+  if (g.k == 3 && i32 && !(no_s2 && kind == 0 && dir == 1)) return pool_dt_k<DT, 3, int>(kind, dir, in, out, idx, g, st);
   if (i32) return pool_dt_k<DT, 0, int>(kind, dir, in, out, idx, g, st);
   return pool_dt_k<DT, 0, long long>(kind, dir, in, out, idx, g, st);
 }

@@ -630,6 +630,25 @@ def test_pool_fp16(native_lib):
         assert yd.dtype == torch.float16 and _rel(yd, yc) < 2e-3 and _rel(gd, gc) < 2e-3
 
 
+@pytest.mark.parametrize("H,W,pad", [(13, 11, 1), (13, 11, 0), (14, 16, 0), (9, 10, 1), (3, 3, 0), (35, 35, 0)])
+def test_maxpool_3x3_s2_bwd(native_lib, H, W, pad):
+    """3x3 / stride-2 max-pool gradient (the unrolled 2 x 2 window path of maxpool_bwd_kernel) vs the
+    CPU path, with ties (first max wins) from a coarse value grid, odd / even sizes, pad 0 and 1."""
+    from deconv_api_amd.ops.autograd import max_pool
+
+    g = torch.Generator().manual_seed(H * 31 + W + pad)
+    x = (torch.randint(-4, 5, (3, H, W, 16), generator=g).float() / 4).to(torch.bfloat16).float()
+    xc = x.clone().requires_grad_(True)
+    yc = max_pool(xc, 3, 2, pad)
+    gy = torch.randn_like(yc).to(torch.bfloat16).float()
+    (gc,) = torch.autograd.grad(yc, xc, gy)
+    xd = x.to(torch.bfloat16).cuda().requires_grad_(True)
+    yd = max_pool(xd, 3, 2, pad)
+    (gd,) = torch.autograd.grad(yd, xd, gy.to(torch.bfloat16).cuda())
+    assert torch.equal(yd.float().cpu(), yc.detach())
+    assert _rel(gd, gc) < 1e-2
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("C,OC,N,H", [(64, 16, 3, 20), (64, 64, 2, 33), (128, 128, 2, 17), (256, 512, 1, 14),
                                       (512, 256, 4, 7), (16, 8, 2, 40)])
