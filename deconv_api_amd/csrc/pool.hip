@@ -16,6 +16,7 @@ struct PoolGeom {
   const float* bias;     // avgpool fwd: + bias[c] (the commuted 1x1 conv's bias), or null
   int relu;              // avgpool fwd: ReLU on the output
   int acc;               // backward: gx += (instead of =) the pooled gradient (Inception max branch)
+  int generic;           // backward: the data-dependent window loop, not the unrolled 3x3 paths (A/B)
 };
 
 template <int DT, int KC, typename IT>
@@ -91,7 +92,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const uint16_t* __rest
     const int h = (int)(pq % g.H);
     const long long n = (long long)(pq / g.H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (KC == 3 && g.s == 2) {
+    if (KC == 3 && g.s == 2 && !g.generic) {
       // 3x3 / stride 2 (every InceptionV3 / ResNet-50 max pool): at most 2 x 2 windows contain
       // (h, w), oh in {ohh - 1, ohh}; all 8 loads are issued (clamped to a real window) before the
       // first use, and summed in the generic loop's (oh, ow) ascending order: bit-identical results
@@ -234,6 +235,36 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __rest
     const int h = (int)(pq % g.H);
     const long long n = (long long)(pq / g.H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (KC == 3 && g.s == 1 && !g.generic) {
+      // 3x3 / stride 1 (the InceptionV3 pool branches): the windows containing (h, w) are
+      // oh = h + pad - 2 .. h + pad; all 9 loads issue (clamped) before the first use, summed in the
+      // generic loop's ascending (oh, ow) order with the same per-window divisor: bit-identical
+      uint4 v[3][3];
+      bool ok[3][3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int oh = h + g.pad - 2 + a;
+        const int ohc = oh < 0 ? 0 : (oh >= g.OH ? g.OH - 1 : oh);
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const int ow = w + g.pad - 2 + b;
+          const int owc = ow < 0 ? 0 : (ow >= g.OW ? g.OW - 1 : ow);
+          ok[a][b] = (unsigned)oh < (unsigned)g.OH && (unsigned)ow < (unsigned)g.OW;
+          v[a][b] = *reinterpret_cast<const uint4*>(gy + ((n * g.OH + ohc) * g.OW + owc) * g.y_ld + ch * 8);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          if (!ok[a][b]) continue;
+          const int oh = h + g.pad - 2 + a, ow = w + g.pad - 2 + b;
+          const float inv = 1.f / (float)(win_count(oh, 1, g.pad, 3, g.H) * win_count(ow, 1, g.pad, 3, g.W));
+          const uint32_t w4[4] = {v[a][b].x, v[a][b].y, v[a][b].z, v[a][b].w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += inv * to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+        }
+    } else {
     const int oh_lo = max(0, (h + g.pad - k + g.s) / g.s), oh_hi = min(g.OH - 1, (h + g.pad) / g.s);
     const int ow_lo = max(0, (w + g.pad - k + g.s) / g.s), ow_hi = min(g.OW - 1, (w + g.pad) / g.s);
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
@@ -248,6 +279,7 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const uint16_t* __rest
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += inv * to_f<DT>((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
       }
+    }
     }
     if (g.acc) {  // accumulate into the existing gradient (one pass instead of pool + add)
       const uint4 old = *reinterpret_cast<const uint4*>(gx + (long long)pix * g.x_ld + ch * 8);
@@ -332,9 +364,7 @@ static int pool_dt(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t
                    hipStream_t st) {
   const long long big = std::max((long long)g.N * g.OH * g.OW, (long long)g.N * g.H * g.W) * (g.C / 8) + 256LL * 32 * 256;
   const bool i32 = big < 0x7FFFFFFFLL;
-  // DV_NO_POOL_S2=1: max-pool backward on the generic window loop instead of the unrolled 3x3 / s2 path (A/B)
-  static const bool no_s2 = std::getenv("DV_NO_POOL_S2") != nullptr;
-  if (g.k == 3 && i32 && !(no_s2 && kind == 0 && dir == 1)) return pool_dt_k<DT, 3, int>(kind, dir, in, out, idx, g, st);
+  if (g.k == 3 && i32) return pool_dt_k<DT, 3, int>(kind, dir, in, out, idx, g, st);
   if (i32) return pool_dt_k<DT, 0, int>(kind, dir, in, out, idx, g, st);
   return pool_dt_k<DT, 0, long long>(kind, dir, in, out, idx, g, st);
 }
@@ -358,7 +388,9 @@ int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* i
   if (y_ld <= 0) y_ld = C;
   if (x_ld % 8 || y_ld % 8 || x_ld < C || y_ld < C) return -1;
   if (acc && dir != 1) return -1;
-  const PoolGeom g{N, H, W, C, OH, OW, k, s, pad, x_ld, y_ld, bias, relu, acc};
+  // DV_NO_POOL_UNROLL=1 (read per call): backward passes on the generic window loop (A/B, bit-identity tests)
+  const int generic = std::getenv("DV_NO_POOL_UNROLL") != nullptr;
+  const PoolGeom g{N, H, W, C, OH, OW, k, s, pad, x_ld, y_ld, bias, relu, acc, generic};
   return dtype == DT_F16 ? pool_dt<DT_F16>(kind, dir, in, out, idx, g, st)
                          : pool_dt<DT_BF16>(kind, dir, in, out, idx, g, st);
 }

@@ -649,6 +649,33 @@ def test_maxpool_3x3_s2_bwd(native_lib, H, W, pad):
     assert _rel(gd, gc) < 1e-2
 
 
+@pytest.mark.parametrize("s,pad", [(1, 1), (1, 0), (2, 0), (2, 1)])
+@pytest.mark.parametrize("kind", ["max", "avg"])
+def test_pool_bwd_unrolled_bit_identical(native_lib, monkeypatch, kind, s, pad):
+    """The unrolled 3x3 backward paths (max: stride 2, avg: stride 1) against the generic window loop
+    (DV_NO_POOL_UNROLL=1, read per call): bit-identical gradients; and both against the CPU path."""
+    from deconv_api_amd.ops.autograd import avg_pool, max_pool
+
+    fn = max_pool if kind == "max" else avg_pool
+    g = torch.Generator().manual_seed(7 * s + pad)
+    x = (torch.randint(-4, 5, (2, 17, 12, 24), generator=g).float() / 4).to(torch.bfloat16).float()
+    xc = x.clone().requires_grad_(True)
+    yc = fn(xc, 3, s, pad)
+    gy = torch.randn_like(yc).to(torch.bfloat16).float()
+    (gc,) = torch.autograd.grad(yc, xc, gy)
+
+    def dev_grad():
+        xd = x.to(torch.bfloat16).cuda().requires_grad_(True)
+        (gd,) = torch.autograd.grad(fn(xd, 3, s, pad), xd, gy.to(torch.bfloat16).cuda())
+        return gd
+
+    fast = dev_grad()
+    monkeypatch.setenv("DV_NO_POOL_UNROLL", "1")
+    slow = dev_grad()
+    assert torch.equal(fast, slow)
+    assert _rel(fast, gc) < 1e-2
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("C,OC,N,H", [(64, 16, 3, 20), (64, 64, 2, 33), (128, 128, 2, 17), (256, 512, 1, 14),
                                       (512, 256, 4, 7), (16, 8, 2, 40)])
