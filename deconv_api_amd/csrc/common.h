@@ -106,7 +106,13 @@ __device__ __forceinline__ uint32_t relu_bf2(uint32_t v) {
 // per dword maps every byte to 0xFF exactly where the code equals pos (selector bytes 0..3 index the constant)
 // and an AND applies it: 8 VALU per chunk and position instead of ~28 for per-byte compare/select (the unpool
 // expansions are VALU-bound: round 4 tail launch 4.27 -> 3.93 ms, profiles/bench_c2_r4_unpool_perm_ab.txt).
+// Precondition: code bytes are 2x2-window positions 0..3 (every switch-code producer writes those). v_perm_b32
+// selector bytes 8..15 would select sign-replicated bytes and >= 13 yield 0xFF, i.e. KEEP the value, where
+// the old compare zeroed it; the codes are masked to 2 bits first (one VALU per dword) so an out-of-range
+// byte can never select a value.
 __device__ __forceinline__ uint4 unpool_spread(uint2 codes) {
+  codes.x &= 0x03030303u;
+  codes.y &= 0x03030303u;
   return make_uint4(__builtin_amdgcn_perm(0u, codes.x, 0x01010000u), __builtin_amdgcn_perm(0u, codes.x, 0x03030202u),
                     __builtin_amdgcn_perm(0u, codes.y, 0x01010000u), __builtin_amdgcn_perm(0u, codes.y, 0x03030202u));
 }

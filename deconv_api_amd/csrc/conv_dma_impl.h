@@ -1033,7 +1033,23 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
 // config-2 shape. Measured and removed: the fragment pipeline alone in the non-persistent kernel
 // (-2 % .. +2 %, noise) and the next step's DMA pieces issued one per MFMA group instead of all
 // after the first reads (-3 % .. +3 % vs this kernel, shape-dependent).
-template <int DT, int BN_ = 256, int BM_ = 256>
+//
+// UNP = true: the max-unpool-out epilogue (the deconvnet's block{3,4,5}_conv1.down, which write the
+// 2x-upsampled map with each value at its switch position and zeros elsewhere). Round 4 tried the
+// register-transposed form (each lane's 4 channels stored to the 4 window positions as 8-B stores):
+// bit-identical but config 2 -3 %, because 8-B stores to every other pixel touch 32-B pieces of many
+// lines. Here each wave stages its 128 x 64 C tile through a private 4 KiB slice of the LDS stage the
+// last K step just released (32 rows per pass, 4 passes), reads it back as 16-B chunks (8 lanes per
+// row: every unpooled store instruction writes 8 whole 128-B lines) and stores value-or-zero to the
+// 4 window positions. The switch codes of all 16 of a lane's rows are loaded before the first pass.
+// One workgroup barrier per tile (after the last pass's LDS reads) keeps the next tile's first DMA
+// into that stage behind every wave's reads; the stores drain behind the next tile's first K step.
+// LDS layout per wave slice: row r (128 B) holds its 8 chunks at chunk ^ 2 (r & 3): the quad-
+// transposed ds_write_b64 of 4 rows x 4 column groups hits 16 distinct 8-B slots per lane group, and
+// each lane reads the chunk physically at (lane & 7) of row lane >> 3 (conflict-free ds_read_b128).
+// SV (store variant, timing experiments through DV_KW3_VAR): 0 = default, 1 = no epilogue stores (ablation:
+// wrong outputs), 2 = non-temporal (nt) epilogue stores.
+template <int DT, int BN_ = 256, int BM_ = 256, bool UNP = false, int SV = 0>
 __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, int tiles_n, int ntiles) {
   constexpr int BN = BN_, BM = BM_, NW = 8;
   constexpr int WN = BN / 64, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
@@ -1216,6 +1232,106 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
     float bias[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) bias[j] = a.bias ? a.bias[cn0 + wn * FN * 16 + j * 16 + cl] : 0.f;
+    if constexpr (UNP) {
+      static_assert(FN == 4 && FM % 2 == 0 && A_BYTES >= NW * 4096, "KW3P unpool: 128 x 64 wave tiles, 4 KiB slices");
+      uint8_t* wreg = smem + 2 * B_BYTES + ((g & 1) ^ 1) * A_BYTES + wave * 4096;
+      const int rl = lane >> 3, pc = lane & 7, lch = pc ^ ((rl & 3) << 1);
+      const int gcol = cn0 + wn * FN * 16 + lch * 8;
+      const int mb = cm0 + wm * FM * 16 + rl;  // this lane's rows: mb + 8 k, k = 0 .. 2 FM - 1
+      const int nb = mb / HW, remb = mb - nb * HW, ohb = remb / W, owb = remb - ohb * W;
+      const int ndb = nb / a.ucode_div, nrb = nb - ndb * a.ucode_div;
+      // step (n, oh, ow) and (n / ucode_div, n % ucode_div) by 8 rows (host: W >= 8)
+      auto step8 = [&](int& n, int& nd, int& nr, int& oh, int& ow) {
+        ow += 8;
+        if (ow >= W) {
+          ow -= W;
+          if (++oh == H) {
+            oh = 0;
+            ++n;
+            if (++nr == a.ucode_div) {
+              nr = 0;
+              ++nd;
+            }
+          }
+        }
+      };
+      uint2 cd[2 * FM];
+      {
+        int n = nb, nd = ndb, nr = nrb, oh = ohb, ow = owb;
+#pragma unroll
+        for (int k = 0; k < 2 * FM; ++k) {
+          cd[k] = make_uint2(0u, 0u);
+          if (mb + 8 * k < a.M)
+            cd[k] = *reinterpret_cast<const uint2*>(a.ucode + ((long long)nd * HW + oh * W + ow) * a.OC + gcol);
+          step8(n, nd, nr, oh, ow);
+        }
+      }
+      uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+      int n = nb, nd = ndb, nr = nrb, oh = ohb, ow = owb;
+#pragma unroll
+      for (int p = 0; p < FM / 2; ++p) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int i = 2 * p + ii;
+            const bool rl_ = pre_relu && relu_at(a, cn0 + wn * FN * 16 + j * 16 + cl);
+            float f0 = acc[i][j][0] + bias[j], f1 = acc[i][j][1] + bias[j], f2 = acc[i][j][2] + bias[j],
+                  f3 = acc[i][j][3] + bias[j];
+            if (rl_) {
+              f0 = fmaxf(f0, 0.f);
+              f1 = fmaxf(f1, 0.f);
+              f2 = fmaxf(f2, 0.f);
+              f3 = fmaxf(f3, 0.f);
+            }
+            const uint32_t p0 = pack2<DT>(f0, f1), p1 = pack2<DT>(f2, f3);
+            const uint32_t keep = ce ? p1 : p0;
+            const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(ce ? p0 : p1), 0xB1, 0xF, 0xF, false);
+            const uint32_t lo = ce ? recv : keep, hi = ce ? keep : recv;
+            const uint32_t d0 = (lo & 0xFFFFu) | (hi << 16), d1 = (lo >> 16) | (hi & 0xFFFF0000u);
+            const uint32_t recv2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(cu ? d0 : d1), 0x4E, 0xF, 0xF, false);
+            const int lr = ii * 16 + rsub, lc = j * 16 + csub;
+            *reinterpret_cast<uint2*>(wreg + lr * 128 + (((lc >> 3) ^ ((lr & 3) << 1)) << 4) + (lc & 4) * 2) =
+                make_uint2(cu ? recv2 : d0, cu ? d1 : recv2);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: this wave's writes before its reads
+        uint4 cv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) cv[t] = *reinterpret_cast<const uint4*>(wreg + (t * 8 + rl) * 128 + pc * 16);
+        if (p == FM / 2 - 1) {  // every wave's reads of the stage done before the next tile's DMA into it
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int k = 4 * p + t;
+          if (mb + 8 * k < a.M) {
+            const uint4 sp = unpool_spread(cd[k]);
+            const long long ob = (((long long)n * 2 * H + 2 * oh) * 2 * W + 2 * ow) * a.out_ld + gcol;
+#pragma unroll
+            for (int pos = 0; pos < 4; ++pos) {
+              const long long po = ob + (long long)((pos >> 1) * 2 * W + (pos & 1)) * a.out_ld;
+              if constexpr (SV == 1) {
+                const uint4 pv = unpool_pick_s(cv[t], sp, (uint32_t)pos);
+                asm volatile("" ::"v"(pv.x), "v"(pv.y), "v"(pv.z), "v"(pv.w), "v"((uint32_t)po));
+              } else if constexpr (SV == 2) {
+                typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_nt;
+                const uint4 pv = unpool_pick_s(cv[t], sp, (uint32_t)pos);
+                __builtin_nontemporal_store(u32x4_nt{pv.x, pv.y, pv.z, pv.w}, reinterpret_cast<u32x4_nt*>(out + po));
+              } else if (DV_BOUNDS(po, 8, a.out_elems, "kw3p unpool-out store")) {
+                *reinterpret_cast<uint4*>(out + po) = unpool_pick_s(cv[t], sp, (uint32_t)pos);
+              }
+            }
+          }
+          step8(n, nd, nr, oh, ow);
+        }
+      }
+      if (!more) break;
+      v = vnext;
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int gcol = cn0 + wn * FN * 16 + j * 16 + cl;
@@ -1243,7 +1359,10 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
         const int col = cn0 + wn * FN * 16 + j * 16 + csub;
         const uint32_t off = row < a.M ? ((uint32_t)row * (uint32_t)a.out_ld + (uint32_t)col) * 2u : kOOB;
         typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{w0, w1}, orr, (int)off, 0, 0);
+        if constexpr (SV == 1)
+          asm volatile("" ::"v"(w0), "v"(w1), "v"(off));
+        else
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{w0, w1}, orr, (int)off, 0, SV == 2 ? 2 : 0);
       }
     }
     if (!more) break;
@@ -1266,11 +1385,24 @@ static int kw3_mode() {
   const char* e = std::getenv("DV_KW3");
   return e ? std::atoi(e) : 1;
 }
-// DV_KW3_VAR: the KW3 main-loop variant (conv_dma_kw3_kernel VAR; 8 / 9 are timing ablations that
-// produce wrong outputs, tools/kw3_ab.py only). Read per launch.
+// DV_KW3_VAR: the KW3 main-loop variant (conv_dma_kw3_kernel VAR; 8 / 9 and 10 (KW3P without stores) are
+// timing ablations that produce wrong outputs; 11 = KW3P with nt stores, tools/kw3_ab.py only: they also need DV_ALLOW_WRONG_ABLATION=1, so a stray
+// DV_KW3_VAR in a serving process cannot corrupt convs; without it they fall back to the default).
+// Read per launch.
 static int kw3_var() {
   const char* e = std::getenv("DV_KW3_VAR");
-  return e ? std::atoi(e) : kKw3DefaultVar;
+  const int v = e ? std::atoi(e) : kKw3DefaultVar;
+  if (v == 8 || v == 9 || v == 10) {
+    static bool warned = false;
+    if (std::getenv("DV_ALLOW_WRONG_ABLATION") == nullptr) {
+      if (!warned) fprintf(stderr, "deconv_api_amd: DV_KW3_VAR=%d ignored (needs DV_ALLOW_WRONG_ABLATION=1)\n", v);
+      warned = true;
+      return kKw3DefaultVar;
+    }
+    if (!warned) fprintf(stderr, "deconv_api_amd: DV_KW3_VAR=%d: timing ablation, outputs are WRONG\n", v);
+    warned = true;
+  }
+  return v;
 }
 
 // tiles_m_limit > 0: launch only the first tiles_m_limit row tiles (kw3_split's full rounds)
@@ -1295,15 +1427,36 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
     const int var = kw3_var();
     const dim3 grid((unsigned)nwg);
     if constexpr (EPI == CONV_E_BF16) {
+      // VAR 10 / 11 (bf16 only): KW3P without epilogue stores (timing ablation) / with nt stores
+      const bool pvar = var == 2 || (DT == DT_BF16 && (var == 10 || var == 11));
+      auto launch_p = [&](auto unp) -> int {
+        constexpr bool U = decltype(unp)::value;
+        const unsigned g = (unsigned)(nwg < (long long)num_cus() ? nwg : (long long)num_cus());
+        if constexpr (DT == DT_BF16) {
+          if (var == 10) {
+            hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 1>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+            return (int)hipGetLastError();
+          }
+          if (var == 11) {
+            hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 2>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+            return (int)hipGetLastError();
+          }
+        }
+        hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+        return (int)hipGetLastError();
+      };
       // persistent KW3P: plain 16-bit epilogue only (its register-transpose stores write exactly
       // the C tile), output addressable by a 31-bit buffer offset, one workgroup per CU
-      if (var == 2 && a.res == nullptr && a.emask == nullptr && !a.accumulate && a.ucode == nullptr &&
+      if (pvar && a.res == nullptr && a.emask == nullptr && !a.accumulate && a.ucode == nullptr &&
           a.out2 == nullptr && a.OC == a.OCpad && a.OC % 4 == 0 && a.out_ld % 4 == 0 &&
-          a.out_elems * 2 < 0x7FFFFFF0LL && a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19)) {
-        const unsigned g = (unsigned)(nwg < (long long)num_cus() ? nwg : (long long)num_cus());
-        hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
-        return (int)hipGetLastError();
-      }
+          a.out_elems * 2 < 0x7FFFFFF0LL && a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19))
+        return launch_p(std::false_type{});
+      // persistent KW3P with the LDS-sliced max-unpool-out epilogue (DV_NO_KW3P_UNPOOL=1: the
+      // non-persistent KW3 kernel's workgroup-staged one, A/B; read per launch)
+      if (pvar && a.ucode != nullptr && a.res == nullptr && a.emask == nullptr && !a.accumulate &&
+          a.out2 == nullptr && a.OC == a.OCpad && a.OC % 8 == 0 && a.out_ld % 8 == 0 && a.W >= 8 && a.ucode_div >= 1 &&
+          a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19) && std::getenv("DV_NO_KW3P_UNPOOL") == nullptr)
+        return launch_p(std::true_type{});
     }
     if constexpr (DT == DT_BF16 && EPI == CONV_E_BF16) {
       if (var == 8 || var == 9) {

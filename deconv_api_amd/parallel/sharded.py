@@ -51,6 +51,7 @@ keeps beating) is only caught by the collective deadline (``ack_timeout``), not 
 """
 from __future__ import annotations
 
+import contextlib
 import threading
 import time
 from dataclasses import dataclass, field
@@ -188,6 +189,9 @@ class ShardedRunner:
         # stream; the gather runs on ``comm_stream`` behind that batch's event only
         self.slots: List[Optional[torch.Tensor]] = [None, None]
         self.comm_stream = torch.cuda.Stream(info.device) if cuda else None
+        # a batch's input path (upload + resize + scatter) runs on its own stream, never behind the
+        # previous batch's engine work on the compute stream nor behind a gather on comm_stream
+        self.in_stream = torch.cuda.Stream(info.device) if cuda else None
         self._bid = 0
 
     @property
@@ -253,6 +257,11 @@ class ShardedRunner:
                     work.wait()  # re-raises a transport error (e.g. Gloo: peer closed its socket)
                     return
             except RuntimeError as e:
+                if isinstance(work, _EventWork):
+                    # a local GPU fault (this rank's own kernels, e.g. an illegal access surfacing in
+                    # hipEventQuery) is NOT a peer loss: degrading the group and restarting the dream
+                    # on a faulted context would hide it; it propagates as the local error it is
+                    raise
                 if follower:
                     raise PeerLost([]) from e
                 raise PeerLost(self._which_dead()) from e
@@ -337,6 +346,9 @@ class ShardedRunner:
 
     def _after_reform(self) -> None:
         self.slots = [None, None]
+        self._reset_dream_state()
+
+    def _reset_dream_state(self) -> None:
         self._dreams.clear()
         for dd in self._dream_tiled.values():  # unit plans / packs / graphs were for the old world
             dd._tgraphs.clear()
@@ -422,6 +434,7 @@ class ShardedRunner:
         for o in range(octaves):
             with self._cmd_lock:  # released between octaves: deconv batches interleave
                 if ctl.epoch != epoch:  # another command re-formed the group meanwhile
+                    self._reset_dream_state()  # (done by its _reform already; idempotent)
                     raise _DreamRestart()
                 try:
                     seq = ctl.post_cmd({"op": "dream_oct", "did": did, "o": o})
@@ -439,13 +452,32 @@ class ShardedRunner:
         per = shard_sizes(n, self.world)[0]
         ctl = self.ctl
         seq = ctl.post_cmd({"op": "run", "layer": b.layer, "n": n, "per": per, "b": b.bid})
-        u8, b.staged = self._resize_u8(b.images, per * self.world)  # overlaps the followers' acks
-        ctl.wait_acks("ready", seq)
-        ctl.go("go1", seq)
-        shard = torch.empty(per, self.S, self.S, 3, dtype=torch.uint8, device=u8.device)
-        self._await(dist.scatter(shard, scatter_list=list(u8.chunk(self.world)), src=0, async_op=True), "scatter")
+        # upload + resize + scatter on the side stream: on the compute stream they would queue behind
+        # the previous batch's engine work, and the host (polling the scatter below) could enqueue
+        # this batch's engine only after that finished - an idle GPU gap per batch with two in flight
+        with self._side():
+            u8, b.staged = self._resize_u8(b.images, per * self.world)  # overlaps the followers' acks
+            ctl.wait_acks("ready", seq)
+            ctl.go("go1", seq)
+            shard = torch.empty(per, self.S, self.S, 3, dtype=torch.uint8, device=u8.device)
+            work = dist.scatter(shard, scatter_list=list(u8.chunk(self.world)), src=0, async_op=True)
+        self._await(work, "scatter")
+        shard = self._to_compute(shard)
         self.faults.on_batch()
         b.mos, b.ev = self._keep(b.bid, self._engine(self._preprocess(shard), b.layer).contiguous())
+
+    def _side(self):
+        """Stream context for a batch's input path (resize + scatter): the side stream on a GPU."""
+        return torch.cuda.stream(self.in_stream) if self.in_stream is not None else contextlib.nullcontext()
+
+    def _to_compute(self, t: torch.Tensor) -> torch.Tensor:
+        """Hand a tensor produced on the side stream (its collective polled complete) to the compute
+        stream: stream order for the kernels, allocator lifetime for its block."""
+        if self.in_stream is not None and t.is_cuda:
+            cur = torch.cuda.current_stream(t.device)
+            cur.wait_stream(self.in_stream)
+            t.record_stream(cur)
+        return t
 
     def _gather_cmd(self, b: Batch) -> None:
         ctl = self.ctl
@@ -492,14 +524,19 @@ class ShardedRunner:
         return h[2].numpy()
 
     def ping(self) -> bool:
-        """Idle liveness check: re-forms the group if a follower stopped heartbeating."""
+        """Idle liveness check: re-forms the group if a follower stopped heartbeating. Under the
+        command lock (a dream between octaves may hold the group: its own _await and this must not
+        re-form concurrently) and through ``_reform``, so ``_after_reform`` drops every per-world
+        state (dream unit plans, packs, octave graphs with captured collectives)."""
         if self.world == 1 or self.ctl is None:
             return True
-        dead = self.ctl.stale()
-        if dead:
-            self.ctl.reform(dead)
-            self.reforms += 1
-            return False
+        with self._cmd_lock:
+            if self.world == 1:
+                return True
+            dead = self.ctl.stale()
+            if dead:
+                self._reform(PeerLost(dead))
+                return False
         return True
 
     def stop(self):
@@ -532,8 +569,11 @@ class ShardedRunner:
                     ctl.ack("ready", seq)
                     self.faults.at("ready", runs)  # fault window: acked, then gone before the scatter
                     self._go(ctl, "go1", seq)
-                    shard = torch.empty(msg["per"], self.S, self.S, 3, dtype=torch.uint8, device=dev)
-                    self._await(dist.scatter(shard, scatter_list=None, src=0, async_op=True), "scatter", True)
+                    with self._side():  # not queued behind the previous batch's engine work (_run_cmd)
+                        shard = torch.empty(msg["per"], self.S, self.S, 3, dtype=torch.uint8, device=dev)
+                        work = dist.scatter(shard, scatter_list=None, src=0, async_op=True)
+                    self._await(work, "scatter", True)
+                    shard = self._to_compute(shard)
                     self.faults.on_batch()
                     mos = self._engine(self._preprocess(shard), msg["layer"]).contiguous()
                     pending[msg["b"]] = self._keep(msg["b"], mos)

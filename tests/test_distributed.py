@@ -423,9 +423,19 @@ def _worker_dream_fault(rank, world, port, q, fault, interleave):
             rng = np.random.default_rng(2)
             img = torch.from_numpy(rng.integers(0, 256, (1, 160, 176, 3), dtype=np.uint8))
             imgs = [rng.integers(0, 256, (30, 28, 3), dtype=np.uint8) for _ in range(3)]
-            octaves = 3 if interleave else 2
+            octaves = 3 if interleave is True else 2
             t = {}
-            if interleave:
+            stop_ping = threading.Event()
+            if interleave == "ping":  # the service's idle liveness check, running beside the dream
+
+                def pinger():
+                    while not stop_ping.is_set():
+                        runner.ping()
+                        time.sleep(0.05)
+
+                pth = threading.Thread(target=pinger)
+                pth.start()
+            if interleave is True:
                 res = {}
 
                 def deconv():
@@ -440,8 +450,11 @@ def _worker_dream_fault(rank, world, port, q, fault, interleave):
             got = runner.dream(img, "resnet50", octaves, 2)
             t["dream_done"] = time.time()
             t["dream_s"] = t["dream_done"] - t0
+            stop_ping.set()
+            if interleave == "ping":
+                pth.join()
             mos_ok = None
-            if interleave:
+            if interleave is True:
                 th.join()
                 want_mos = ShardedRunner(eng, type(info)(), image_size=32)._local("block2_conv1", imgs).numpy()
                 mos_ok = bool(np.array_equal(res["mos"], want_mos)) and t["deconv_done"] < t["dream_done"]
@@ -464,14 +477,19 @@ def _worker_dream_fault(rank, world, port, q, fault, interleave):
         q.put((rank, traceback.format_exc(), None, None, None, None, None))
 
 
-@pytest.mark.parametrize("fault,interleave", [("exit_octave@2/rank=2", False), ("", True)])
+@pytest.mark.parametrize("fault,interleave", [("exit_octave@2/rank=2", False), ("", True),
+                                             ("exit_octave@2/rank=2", "ping")])
 def test_dream_fault_and_interleave(fault, interleave):
     """Multi-rank /deepdream (world 3, one command per octave, every collective polled):
     * a follower killed inside the dream's 2nd octave: rank 0 detects it (the octave's polled
       collectives / heartbeats), the survivors re-form, and the dream restarts and completes on
       world 2, equal to the one-process dream up to rounding;
     * no fault: a deconv batch submitted while a 3-octave dream runs completes BEFORE the dream
-      (the FIFO command lock is released between octaves) and equals the single-process result."""
+      (the FIFO command lock is released between octaves) and equals the single-process result;
+    * the same fault with the service's ``ping()`` polling beside the dream: whichever of the two
+      detects the loss re-forms the group exactly once (ping takes the command lock and re-forms
+      through ``_reform``, which drops the dream's per-world tiled state), and the restarted dream
+      is equal to the one-process dream."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

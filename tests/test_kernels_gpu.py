@@ -339,6 +339,40 @@ def test_conv_kw3_persistent(native_lib, monkeypatch, N, H, W, C, OC, dt):
         assert _rel(outs["2"][: min(N, 8)], ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C,OC,div,dt", [(600, 14, 14, 64, 256, 4, torch.bfloat16),
+                                                (90, 28, 28, 96, 256, 2, torch.bfloat16),
+                                                (80, 56, 56, 32, 128, 4, torch.bfloat16),
+                                                (131, 10, 12, 32, 512, 1, torch.bfloat16),
+                                                (300, 20, 20, 64, 256, 3, torch.float16)])
+def test_conv_kw3p_unpool_out(native_lib, monkeypatch, N, H, W, C, OC, div, dt):
+    """Persistent KW3 with the LDS-sliced max-unpool-out epilogue (conv_dma_kw3p_kernel<.., UNP>, the
+    default for the deconvnet's block{3,4,5}_conv1.down): several tiles per workgroup, tiles crossing
+    image rows and images, an M tail (N*H*W not a multiple of the tile), the 512 x 128 tile, code_div
+    1..4, odd K-step counts (C = 96). Equal BIT FOR BIT to the non-persistent KW3 workgroup-staged
+    unpool epilogue (DV_NO_KW3P_UNPOOL=1: same accumulation order, same rounding), nothing off the
+    switch positions, and the fp32 reference up to bf16 rounding."""
+    monkeypatch.setenv("DV_KW3", "2")
+    monkeypatch.setenv("DV_NO_SPLITK", "1")
+    g = torch.Generator().manual_seed(N + W)
+    x = torch.relu(torch.randn(N, H, W, C, generator=g)).to(dt)
+    code = torch.randint(0, 4, (N // div, H, W, OC), generator=g, dtype=torch.uint8)
+    cw = _cw(OC, C, bias=False)
+    xd, cwd, cd = x.to(DEV), cw.to_device(DEV, dt), code.to(DEV)
+    kw = dict(relu=True, use_bias=False, unpool_out=cd, unpool_div=div)
+    got = ops.conv2d(xd, cwd, **kw)
+    monkeypatch.setenv("DV_NO_KW3P_UNPOOL", "1")
+    base = ops.conv2d(xd, cwd, **kw)
+    monkeypatch.delenv("DV_NO_KW3P_UNPOOL")
+    assert got.shape == (N, 2 * H, 2 * W, OC)
+    assert torch.equal(got, base)
+    plain = ops.conv2d(xd, cwd, relu=True, use_bias=False)
+    want = ops.unpool_ref(plain, cd, div)
+    assert ((got != 0) & (want == 0)).sum() == 0  # nothing lands off the switch position
+    n = 2 * div
+    ref = ops.conv2d(x[:n].float(), cw, relu=True, use_bias=False, unpool_out=code[: n // div], unpool_div=div)
+    assert _rel(got[:n], ref) < 1e-2
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N,H,W,C,OC", [(5, 7, 7, 64, 256), (3, 14, 13, 96, 512), (2, 28, 28, 256, 256), (1, 9, 1, 32, 256),
                                         (4, 10, 9, 64, 128), (2, 56, 56, 256, 128)])

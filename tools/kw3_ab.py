@@ -31,6 +31,10 @@ CASES = {
     "b3c1down": (1024, 56, 56, 256, 128),   # block3_conv1.down: 512 x 128 KW3 tile
     "b4fwd": (256, 28, 28, 512, 512),       # block4_conv{2,3} forward
     "b5fwd": (256, 14, 14, 512, 512),       # block5 forward (tail-split KW3)
+    # unpool-out conv-downs (suffix "unp": max-unpooled output, switch codes shared by 4 signals)
+    "b5c1unp": (1024, 14, 14, 512, 512),    # block5_conv1.down -> 28^2
+    "b4c1unp": (1024, 28, 28, 512, 256),    # block4_conv1.down -> 56^2
+    "b3c1unp": (1024, 56, 56, 256, 128),    # block3_conv1.down -> 112^2 (512 x 128 tile)
 }
 
 
@@ -41,6 +45,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
+    os.environ.setdefault("DV_ALLOW_WRONG_ABLATION", "1")  # VAR 8 / 9 are wrong-output timing ablations
     ops.native.load()
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in a.vars.split(",")]
@@ -51,9 +56,14 @@ def main():
         cw = ConvWeights(w, None, "fwd").to_device(dev)
         x = (torch.rand(N, H, W, C, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         out = {v: torch.empty(N, H, W, OC, dtype=torch.bfloat16, device=dev) for v in variants}
+        unp = case.endswith("unp")
+        code = torch.randint(0, 4, (N // 4, H, W, OC), device=dev, dtype=torch.uint8, generator=g) if unp else None
 
         def run(v):
             os.environ["DV_KW3_VAR"] = str(v)
+            if unp:  # a fresh unpooled output per call (as the engine does)
+                out[v] = ops.conv2d(x, cw, relu=True, use_bias=False, unpool_out=code, unpool_div=4)
+                return out[v]
             return ops.conv2d(x, cw, relu=True, use_bias=False, out=out[v])
 
         for v in variants:  # warm up every variant (and check the real ones agree)
