@@ -153,17 +153,15 @@ def save(model, path: str) -> None:
 
 
 def load_weights(model, path: str):
-    """``path``: folded ``.safetensors`` (this module's format) or a Keras ``.h5`` (needs h5py)."""
+    """``path``: folded ``.safetensors`` (this module's format) or a Keras ``.h5`` (h5py when importable,
+    else the dependency-free ``models/h5lite.py`` reader)."""
     if path.endswith(".safetensors"):
         from safetensors.torch import load_file
 
         return apply_state(model, load_file(path))
-    try:
-        import h5py
-    except ImportError as e:  # pragma: no cover - environment dependent
-        raise ImportError("reading Keras .h5 needs h5py; convert once elsewhere with "
-                          "`python -m deconv_api_amd.models.dream_import MODEL in.h5 out.safetensors`") from e
-    with h5py.File(path, "r") as f:
+    from .h5lite import open_h5
+
+    with open_h5(path) as f:
         return apply_state(model, state_from_h5_like(f, model))
 
 

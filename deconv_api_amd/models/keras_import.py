@@ -8,9 +8,10 @@ order our NHWC flatten produces), so the import is a pure name mapping; the devi
 models/vgg16.py does every transpose.
 
 ``h5py`` is not installed in this environment; the reader is duck-typed over any mapping with the
-h5py interface (``f[name]``, ``.attrs``, ``np.asarray(dataset)``) so it is testable without it,
-and ``load_keras_vgg16_h5`` imports h5py lazily. ``python -m deconv_api_amd.models.keras_import
-in.h5 out.safetensors`` converts once on a machine that has h5py.
+h5py interface (``f[name]``, ``.attrs``, ``np.asarray(dataset)``), and ``load_keras_vgg16_h5``
+opens the file with h5py when it is importable and with the framework's own dependency-free HDF5
+reader (``models/h5lite.py``) otherwise, so ``VGG16.load("x.h5")`` works in the shipped container.
+``python -m deconv_api_amd.models.keras_import in.h5 out.safetensors`` converts once.
 """
 from __future__ import annotations
 
@@ -62,14 +63,9 @@ def keras_state_from_h5_like(f: Mapping) -> Dict[str, torch.Tensor]:
 
 
 def load_keras_vgg16_h5(path: str) -> VGG16:
-    try:
-        import h5py  # noqa: F401
-    except ImportError as e:  # pragma: no cover - environment dependent
-        raise ImportError("reading Keras .h5 needs h5py; convert once elsewhere with "
-                          "`python -m deconv_api_amd.models.keras_import in.h5 out.safetensors`") from e
-    import h5py
+    from .h5lite import open_h5
 
-    with h5py.File(path, "r") as f:
+    with open_h5(path) as f:
         sd = keras_state_from_h5_like(f)
     return VGG16.from_state_dict(sd)
 

@@ -135,6 +135,10 @@ class VGG16:
             from safetensors.torch import load_file
 
             return cls.from_state_dict(load_file(path))
+        if path.endswith((".h5", ".hdf5")):  # Keras weights (app/main.py:17's ImageNet file)
+            from .keras_import import load_keras_vgg16_h5
+
+            return load_keras_vgg16_h5(path)
         return cls.from_state_dict(torch.load(path, map_location="cpu", weights_only=True))
 
     @property
