@@ -100,6 +100,20 @@ int64_t conv_group_end() {
   return launches;
 }
 
+// compute units of the current device (cached per device)
+int64_t device_cus() {
+  static std::mutex mu;
+  static std::map<int, int64_t> cache;
+  int dev = 0;
+  check_rc((int)hipGetDevice(&dev), "hipGetDevice");
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int cu = 0;
+  check_rc((int)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+  return cache[dev] = cu > 0 ? cu : 256;
+}
+
 // geom: N,H,W,C, OH,OW,OC,OCpad, KH,KW,stride,pad_h,pad_w, K,Kpad, M, relu,relu_in,accumulate,
 //       code_div, x_ld, mask_ld, out_ld
 void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
@@ -421,6 +435,19 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
         finish_stats();
         return;
       }
+    }
+    // KW3P stream-K workspace (conv_dma_impl.h:kw3_sk_ok decides whether it is used): one fp32 partial-tile
+    // slot + one flag per CU, from the stream-ordered caching allocator (graph-capture safe; concurrent
+    // streams never share one)
+    Tensor skws;
+    const int64_t cus = device_cus();
+    if (ks == 1 && amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16 && !mask.has_value() && a.KH == 3 && a.KW == 3 &&
+        a.stride == 1 && a.pad_h == 1 && a.pad_w == 1 && a.C % 32 == 0 && a.OCpad % 128 == 0 && !a.res && !a.emask &&
+        !a.accumulate && (int64_t)a.M * a.OCpad > cus * dv::kSkSlotFloats && cus <= dv::kSkMaxWg &&
+        std::getenv("DV_NO_KW3_SK") == nullptr) {
+      skws = at::empty({cus * dv::kSkSlotFloats + cus}, x.options().dtype(at::kFloat));
+      a.skw = skws.data_ptr<float>();
+      a.skflag = reinterpret_cast<unsigned*>(a.skw + cus * dv::kSkSlotFloats);
     }
     check_rc(dv::conv_dma_launch(a, (int)amode, (int)epi, cur_stream()), "conv_dma");
     if (ks > 1) check_rc(dv::splitk_reduce_launch(a, (int)epi, cur_stream()), "splitk_reduce");

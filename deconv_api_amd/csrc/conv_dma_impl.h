@@ -25,6 +25,7 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace dv {
@@ -1049,8 +1050,30 @@ __global__ void __launch_bounds__(512) conv_dma_kw3_kernel(const ConvArgs a, int
 // each lane reads the chunk physically at (lane & 7) of row lane >> 3 (conflict-free ds_read_b128).
 // SV (store variant, timing experiments through DV_KW3_VAR): 0 = default, 1 = no epilogue stores (ablation:
 // wrong outputs), 2 = non-temporal (nt) epilogue stores.
-template <int DT, int BN_ = 256, int BM_ = 256, bool UNP = false, int SV = 0>
-__global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, int tiles_n, int ntiles) {
+//
+// SK = true: stream-K. The plain persistent walk (tile v, v + G, ...) ends every workgroup's tiles at the
+// same moment, so the whole chip writes its C tiles in one burst and the next tile's first K step waits
+// for it (tools/kw3_ab.py, VAR 10 = no epilogue stores: 5-9 % faster on the plain config-2 shapes, 10-15 %
+// on the unpool-out ones, profiles/kw3_store_ablation_r5.txt), and a grid of R.f rounds pays a whole
+// round (or a 128 x 128 tail launch, kw3_split) for its fraction f. Here the G = gridDim workgroups of
+// each output-column group (tile_n; the tiles_n groups interleave so the two workgroups sharing a row
+// range sit side by side on one XCD and share its A rows in L2) split the group's tiles_m x nsteps
+// K steps into G / tiles_n equal contiguous ranges: every workgroup does the same work, and its tile
+// boundaries sit at a different K-step phase than its neighbours', so the C-tile stores of the chip
+// are spread over the whole launch. A range of >= nsteps steps (host-checked) starts with at most one
+// partial tile (its tail K steps) and ends with at most one (its head steps): the tail piece is computed
+// first and published as fp32 partial accumulators (write-through sc1 stores, counted drain, barrier,
+// one agent-scope flag store: the MI355X hand-off recipe); the workgroup holding the head finishes it
+// last, polls the flag (bounded), reads the partial with sc1 loads and applies the epilogue to the sum.
+// Split tiles round differently from one-pass accumulation (fp32, tests compare to the reference).
+// EM (epilogue mode): 0 = register-transposed 8-B stores; 1 = max-unpool-out through the per-wave LDS slices
+// (UNP below); 2 = the same LDS slices for the plain output: 16-B stores, every store instruction writes
+// 8 whole 128-B line segments instead of 16 rows x 32 B (the default; DV_KW3P_EPI=reg for mode 0, A/B).
+// Mode 0's scattered 8-B stores cost 9-13 % of a config-2 KW3P launch (a no-store ablation ran 11-15 %
+// faster); mode 2 recovers most of it (profiles/kw3_epi_ab_r5.txt).
+template <int DT, int BN_ = 256, int BM_ = 256, int EM = 0, int SV = 0, bool SK = false>
+__global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, int tiles_n, int ntiles, int use_pre) {
+  constexpr bool UNP = EM == 1, LDSEPI = EM != 0;
   constexpr int BN = BN_, BM = BM_, NW = 8;
   constexpr int WN = BN / 64, FN = 4, WM = NW / WN, FM = BM / (16 * WM);
   constexpr int A_I = kw3_a_i(BM);
@@ -1088,9 +1111,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
   // zero slot (host: H < 4096 and 2 HW + BM < 2^19); one VGPR per slot instead of two
   uint32_t r_po[A_I];
   __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, 16);
-  auto setup = [&](int v) {
-    const int wgid = xcd_remap(v, ntiles);
-    const int tile_n = wgid % tiles_n, tile_m = wgid / tiles_n;
+  auto setup = [&](int tile_m, int tile_n) {
     m0 = a.m_base + tile_m * BM;
     n0 = tile_n * BN;
     const int n_base = (m0 < a.M ? m0 : a.M - 1) / HW;
@@ -1132,13 +1153,40 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
     }
   };
 
-  int v = blockIdx.x;
-  if (v >= ntiles) return;
-  setup(v);
-  issue(0, 0);
+  // segment walk: [k0, k1) K steps of tile (tm, tn); plain persistent: whole tiles v, v + G, ...;
+  // stream-K: this workgroup's contiguous range [u, ue) of its column group's tiles_m x nsteps steps
+  const int tiles_m = ntiles / tiles_n;
+  int tm = 0, tn = 0, k0 = 0, k1 = nsteps, v = blockIdx.x;
+  int ue = 0;    // stream-K: end of this workgroup's step range (host: tiles_m * nsteps < 2^31)
+  int slot = 0;  // stream-K: this workgroup's partial slot (its XCD-remapped index)
+  if constexpr (SK) {
+    slot = xcd_remap(blockIdx.x, gridDim.x);
+    tn = slot % tiles_n;
+    const long long gq = gridDim.x / tiles_n, qi = slot / tiles_n, U = (long long)tiles_m * nsteps;
+    const int u = (int)(qi * U / gq);
+    ue = (int)((qi + 1) * U / gq);
+    tm = u / nsteps;
+    k0 = u - tm * nsteps;
+    k1 = min(nsteps, ue - tm * nsteps);
+  } else {
+    if (v >= ntiles) return;
+    const int wgid = xcd_remap(v, ntiles);
+    tn = wgid % tiles_n;
+    tm = wgid / tiles_n;
+  }
+  setup(tm, tn);
+  issue(k0, 0);
   wait_vm<0>();
   __builtin_amdgcn_s_barrier();
   int g = 0;  // global K step counter: LDS stage parity
+  // PRE (plain epilogue): the previous tile's epilogue issued this segment's step-1 DMA BEFORE its C-tile
+  // stores, so this segment's first K step issues nothing and waits with vmcnt(kPreStores) (the stores
+  // are the youngest vector-memory ops: in-order counting lets them stay in flight). The stores then
+  // have two K steps, not one, to be acknowledged before a wait covers them (tools/kw3_ab.py: KW3P
+  // without stores ran 5-9 % faster; stream-K spreading of the bursts did not recover it)
+  constexpr int kPreStores = FM * FN;  // buffer stores per wave of the plain epilogue (rows past M: kOOB)
+  static_assert(kPreStores <= 63, "vmcnt immediate");
+  bool pre = false;
   for (;;) {
     const int cm0 = m0, cn0 = n0;
     // per-lane A fragment addresses of this tile (stage 0; opaque: one VGPR each, as in KW3)
@@ -1154,8 +1202,24 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
       }
     }
     auto aad = [&](int i, int kw) { return aaddr[i][kw]; };
-    const int vnext = v + (int)gridDim.x;
-    const bool more = vnext < ntiles;
+    // the next segment (its first step is issued by this segment's last K step)
+    int ntm = tm, ntn = tn, nk1 = nsteps, vnext = v;
+    bool more;
+    if constexpr (SK) {
+      const int un = (tm + 1) * nsteps;  // next segment starts at its tile's step 0
+      more = un < ue;
+      ntm = tm + 1;
+      nk1 = min(nsteps, ue - un);
+    } else {
+      vnext = v + (int)gridDim.x;
+      more = vnext < ntiles;
+      if (more) {
+        const int wgid = xcd_remap(vnext, ntiles);
+        ntn = wgid % tiles_n;
+        ntm = wgid / tiles_n;
+      }
+    }
+    const int ck0 = k0, ck1 = k1;
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -1164,7 +1228,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
     // one K step on stage `cur` (its DMAs landed and every wave passed the barrier); `nxt` issues
     // the following step's DMAs behind the first fragment reads; ends with the wait + barrier that
     // make the next step's stage readable
-    auto kstep = [&](int cur, auto nxt) {
+    auto kstep = [&](int cur, auto nxt, bool counted) {
       const int aoff = cur * A_BYTES;
       const uint8_t* Bs = smem + baddr0 + cur * B_BYTES;
       v8 bA[FN], bB[FN], af[FM];
@@ -1209,37 +1273,112 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
       // my next-stage DMAs landed AND every fragment read of this stage returned (the barrier may
       // be scheduled among the last MFMAs: with reads still in flight, another wave's next DMA
       // into this stage could overwrite what they have not fetched yet)
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (counted)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kPreStores) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     };
 #pragma unroll 1
-    for (int k = 0; k + 1 < nsteps; ++k, ++g) kstep(g & 1, [&] { issue(k + 1, (g & 1) ^ 1); });
+    for (int k = ck0; k + 1 < ck1; ++k, ++g) {
+      const bool first_pre = pre && k == ck0;
+      kstep(
+          g & 1,
+          [&] {
+            if (!first_pre) issue(k + 1, (g & 1) ^ 1);
+          },
+          first_pre);
+    }
     // the last step issues the next tile's first step (gather state computed before its fragments
     // are live): those operands land behind this step's MFMAs, its trailing wait covers them, and
     // the epilogue's stores below are younger than them
-    if (more) setup(vnext);
-    kstep(g & 1, [&] {
-      if (more) issue(0, (g & 1) ^ 1);
-    });
-    ++g;
-    // ---- epilogue: register transpose -> 8-B stores (no LDS, no barrier) ----
-    // lane roles (see the header; derived here, not kept live across the K loop): this lane stores
-    // row rsub of each 16-row block, 4 columns from csub
-    const int cl = lane & 15, ce = cl & 1, cu = (cl >> 1) & 1;
-    const int rsub = (lane >> 4) * 4 + ce * 2 + cu, csub = cl & ~3;
-    const bool pre_relu = a.relu != 0;
-    // (every bias load before the first store: a load issued behind stores would wait for them)
+    if (more) setup(ntm, ntn);
+    // this tile's bias, loaded before the last K step (whose vmcnt(0) covers it): a load issued after
+    // the PRE DMA below would make the epilogue wait for that DMA
+    const int cl = lane & 15;
     float bias[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) bias[j] = a.bias ? a.bias[cn0 + wn * FN * 16 + j * 16 + cl] : 0.f;
-    if constexpr (UNP) {
-      static_assert(FN == 4 && FM % 2 == 0 && A_BYTES >= NW * 4096, "KW3P unpool: 128 x 64 wave tiles, 4 KiB slices");
+    kstep(
+        g & 1,
+        [&] {
+          if (more) issue(0, (g & 1) ^ 1);
+        },
+        false);
+    ++g;
+    // advance the walk (the epilogue below uses cm0 / cn0 / ck0 / ck1 only)
+    tm = ntm;
+    tn = ntn;
+    v = vnext;
+    k0 = 0;
+    k1 = nk1;
+    // step 1 of the next segment into the stage the last K step just released (every wave passed its
+    // barrier), ahead of the epilogue's stores (see PRE above); the UNP epilogue stages through that stage
+    pre = !LDSEPI && SV != 1 && use_pre && more && nk1 > 1;
+    if (pre) issue(1, (g & 1) ^ 1);
+    if constexpr (SK) {
+      typedef __attribute__((ext_vector_type(4))) float f32x4v;
+      const __amdgpu_buffer_rsrc_t skr = make_rsrc(a.skw, (uint64_t)gridDim.x * kSkSlotFloats * 4);
+      // this wave's slice of a slot: [wave][i][j][lane] f32x4 (1 KiB per (i, j): coalesced)
+      auto sk_off = [&](int s_, int i, int j) {
+        return (uint32_t)(((((long long)s_ * NW + wave) * FM + i) * FN + j) * 64 + lane) * 16u;
+      };
+      if (ck0 > 0) {  // tail piece (this range's first segment): publish the partial accumulators
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4v, acc[i][j]), skr, (int)sk_off(slot, i, j), 0,
+                                                   16 /* sc1: write-through */);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its partial stores
+        __syncthreads();
+        if (tid == 0)
+          __hip_atomic_store(a.skflag + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!more) break;
+        continue;
+      }
+      if (ck1 < nsteps) {  // head piece (this range's last segment): add the tail's partial, then the epilogue
+        const int src = (slot + tiles_n) % (int)gridDim.x;  // the next workgroup of this column group
+        if (tid == 0) {
+          // bounded poll (~seconds): a lost hand-off must not hang the GPU (it would corrupt this tile)
+          for (int it = 0; it < (1 << 22); ++it) {
+            if (__hip_atomic_load(a.skflag + src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) break;
+            __builtin_amdgcn_s_sleep(8);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load moves above the poll
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          f32x4v pv[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            pv[j] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(skr, (int)sk_off(src, i, j), 0,
+                                                                                  16 /* sc1 */));
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            acc[i][j][0] += pv[j][0];
+            acc[i][j][1] += pv[j][1];
+            acc[i][j][2] += pv[j][2];
+            acc[i][j][3] += pv[j][3];
+          }
+        }
+      }
+    }
+    // ---- epilogue: register transpose -> 8-B stores (no LDS, no barrier) ----
+    // lane roles (see the header; derived here, not kept live across the K loop): this lane stores
+    // row rsub of each 16-row block, 4 columns from csub
+    const int ce = cl & 1, cu = (cl >> 1) & 1;
+    const int rsub = (lane >> 4) * 4 + ce * 2 + cu, csub = cl & ~3;
+    const bool pre_relu = a.relu != 0;
+    if constexpr (LDSEPI) {
+      static_assert(FN == 4 && FM % 2 == 0 && A_BYTES >= NW * 4096, "KW3P LDS epilogue: 128 x 64 wave tiles, 4 KiB slices");
       uint8_t* wreg = smem + 2 * B_BYTES + ((g & 1) ^ 1) * A_BYTES + wave * 4096;
       const int rl = lane >> 3, pc = lane & 7, lch = pc ^ ((rl & 3) << 1);
       const int gcol = cn0 + wn * FN * 16 + lch * 8;
       const int mb = cm0 + wm * FM * 16 + rl;  // this lane's rows: mb + 8 k, k = 0 .. 2 FM - 1
-      const int nb = mb / HW, remb = mb - nb * HW, ohb = remb / W, owb = remb - ohb * W;
-      const int ndb = nb / a.ucode_div, nrb = nb - ndb * a.ucode_div;
+      const int nb = UNP ? mb / HW : 0, remb = mb - nb * HW, ohb = UNP ? remb / W : 0, owb = remb - ohb * W;
+      const int ndb = UNP ? nb / a.ucode_div : 0, nrb = nb - ndb * (UNP ? a.ucode_div : 1);
       // step (n, oh, ow) and (n / ucode_div, n % ucode_div) by 8 rows (host: W >= 8)
       auto step8 = [&](int& n, int& nd, int& nr, int& oh, int& ow) {
         ow += 8;
@@ -1256,7 +1395,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
         }
       };
       uint2 cd[2 * FM];
-      {
+      if constexpr (UNP) {
         int n = nb, nd = ndb, nr = nrb, oh = ohb, ow = owb;
 #pragma unroll
         for (int k = 0; k < 2 * FM; ++k) {
@@ -1304,6 +1443,16 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
         }
+        if constexpr (!UNP) {  // plain: one 16-B store per chunk (rows past M: out-of-range offset, dropped)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int m = mb + 8 * (4 * p + t);
+            const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.out_ld + (uint32_t)gcol) * 2u : kOOB;
+            typedef __attribute__((ext_vector_type(4))) unsigned int u32x4e;
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4e{cv[t].x, cv[t].y, cv[t].z, cv[t].w}, orr, (int)off, 0, 0);
+          }
+          continue;
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int k = 4 * p + t;
@@ -1329,7 +1478,6 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
         }
       }
       if (!more) break;
-      v = vnext;
       continue;
     }
 #pragma unroll
@@ -1366,7 +1514,6 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
       }
     }
     if (!more) break;
-    v = vnext;
   }
 }
 
@@ -1405,6 +1552,29 @@ static int kw3_var() {
   return v;
 }
 
+// DV_KW3P_NO_PRE=1: KW3P without the step-1 DMA issued ahead of the epilogue stores (A/B; read per launch)
+static int kw3p_pre() { return std::getenv("DV_KW3P_NO_PRE") == nullptr ? 1 : 0; }
+
+// KW3P stream-K applies (conv_dma_kw3p_kernel SK): a workspace was passed (bindings.cpp), not switched off
+// (DV_NO_KW3_SK=1, read per launch), one workgroup per CU with the column groups dividing the grid, more
+// tiles than workgroups, and every workgroup's range at least one tile long (at most one split tile at
+// each end of a range). The caller checked the KW3P epilogue conditions.
+static bool kw3_sk_ok(const ConvArgs& a, int BM, int BN) {
+  if (a.skw == nullptr || a.skflag == nullptr || a.m_base != 0 || std::getenv("DV_NO_KW3_SK") != nullptr) return false;
+  if (a.res != nullptr || a.emask != nullptr || a.accumulate || a.out2 != nullptr || a.OC != a.OCpad || a.OC % 8 ||
+      a.out_ld % 8 || a.H >= 4096 || 2LL * a.H * a.W + BM >= (1LL << 19) || a.dtype != DT_BF16 && a.dtype != DT_F16)
+    return false;  // (the KW3P epilogue conditions of kw3_try)
+  if (a.ucode != nullptr ? (a.W < 8 || a.ucode_div < 1) : a.out_elems * 2 >= 0x7FFFFFF0LL) return false;
+  const int G = num_cus(), tiles_n = a.OCpad / BN;
+  const long long tiles_m = (a.M + BM - 1) / BM;
+  // (only short grids: stream-K removes a partial last round, 1.53 rounds on the block5 forward convs,
+  // 0.26 -> 0.22 ms; on many-round grids its split-tile traffic and lost A sharing cost 1-3 %,
+  // profiles/kw3_sk_ab_r5.txt)
+  return G <= kSkMaxWg && (long long)BM * BN <= kSkSlotFloats && tiles_n >= 1 && G % tiles_n == 0 &&
+         tiles_m * tiles_n > G && tiles_m * tiles_n < 4LL * G && tiles_m >= G / tiles_n &&
+         tiles_m * (3LL * a.C / 32) < (1LL << 31);
+}
+
 // tiles_m_limit > 0: launch only the first tiles_m_limit row tiles (kw3_split's full rounds)
 template <int DT, int AMODE, int EPI, int BN = 256, int BM = 256>
 static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
@@ -1429,20 +1599,27 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
     if constexpr (EPI == CONV_E_BF16) {
       // VAR 10 / 11 (bf16 only): KW3P without epilogue stores (timing ablation) / with nt stores
       const bool pvar = var == 2 || (DT == DT_BF16 && (var == 10 || var == 11));
-      auto launch_p = [&](auto unp) -> int {
-        constexpr bool U = decltype(unp)::value;
+      auto launch_p = [&](auto em) -> int {
+        constexpr int U = decltype(em)::value;
         const unsigned g = (unsigned)(nwg < (long long)num_cus() ? nwg : (long long)num_cus());
         if constexpr (DT == DT_BF16) {
           if (var == 10) {
-            hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 1>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+            hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 1>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg, kw3p_pre());
             return (int)hipGetLastError();
           }
           if (var == 11) {
-            hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 2>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+            hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 2>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg, kw3p_pre());
             return (int)hipGetLastError();
           }
         }
-        hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg);
+        if (tiles_m_limit == 0 && kw3_sk_ok(a, BM, BN)) {  // stream-K over the whole grid (no tail launch)
+          const int G = num_cus();
+          if (hipMemsetAsync(a.skflag, 0, (size_t)G * sizeof(unsigned), s) != hipSuccess) return (int)hipGetLastError();
+          hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 0, true>), dim3(G), dim3(512), 0, s, a, tiles_n,
+                             (int)nwg, kw3p_pre());
+          return (int)hipGetLastError();
+        }
+        hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg, kw3p_pre());
         return (int)hipGetLastError();
       };
       // persistent KW3P: plain 16-bit epilogue only (its register-transpose stores write exactly
@@ -1450,13 +1627,19 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
       if (pvar && a.res == nullptr && a.emask == nullptr && !a.accumulate && a.ucode == nullptr &&
           a.out2 == nullptr && a.OC == a.OCpad && a.OC % 4 == 0 && a.out_ld % 4 == 0 &&
           a.out_elems * 2 < 0x7FFFFFF0LL && a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19))
-        return launch_p(std::false_type{});
+        // the LDS-sliced 16-B store epilogue unless DV_KW3P_EPI=reg (A/B) or the rows are not 16-B aligned:
+        // config-2 KW3P launches 9-13 % faster than with the register-transposed 8-B stores
+        // (profiles/kw3_epi_ab_r5.txt), config 2 +6.6 % (7418 / 7457 vs 6966 / 6985 img/s, same box)
+        return (std::getenv("DV_KW3P_EPI") == nullptr || std::strcmp(std::getenv("DV_KW3P_EPI"), "reg") != 0) &&
+                       a.OC % 8 == 0 && a.out_ld % 8 == 0
+                   ? launch_p(std::integral_constant<int, 2>{})
+                   : launch_p(std::integral_constant<int, 0>{});
       // persistent KW3P with the LDS-sliced max-unpool-out epilogue (DV_NO_KW3P_UNPOOL=1: the
       // non-persistent KW3 kernel's workgroup-staged one, A/B; read per launch)
       if (pvar && a.ucode != nullptr && a.res == nullptr && a.emask == nullptr && !a.accumulate &&
           a.out2 == nullptr && a.OC == a.OCpad && a.OC % 8 == 0 && a.out_ld % 8 == 0 && a.W >= 8 && a.ucode_div >= 1 &&
           a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19) && std::getenv("DV_NO_KW3P_UNPOOL") == nullptr)
-        return launch_p(std::true_type{});
+        return launch_p(std::integral_constant<int, 1>{});
     }
     if constexpr (DT == DT_BF16 && EPI == CONV_E_BF16) {
       if (var == 8 || var == 9) {
@@ -1498,6 +1681,10 @@ static int dma_cfg(const ConvArgs& a, hipStream_t s) {
 // DMA tiles (4x the workgroups, 2 per CU) starting at row m_base. Same stream, in order.
 template <int DT, int AMODE, int EPI>
 static int kw3_split(const ConvArgs& a, hipStream_t s, long long cus) {
+  if (kw3_sk_ok(a, 256, 256) && kw3_var() == 2) {  // stream-K: no partial round, no tail launch
+    const int rc = kw3_try<DT, AMODE, EPI>(a, s);
+    if (rc != -4) return rc;
+  }
   const int tiles_m = (a.M + 255) / 256, tiles_n = a.OCpad / 256;
   const long long nwg = (long long)tiles_m * tiles_n;
   const long long full = nwg / cus, rem = nwg % cus;

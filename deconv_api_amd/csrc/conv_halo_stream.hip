@@ -29,6 +29,7 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace dv {
 
@@ -349,8 +350,14 @@ constexpr int HU_PBUF = HU_PI * 4 * 1024, HU_CBUF = HU_CI * 4 * 1024;
 // taps, 48 MFMAs per wave between barriers instead of 16), the weight slot holds the row's three
 // taps, and a 2-slot ring with the next step's weights issued right after the barrier (prefetch
 // distance one 48-MFMA step) keeps 72 KiB of LDS -> 2 workgroups per CU.
-template <int DT, int OCT, bool POOL, bool UNPOOL, int TPS = 1>
+// LEPI (plain / emask epilogue, host: OC, out_ld, emask_ld % 8 == 0, 16-B aligned rows): the C tile goes
+// through LDS (the operand buffers, free after the K loop: 16 or 8 KiB per wave) and every lane stores
+// whole 16-B chunks, OCT / 8 lanes per pixel row: each store instruction writes 4 (OCT 128) or 8 pixels'
+// complete 256 / 128-B rows instead of 16 pixels x 32 B (the register layout's 8-B stores). The same
+// change on the persistent KW3P kernel took 9-13 % off its launches (profiles/kw3_epi_ab_r5.txt).
+template <int DT, int OCT, bool POOL, bool UNPOOL, int TPS = 1, bool LEPI = false>
 __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+  static_assert(!LEPI || !POOL, "LDS epilogue: plain / emask outputs");
   static_assert(TPS == 1 || (TPS == 3 && OCT == 64 && !UNPOOL), "3-tap steps: 64 output channels, no unpool");
   constexpr int FN = OCT / 16;                // output-channel blocks
   constexpr int BI = OCT / 64 * TPS;          // weight DMA instructions per wave and step (TPS*OCT*64 B / 4 KiB)
@@ -613,6 +620,57 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
     }
     return;
   }
+  if constexpr (LEPI) {
+    // every wave's last fragment reads of the operand buffers are done before any wave overwrites them
+    __syncthreads();
+    constexpr int ROWB = OCT * 2, CPR = OCT / 8;  // bytes / 16-B chunks per pixel row
+    uint8_t* wreg = smem + wave * 64 * ROWB;      // this wave's 4 x 16 pixels
+    static_assert(4 * 64 * ROWB <= (int)sizeof(smem), "LDS epilogue slices");
+    // C -> LDS: lane (px, q) writes channels 16 j + 4 q .. + 3 of pixel (i, px) as one 8-B write; the 16-B
+    // chunk index is XOR-swizzled by the pixel (chunk ^ (px mod CPR)) so the 16 lanes of a ds_write_b64
+    // group (16 pixels, one chunk) hit distinct bank slots
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const float v0 = fmaxf(acc[i][j][0] + bv[j].x, lo), v1 = fmaxf(acc[i][j][1] + bv[j].y, lo);
+        const float v2 = fmaxf(acc[i][j][2] + bv[j].z, lo), v3 = fmaxf(acc[i][j][3] + bv[j].w, lo);
+        const int ch = 2 * j + (q >> 1);
+        *reinterpret_cast<uint2*>(wreg + (i * 16 + px) * ROWB + ((ch ^ (px & (CPR - 1))) << 4) + (q & 1) * 8) =
+            make_uint2(pack2<DT>(v0, v1), pack2<DT>(v2, v3));
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: this wave's writes before its reads
+    // LDS -> global: lane reads the chunk physically at (lane mod CPR) of local pixel lp (logical chunk
+    // = that ^ the pixel's swizzle), so the 16 lanes of every ds_read_b128 group read 16 distinct slots
+    constexpr int PPI = 64 / CPR, NT = 64 / PPI;  // pixels per instruction, instructions per lane
+    const int pc = lane % CPR;
+    uint4 em[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {  // every output-mask load before the first store
+      const int lp = t * PPI + lane / CPR;
+      const int lc = pc ^ (lp & (CPR - 1));
+      const long long pix = ((long long)n * a.OH + ty0 + 4 * wave + (lp >> 4)) * a.OW + tx0 + (lp & 15);
+      em[t] = make_uint4(0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u);  // any > 0
+      if (a.emask && lc * 8 < a.OC && DV_BOUNDS(pix * a.emask_ld + lc * 8, 8, a.emask_elems, "hs16 emask"))
+        em[t] = *reinterpret_cast<const uint4*>(a.emask + pix * a.emask_ld + lc * 8);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int lp = t * PPI + lane / CPR;
+      const int lc = pc ^ (lp & (CPR - 1));
+      const long long pix = ((long long)n * a.OH + ty0 + 4 * wave + (lp >> 4)) * a.OW + tx0 + (lp & 15);
+      uint4 v = *reinterpret_cast<const uint4*>(wreg + lp * ROWB + pc * 16);
+      if (a.emask) {
+        v.x = mask_pos_pk(v.x, em[t].x);
+        v.y = mask_pos_pk(v.y, em[t].y);
+        v.z = mask_pos_pk(v.z, em[t].z);
+        v.w = mask_pos_pk(v.w, em[t].w);
+      }
+      if (lc * 8 < a.OC && DV_BOUNDS(pix * a.out_ld + lc * 8, 8, a.out_elems, "hs16 out"))
+        *reinterpret_cast<uint4*>(out + pix * a.out_ld + lc * 8) = v;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int oy = ty0 + 4 * wave + i;
@@ -705,17 +763,33 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
     const long long n16 = (long long)a.N * t16x * t16y;
     if (n16 <= 0 || n16 > 0x7fffffffLL) return -2;
     const dim3 g16((unsigned)n16), b16(256);
-#define HS16(DT_, OCT_, POOL_)                                                                               \
-  hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_, OCT_, POOL_, false, OCT_ == 64 ? 3 : 1>), g16, b16, 0, s, a, t16x, t16y)
+#define HS16(DT_, OCT_, POOL_, LEPI_)                                                                            \
+  hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_, OCT_, POOL_, false, OCT_ == 64 ? 3 : 1, LEPI_>), g16, b16, 0, s, a, t16x, \
+                     t16y)
+    // the LDS-staged 16-B store epilogue (DV_HS16_EPI=reg: the register layout's 8-B stores, A/B; read per launch)
+    const char* he = std::getenv("DV_HS16_EPI");
+    const bool lepi = !pool && !(he && std::strcmp(he, "reg") == 0) && a.OC % 8 == 0 && a.out_ld % 8 == 0 &&
+                      !(reinterpret_cast<uintptr_t>(a.out) & 15) &&
+                      (!a.emask || (a.emask_ld % 8 == 0 && !(reinterpret_cast<uintptr_t>(a.emask) & 15)));
     if (pool) {
-      if (a.OCpad == 128) HS16(DT_BF16, 128, true);
-      else HS16(DT_BF16, 64, true);
+      if (a.OCpad == 128) HS16(DT_BF16, 128, true, false);
+      else HS16(DT_BF16, 64, true, false);
     } else if (a.dtype == DT_F16) {
-      if (a.OCpad == 128) HS16(DT_F16, 128, false);
-      else HS16(DT_F16, 64, false);
+      if (a.OCpad == 128) {
+        if (lepi) HS16(DT_F16, 128, false, true);
+        else HS16(DT_F16, 128, false, false);
+      } else {
+        if (lepi) HS16(DT_F16, 64, false, true);
+        else HS16(DT_F16, 64, false, false);
+      }
     } else {
-      if (a.OCpad == 128) HS16(DT_BF16, 128, false);
-      else HS16(DT_BF16, 64, false);
+      if (a.OCpad == 128) {
+        if (lepi) HS16(DT_BF16, 128, false, true);
+        else HS16(DT_BF16, 128, false, false);
+      } else {
+        if (lepi) HS16(DT_BF16, 64, false, true);
+        else HS16(DT_BF16, 64, false, false);
+      }
     }
 #undef HS16
     return (int)hipGetLastError();

@@ -68,7 +68,12 @@ struct ConvArgs {
                           //   next conv-down's taps as a [32][64] matrix, row tap*3+c = W[c][tap][:])
   int pool_t;             // host-checked (POOL epilogue): OC, out_ld % 4 == 0, out 8-B / out_code 4-B aligned ->
                           //   the transposed pooled-max epilogue (conv_dma_impl.h:epilogue_pool_t)
+  float* skw;             // optional: KW3P stream-K workspace, kSkSlotFloats fp32 per workgroup (partial tiles)
+  unsigned* skflag;       //   + one ready flag per workgroup; zeroed by the launcher before each launch
 };
+// KW3P stream-K: fp32 partial-tile slot per workgroup (BM x BN = 65536 for both KW3P tile shapes)
+constexpr long long kSkSlotFloats = 256LL * 256LL;
+constexpr int kSkMaxWg = 1024;
 
 // grouped LDS-DMA launch of up to kGroupMax independent problems (conv_dma.hip:conv_dma_group_launch)
 constexpr int kGroupMax = 4;

@@ -207,6 +207,12 @@ def test_conv_halo_stream(native_lib, dt, N, H, W, C, OC, bias, relu):
     ref = ops.conv2d(x.to(dt).float(), cw, relu=relu, use_bias=bias)
     got = ops.conv2d(xd, cw.to_device(DEV, dt), relu=relu, use_bias=bias)
     assert got.shape == ref.shape and got.dtype == dt and _rel(got, ref) < 1e-2
+    os.environ["DV_HS16_EPI"] = "reg"  # hs16 register-layout 8-B store epilogue: bit-identical to the LDS one
+    try:
+        reg = ops.conv2d(xd, cw.to_device(DEV, dt), relu=relu, use_bias=bias)
+    finally:
+        del os.environ["DV_HS16_EPI"]
+    assert torch.equal(got, reg)
     for env in ("DV_NO_HS", "DV_NO_HS16"):  # implicit GEMM; 16x32-tile kernel instead of 16x16
         os.environ[env] = "1"
         try:
@@ -323,18 +329,23 @@ def test_conv_kw3_persistent(native_lib, monkeypatch, N, H, W, C, OC, dt):
     accumulation order, same rounding) and to the fp32 reference up to bf16 rounding."""
     monkeypatch.setenv("DV_KW3", "2")
     monkeypatch.setenv("DV_NO_SPLITK", "1")
+    monkeypatch.setenv("DV_NO_KW3_SK", "1")  # whole tiles (stream-K rounds split tiles differently)
     g = torch.Generator().manual_seed(N + C)
     x = torch.randn(N, H, W, C, generator=g).to(dt)
     cw = _cw(OC, C)
     xd, cwd = x.to(DEV), cw.to_device(DEV, dt)
     for relu in (True, False):
         outs = {}
-        for var in ("0", "2"):
-            monkeypatch.setenv("DV_KW3_VAR", var)
+        for var in ("0", "2", "2reg"):  # 2reg: KW3P with the register-transposed 8-B stores (DV_KW3P_EPI=reg)
+            monkeypatch.setenv("DV_KW3_VAR", var[0])
+            if var == "2reg":
+                monkeypatch.setenv("DV_KW3P_EPI", "reg")
             big = torch.full((N, H, W, OC + 8), 7.0, dtype=dt, device=DEV)
             outs[var] = ops.conv2d(xd, cwd, relu=relu, out=big[..., :OC])
+            monkeypatch.delenv("DV_KW3P_EPI", raising=False)
             assert bool((big[..., OC:] == 7.0).all()), "wrote past the channel slice"
         assert torch.equal(outs["0"], outs["2"]), relu
+        assert torch.equal(outs["0"], outs["2reg"]), relu
         ref = ops.conv2d(x[: min(N, 8)].float(), cw, relu=relu)
         assert _rel(outs["2"][: min(N, 8)], ref) < 1e-2
 
@@ -353,6 +364,7 @@ def test_conv_kw3p_unpool_out(native_lib, monkeypatch, N, H, W, C, OC, div, dt):
     switch positions, and the fp32 reference up to bf16 rounding."""
     monkeypatch.setenv("DV_KW3", "2")
     monkeypatch.setenv("DV_NO_SPLITK", "1")
+    monkeypatch.setenv("DV_NO_KW3_SK", "1")  # whole tiles (stream-K: test_conv_kw3p_stream_k)
     g = torch.Generator().manual_seed(N + W)
     x = torch.relu(torch.randn(N, H, W, C, generator=g)).to(dt)
     code = torch.randint(0, 4, (N // div, H, W, OC), generator=g, dtype=torch.uint8)
@@ -371,6 +383,52 @@ def test_conv_kw3p_unpool_out(native_lib, monkeypatch, N, H, W, C, OC, div, dt):
     n = 2 * div
     ref = ops.conv2d(x[:n].float(), cw, relu=True, use_bias=False, unpool_out=code[: n // div], unpool_div=div)
     assert _rel(got[:n], ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C,OC,div,dt", [(600, 14, 14, 64, 256, 0, torch.bfloat16),
+                                                (300, 14, 14, 96, 512, 4, torch.bfloat16),
+                                                (80, 56, 56, 32, 128, 2, torch.bfloat16),
+                                                (80, 56, 56, 64, 128, 0, torch.bfloat16),
+                                                (150, 28, 28, 32, 512, 0, torch.float16),
+                                                (700, 14, 14, 32, 256, 1, torch.float16)])
+def test_conv_kw3p_stream_k(native_lib, monkeypatch, N, H, W, C, OC, div, dt):
+    """Stream-K KW3P (conv_dma_kw3p_kernel<.., SK>: each workgroup a contiguous range of K steps, split
+    tiles handed over as fp32 partials with the sc1 / flag protocol): plain (div 0) and unpool-out
+    epilogues, 256 x 256 (one and two column groups) and 512 x 128 tiles, odd step counts (C = 96).
+    Against the whole-tile kernel (DV_NO_KW3_SK=1): equal up to the one extra fp32 rounding of a split
+    tile's sum (a few bf16 ulps at most), and against the fp32 reference."""
+    monkeypatch.setenv("DV_NO_SPLITK", "1")
+    g = torch.Generator().manual_seed(N + C + OC)
+    x = torch.relu(torch.randn(N, H, W, C, generator=g)).to(dt)
+    cw = _cw(OC, C, bias=div == 0)
+    xd, cwd = x.to(DEV), cw.to_device(DEV, dt)
+    kw = dict(relu=True, use_bias=div == 0)
+    code = None
+    if div:
+        code = torch.randint(0, 4, (N // div, H, W, OC), generator=g, dtype=torch.uint8)
+        kw.update(unpool_out=code.to(DEV), unpool_div=div)
+    got = ops.conv2d(xd, cwd, **kw)
+    monkeypatch.setenv("DV_NO_KW3_SK", "1")
+    whole = ops.conv2d(xd, cwd, **kw)
+    monkeypatch.delenv("DV_NO_KW3_SK")
+    assert got.shape == whole.shape
+    d = (got.float() - whole.float()).abs()
+    assert float(d.max()) <= 2 ** -6 * float(whole.float().abs().max()), float(d.max())
+    assert float((d > 0).float().mean()) < 0.05  # only the split tiles' rounding differs
+    n = 2 * max(div, 1)
+    if div:
+        kw_ref = dict(relu=True, use_bias=False, unpool_out=code[: n // div], unpool_div=div)
+        ref = ops.conv2d(x[:n].float(), cw, **kw_ref)
+    else:
+        ref = ops.conv2d(x[:n].float(), cw, relu=True)
+    assert _rel(got[:n], ref) < 1e-2
+    ntail = 2 * max(div, 1)  # the last images: the last workgroups' ranges and split tiles
+    if div:
+        ref = ops.conv2d(x[-ntail:].float(), cw, relu=True, use_bias=False, unpool_out=code[-(ntail // div):],
+                         unpool_div=div)
+    else:
+        ref = ops.conv2d(x[-ntail:].float(), cw, relu=True)
+    assert _rel(got[-ntail:], ref) < 1e-2
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
@@ -868,6 +926,9 @@ def test_conv_halo_stream_pad_emask(native_lib, monkeypatch, dt, C, OC, H, W, pa
     assert got.dtype == dt and _rel(got, ref) < 1e-2
     if use_emask:
         assert bool(((got.float().cpu() != 0) & (em <= 0)).sum() == 0)
+    monkeypatch.setenv("DV_HS16_EPI", "reg")  # hs16: register-layout 8-B stores, bit-identical
+    assert torch.equal(got, ops.conv2d(x.to(dt).to(DEV), dw, pad=pad, relu=relu, emask=emd))
+    monkeypatch.delenv("DV_HS16_EPI")
     monkeypatch.setenv("DV_NO_HS", "1")
     dma = ops.conv2d(x.to(dt).to(DEV), dw, pad=pad, relu=relu, emask=emd)
     assert _rel(dma, ref) < 1e-2

@@ -30,6 +30,7 @@ CASES = {
     "b3down": (1024, 56, 56, 256, 256),     # block3_conv{2,3}.down
     "b3c1down": (1024, 56, 56, 256, 128),   # block3_conv1.down: 512 x 128 KW3 tile
     "b4fwd": (256, 28, 28, 512, 512),       # block4_conv{2,3} forward
+    "b3fwd": (256, 56, 56, 256, 256),       # block3_conv{2,3} forward
     "b5fwd": (256, 14, 14, 512, 512),       # block5 forward (tail-split KW3)
     # unpool-out conv-downs (suffix "unp": max-unpooled output, switch codes shared by 4 signals)
     "b5c1unp": (1024, 14, 14, 512, 512),    # block5_conv1.down -> 28^2
@@ -60,7 +61,19 @@ def main():
         code = torch.randint(0, 4, (N // 4, H, W, OC), device=dev, dtype=torch.uint8, generator=g) if unp else None
 
         def run(v):
-            os.environ["DV_KW3_VAR"] = str(v)
+            # 2: KW3P as selected (stream-K where it applies, step-1 DMA ahead of the epilogue stores);
+            # 12: whole tiles (DV_NO_KW3_SK=1); 13: whole tiles without the early DMA (+ DV_KW3P_NO_PRE=1);
+            # 14: stream-K without the early DMA; 15: whole tiles with the register-transposed 8-B store epilogue
+            os.environ["DV_KW3_VAR"] = str(2 if v in (12, 13, 14, 15) else v)
+            for k, on in (("DV_NO_KW3_SK", v in (12, 13, 15)), ("DV_KW3P_NO_PRE", v in (13, 14))):
+                if on:
+                    os.environ[k] = "1"
+                else:
+                    os.environ.pop(k, None)
+            if v == 15:
+                os.environ["DV_KW3P_EPI"] = "reg"
+            else:
+                os.environ.pop("DV_KW3P_EPI", None)
             if unp:  # a fresh unpooled output per call (as the engine does)
                 out[v] = ops.conv2d(x, cw, relu=True, use_bias=False, unpool_out=code, unpool_div=4)
                 return out[v]
@@ -69,9 +82,12 @@ def main():
         for v in variants:  # warm up every variant (and check the real ones agree)
             run(v)
         torch.cuda.synchronize()
-        real = [v for v in variants if v < 8]
+        real = [v for v in variants if v < 8 or v in (11, 12, 13, 14, 15)]
         for v in real[1:]:
             same = torch.equal(out[v], out[real[0]])
+            if not same:  # stream-K vs whole tiles: split tiles round differently
+                d = (out[v].float() - out[real[0]].float()).abs()
+                same = float(d.max()) <= 2 ** -6 * float(out[real[0]].float().abs().max())
             if not same:
                 d = (out[v].float() - out[real[0]].float()).abs().max().item()
                 print(json.dumps({"case": case, "var": v, "equal_to": real[0], "equal": False, "maxdiff": d}),
