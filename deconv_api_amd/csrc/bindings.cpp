@@ -195,6 +195,14 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     const bool no_pool_t = std::getenv("DV_NO_POOL_T") != nullptr;  // A/B: the per-element pool stores (per call)
     a.pool_t = !no_pool_t && a.OC % 4 == 0 && a.out_ld % 4 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0 &&
                reinterpret_cast<uintptr_t>(a.out_code) % 4 == 0;
+    // 2 (opt-in, DV_POOL_EPI=lds, per call): the LDS-staged pooled epilogue (whole 16-B value / code chunks
+    // per lane). Measured equal to slightly slower than the transposed 8-B stores on config 2 (the pooled
+    // output is a quarter of the conv's: 7478 / 7506 / 7547 vs 7504 / 7531 / 7549 img/s, same box,
+    // alternating; profiles/bench_c2_r5_pool_epi_ab.txt)
+    const char* pe = std::getenv("DV_POOL_EPI");
+    if (a.pool_t && pe && std::strcmp(pe, "lds") == 0 && a.OC % 16 == 0 && a.out_ld % 8 == 0 &&
+        reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(a.out_code) % 16 == 0)
+      a.pool_t = 2;
   } else if (epi == dv::CONV_E_F32) {
     TORCH_CHECK(out.scalar_type() == at::kFloat, "f32 epilogue needs fp32 out");
   } else {

@@ -388,6 +388,13 @@ __device__ __forceinline__ void conv_dma_body(const ConvArgs& a, int tiles_n, in
       return;
     }
   }
+  if constexpr (EPI == CONV_E_POOL && FM % 4 == 0 && BN % 16 == 0 && (BM / 4) * BN * 3 <= STAGES * STAGE) {
+    if (a.pool_t == 2) {
+      __syncthreads();  // every wave is done reading the operand stages
+      epilogue_pool_lds<DT, NW * 64, BM, BN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+      return;
+    }
+  }
   if constexpr (EPI == CONV_E_BF16) {
     if (a.res || a.emask) {
       epilogue_res<DT, FM, FN>(a, acc, m0 + wm * FM * 16, n0 + wn * FN * 16, lane);
@@ -523,6 +530,93 @@ __device__ __forceinline__ void epilogue_pool_t(const ConvArgs& a, const f32x4 (
             (k0 & 0xFFu) | ((k0 >> 8) & 0xFF00u) | ((k1 & 0xFFu) << 16) | ((k1 >> 16) << 24);
       }
     }
+  }
+}
+
+// Pooled-max epilogue staged through LDS (ConvArgs::pool_t == 2): the transposed (max, code) quads of
+// epilogue_pool_t go to the freed operand stages as [BM/4 pooled rows][BN] values and codes, then every lane
+// stores whole 16-B chunks of one pooled row (values: BN / 8 lanes per row, codes BN / 16): each store
+// instruction writes complete row segments instead of 16 rows x 32 B (values) / 16 B (codes). The same change
+// took 9-13 % off the persistent KW3P launches (profiles/kw3_epi_ab_r5.txt). Bit-identical to epilogue_pool_t.
+// Swizzles (16-B chunk index XOR a function of the pooled row) make the quad-transposed ds_write_b64 /
+// ds_write_b32 groups and the row-wise ds_read_b128 groups conflict-free.
+template <int DT, int NT, int BM, int BN, int FM, int FN>
+__device__ __forceinline__ void epilogue_pool_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
+                                                  int n0, int wm, int wn, int lane, int tid) {
+  static_assert(FM % 4 == 0 && BN % 16 == 0, "pool LDS epilogue shape");
+  constexpr int VROW = BN * 2, CROW = BN;  // bytes per pooled row: values / codes
+  uint8_t* vs = smem;
+  uint8_t* cs = smem + (BM / 4) * VROW;
+  const int q = lane >> 4, cl = lane & 15, ce = cl & 1, cu = (cl >> 1) & 1, csub = cl & ~3, tsel = ce * 2 + cu;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col0 = n0 + wn * FN * 16 + j * 16;
+    const float bias = (a.bias && col0 + cl < a.OC) ? a.bias[col0 + cl] : 0.f;
+#pragma unroll
+    for (int ig = 0; ig < FM / 4; ++ig) {
+      float best[4];
+      uint32_t code[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int i = ig * 4 + t;
+        float b = -INFINITY;
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bias;
+          if (a.relu) v = fmaxf(v, 0.f);
+          v = to_f<DT>(from_f<DT>(v));
+          if (v > b) {
+            b = v;
+            c = (uint32_t)r;
+          }
+        }
+        best[t] = b;
+        code[t] = c;
+      }
+      auto tr = [&](uint32_t p0, uint32_t p1, uint32_t& w0, uint32_t& w1) {
+        const uint32_t keep = ce ? p1 : p0;
+        const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(ce ? p0 : p1), 0xB1, 0xF, 0xF, false);
+        const uint32_t lo = ce ? recv : keep, hi = ce ? keep : recv;
+        const uint32_t d0 = (lo & 0xFFFFu) | (hi << 16), d1 = (lo >> 16) | (hi & 0xFFFF0000u);
+        const uint32_t recv2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(cu ? d0 : d1), 0x4E, 0xF, 0xF, false);
+        w0 = cu ? recv2 : d0;
+        w1 = cu ? d1 : recv2;
+      };
+      uint32_t w0, w1, k0, k1;
+      tr(pack2<DT>(best[0], best[1]), pack2<DT>(best[2], best[3]), w0, w1);
+      tr(code[0] | (code[1] << 16), code[2] | (code[3] << 16), k0, k1);
+      const int prl = (wm * FM * 16 + (ig * 4 + tsel) * 16 + q * 4) >> 2;  // pooled row in the tile
+      const int cc = wn * FN * 16 + j * 16 + csub;                       // channel in the tile
+      const int vch = (cc >> 3) ^ (((prl >> 2) & 3) << 1);
+      *reinterpret_cast<uint2*>(vs + prl * VROW + (vch << 4) + (cc & 4) * 2) = make_uint2(w0, w1);
+      const int cch = (cc >> 4) ^ (((prl >> 2) & 3) | ((prl & 1) << 2));
+      *reinterpret_cast<uint32_t*>(cs + prl * CROW + (cch << 4) + (cc & 12)) =
+          (k0 & 0xFFu) | ((k0 >> 8) & 0xFF00u) | ((k1 & 0xFFu) << 16) | ((k1 >> 16) << 24);
+    }
+  }
+  __syncthreads();
+  uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+  const int prow0 = m0 >> 2, prows = a.M >> 2;
+  constexpr int VCPR = VROW / 16, CCPR = CROW / 16;  // 16-B chunks per pooled row
+#pragma unroll
+  for (int c = tid; c < (BM / 4) * VCPR; c += NT) {
+    const int r = c / VCPR, pc = c % VCPR;
+    const int lc = pc ^ (((r >> 2) & 3) << 1);
+    const int col = n0 + lc * 8;
+    if (prow0 + r >= prows || col >= a.OC) continue;
+    const long long o = (long long)(prow0 + r) * a.out_ld + col;
+    if (DV_BOUNDS(o, 8, a.out_elems, "conv_dma pool lds out"))
+      *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<const uint4*>(vs + r * VROW + pc * 16);
+  }
+#pragma unroll
+  for (int c = tid; c < (BM / 4) * CCPR; c += NT) {
+    const int r = c / CCPR, pc = c % CCPR;
+    const int lc = pc ^ (((r >> 2) & 3) | ((r & 1) << 2));
+    const int col = n0 + lc * 16;
+    if (prow0 + r >= prows || col >= a.OC) continue;
+    *reinterpret_cast<uint4*>(a.out_code + (long long)(prow0 + r) * a.OC + col) =
+        *reinterpret_cast<const uint4*>(cs + r * CROW + pc * 16);
   }
 }
 
@@ -1570,8 +1664,11 @@ static bool kw3_sk_ok(const ConvArgs& a, int BM, int BN) {
   // (only short grids: stream-K removes a partial last round, 1.53 rounds on the block5 forward convs,
   // 0.26 -> 0.22 ms; on many-round grids its split-tile traffic and lost A sharing cost 1-3 %,
   // profiles/kw3_sk_ab_r5.txt)
+  // (DV_KW3_SK=all: every eligible grid, A/B; read per launch)
+  const char* ska = std::getenv("DV_KW3_SK");
+  const long long max_tiles = ska && std::strcmp(ska, "all") == 0 ? (1LL << 40) : 4LL * G;
   return G <= kSkMaxWg && (long long)BM * BN <= kSkSlotFloats && tiles_n >= 1 && G % tiles_n == 0 &&
-         tiles_m * tiles_n > G && tiles_m * tiles_n < 4LL * G && tiles_m >= G / tiles_n &&
+         tiles_m * tiles_n > G && tiles_m * tiles_n < max_tiles && tiles_m >= G / tiles_n &&
          tiles_m * (3LL * a.C / 32) < (1LL << 31);
 }
 
@@ -1609,6 +1706,17 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
           }
           if (var == 11) {
             hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 2>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg, kw3p_pre());
+            return (int)hipGetLastError();
+          }
+        }
+        // the unpool-out epilogue's stores are non-temporal (the 4x-upsampled map, 3/4 zeros, streams past the
+        // caches): config 2 +0.3 % (3 / 3 pairs, profiles/bench_c2_r5_unp_nt_ab.txt). DV_KW3P_UNP_NT=0: plain
+        // stores (A/B; read per launch)
+        if constexpr (U == 1) {
+          const char* unt = std::getenv("DV_KW3P_UNP_NT");
+          if (!(unt && std::strcmp(unt, "0") == 0) && !(tiles_m_limit == 0 && kw3_sk_ok(a, BM, BN))) {
+            hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 2>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg,
+                               kw3p_pre());
             return (int)hipGetLastError();
           }
         }

@@ -94,8 +94,13 @@ __device__ __forceinline__ f32x16 hs_mfma(const typename Vec8<DT>::type& a, cons
 // NB1 (one 32-channel chunk, C == 32): ONE halo buffer (72 KiB of LDS -> 2 workgroups per CU; with a
 // single chunk there is no next-chunk prefetch to double-buffer).
 // emask (non-pool): the output is zeroed where emask <= 0 (an input gradient masked by its ReLU).
-template <int DT, int OCT, bool POOL, int RING, bool NB1 = false>
+// LEPI (plain / emask epilogue; host: OC, out_ld, emask_ld % 8 == 0, 16-B aligned rows): the C tile goes
+// through LDS one tile row per pass (32 px x OCT channels per wave, in the operand buffers freed after the K
+// loop) and every lane stores whole 16-B chunks, OCT / 8 lanes per pixel: each store instruction writes
+// complete pixel rows instead of 32 pixels x 16 B (as hs16's LEPI and KW3P's LDS epilogue).
+template <int DT, int OCT, bool POOL, int RING, bool NB1 = false, bool LEPI = false>
 __global__ void __launch_bounds__(512, NB1 && OCT == 64 ? 4 : 1) conv3x3_hs_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+  static_assert(!LEPI || !POOL, "LDS epilogue: plain / emask outputs");
   constexpr int FN = OCT / 32;  // 32-channel A blocks per wave
   // weights of one step: OCT rows x 80 B. OCT = 128: 10 KiB = one 1-KiB dwordx4 DMA + one 256-B dword
   // DMA per wave (exact); OCT = 64: 5 KiB in one dwordx4 DMA per wave, 3 of them out-of-range dummies
@@ -212,6 +217,62 @@ __global__ void __launch_bounds__(512, NB1 && OCT == 64 ? 4 : 1) conv3x3_hs_kern
   // epilogue: lane = pixel (tile row 2*wave + i, column px); register r of block j = output channel
   // 32j + 8(r >> 2) + 4h + (r & 3): 4 consecutive channels -> one 8-B store
   const int ox = tx0 + px;
+  if constexpr (LEPI) {
+    constexpr int ROWB = OCT * 2, CPR = OCT / 8, PPI = 64 / CPR, NT = 32 / PPI;
+    static_assert(8 * 32 * ROWB <= (int)sizeof(smem), "LDS epilogue slices");
+    float4 bv[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        bv[j][g] = a.bias ? *reinterpret_cast<const float4*>(a.bias + 32 * j + 8 * g + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float lo = a.relu ? 0.f : -INFINITY;
+    uint16_t* out = reinterpret_cast<uint16_t*>(a.out);
+    uint8_t* wreg = smem + wave * 32 * ROWB;
+    const int pc = lane % CPR;
+    __syncthreads();  // every wave's last fragment reads of the halo / weight buffers are done
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float v0 = fmaxf(acc[i][j][4 * g + 0] + bv[j][g].x, lo), v1 = fmaxf(acc[i][j][4 * g + 1] + bv[j][g].y, lo);
+          const float v2 = fmaxf(acc[i][j][4 * g + 2] + bv[j][g].z, lo), v3 = fmaxf(acc[i][j][4 * g + 3] + bv[j][g].w, lo);
+          const int ch = 4 * j + g;  // 16-B chunk; lanes h = 0 / 1 hold its two halves
+          *reinterpret_cast<uint2*>(wreg + px * ROWB + ((ch ^ (px & (CPR - 1))) << 4) + h * 8) =
+              make_uint2(pack2<DT>(v0, v1), pack2<DT>(v2, v3));
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: this wave's writes before its reads
+      const int oy = ty0 + 2 * wave + i;
+      uint4 em[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {  // every output-mask load of the row before its first store
+        const int lp = t * PPI + lane / CPR, lc = pc ^ (lp & (CPR - 1)), x = tx0 + lp;
+        const long long pix = ((long long)n * a.OH + oy) * a.OW + x;
+        em[t] = make_uint4(0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u);  // any > 0
+        if (a.emask && oy < a.OH && x < a.OW && lc * 8 < a.OC &&
+            DV_BOUNDS(pix * a.emask_ld + lc * 8, 8, a.emask_elems, "halo-stream emask"))
+          em[t] = *reinterpret_cast<const uint4*>(a.emask + pix * a.emask_ld + lc * 8);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int lp = t * PPI + lane / CPR, lc = pc ^ (lp & (CPR - 1)), x = tx0 + lp;
+        uint4 v = *reinterpret_cast<const uint4*>(wreg + lp * ROWB + pc * 16);
+        if (a.emask) {
+          v.x = mask_pos_pk(v.x, em[t].x);
+          v.y = mask_pos_pk(v.y, em[t].y);
+          v.z = mask_pos_pk(v.z, em[t].z);
+          v.w = mask_pos_pk(v.w, em[t].w);
+        }
+        const long long pix = ((long long)n * a.OH + oy) * a.OW + x;
+        if (oy < a.OH && x < a.OW && lc * 8 < a.OC && DV_BOUNDS(pix * a.out_ld + lc * 8, 8, a.out_elems, "halo-stream out"))
+          *reinterpret_cast<uint4*>(out + pix * a.out_ld + lc * 8) = v;
+      }
+    }
+    return;
+  }
   if (ox >= a.OW) return;
   // the lane's bias values (the same for both pixel rows), all loads in flight together
   float4 bv[FN][4];
@@ -799,12 +860,32 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
   if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
   const dim3 grid((unsigned)nwg), block(512);
   const int ring = hs_ring();
+  // the LDS-staged 16-B store epilogue (DV_HS16_EPI=reg: the register layout's 8-B stores, A/B; per launch)
+  const char* he = std::getenv("DV_HS16_EPI");
+  const bool lepi = !pool && ring == 3 && !(he && std::strcmp(he, "reg") == 0) && a.OC % 8 == 0 && a.out_ld % 8 == 0 &&
+                    !(reinterpret_cast<uintptr_t>(a.out) & 15) &&
+                    (!a.emask || (a.emask_ld % 8 == 0 && !(reinterpret_cast<uintptr_t>(a.emask) & 15)));
+#define HS_LEPI(DT_, OCT_, NB1_) \
+  hipLaunchKernelGGL((conv3x3_hs_kernel<DT_, OCT_, false, 3, NB1_, true>), grid, block, 0, s, a, tx, ty)
   if (pool) {
     if (a.OCpad == 128) HS_LAUNCH(DT_BF16, 128, true);
     else HS_LAUNCH(DT_BF16, 64, true);
   } else if (a.C == 32 && a.OCpad == 64) {  // one channel chunk: single halo buffer, 2 workgroups per CU
-    if (a.dtype == DT_F16) hipLaunchKernelGGL((conv3x3_hs_kernel<DT_F16, 64, false, 3, true>), grid, block, 0, s, a, tx, ty);
-    else hipLaunchKernelGGL((conv3x3_hs_kernel<DT_BF16, 64, false, 3, true>), grid, block, 0, s, a, tx, ty);
+    if (a.dtype == DT_F16) {
+      if (lepi) HS_LEPI(DT_F16, 64, true);
+      else hipLaunchKernelGGL((conv3x3_hs_kernel<DT_F16, 64, false, 3, true>), grid, block, 0, s, a, tx, ty);
+    } else {
+      if (lepi) HS_LEPI(DT_BF16, 64, true);
+      else hipLaunchKernelGGL((conv3x3_hs_kernel<DT_BF16, 64, false, 3, true>), grid, block, 0, s, a, tx, ty);
+    }
+  } else if (lepi) {
+    if (a.dtype == DT_F16) {
+      if (a.OCpad == 128) HS_LEPI(DT_F16, 128, false);
+      else HS_LEPI(DT_F16, 64, false);
+    } else {
+      if (a.OCpad == 128) HS_LEPI(DT_BF16, 128, false);
+      else HS_LEPI(DT_BF16, 64, false);
+    }
   } else if (a.dtype == DT_F16) {
     if (a.OCpad == 128) HS_LAUNCH(DT_F16, 128, false);
     else HS_LAUNCH(DT_F16, 64, false);
@@ -812,6 +893,7 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
     if (a.OCpad == 128) HS_LAUNCH(DT_BF16, 128, false);
     else HS_LAUNCH(DT_BF16, 64, false);
   }
+#undef HS_LEPI
   return (int)hipGetLastError();
 }
 

@@ -401,20 +401,31 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
           }
         }
       }
-      if (oy < H) {
+      // Z[px][zc]: lane (col, kq) holds Z channels jz*16 + kq*4 + r of pixel col. One v_permlane16_swap per
+      // dword (rows kq <-> kq ^ 1, as the c8 stream kernel) leaves lane kq with block kq & 1, channels
+      // (kq >> 1) * 8 .. + 7: ONE 16-B store per pixel block, each store instruction writing 16 pixels'
+      // complete 64-B Z rows (1 KiB contiguous) instead of two instructions of 16 x 32-B halves
 #pragma unroll
-        for (int pf = 0; pf < 2; ++pf) {
-          const int ox = tx * TW + pf * 16 + col;
-          if (ox >= W) continue;
-          uint16_t* zo = reinterpret_cast<uint16_t*>(a.out) + (((long long)n * H + oy) * W + ox) * a.out_ld;
+      for (int pf = 0; pf < 2; ++pf) {
+        uint32_t pk[2][2];
 #pragma unroll
-          for (int jz = 0; jz < 2; ++jz) {
-            const int zc = jz * 16 + kq * 4;
-            if (DV_BOUNDS((((long long)n * H + oy) * W + ox) * a.out_ld + zc, 4, a.out_elems, "unpool_z out"))
-              *reinterpret_cast<uint2*>(zo + zc) =
-                  make_uint2(pack_bf2(z[jz][pf][0], z[jz][pf][1]), pack_bf2(z[jz][pf][2], z[jz][pf][3]));
-          }
+        for (int jz = 0; jz < 2; ++jz) {
+          pk[jz][0] = pack_bf2(z[jz][pf][0], z[jz][pf][1]);
+          pk[jz][1] = pack_bf2(z[jz][pf][2], z[jz][pf][3]);
         }
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {  // odd rows of pk[0] <-> even rows of pk[1]
+          const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][d], pk[1][d], false, false);
+          pk[0][d] = sw[0];
+          pk[1][d] = sw[1];
+        }
+        const int ox = tx * TW + pf * 16 + col;
+        if (oy >= H || ox >= W) continue;
+        const int zc = (kq & 1) * 16 + (kq >> 1) * 8;
+        const long long zo = (((long long)n * H + oy) * W + ox) * a.out_ld + zc;
+        if (DV_BOUNDS(zo, 8, a.out_elems, "unpool_z out"))
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(a.out) + zo) =
+              make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
       }
     } else {  // ---- Cst -> global, 16 B per store ----
       const int tid = opaque_tid();

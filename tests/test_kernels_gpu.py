@@ -109,15 +109,20 @@ def test_conv_pool_epilogue(native_lib):
 @pytest.mark.parametrize("N,H,W,C,OC", [(2, 56, 56, 256, 256), (3, 28, 28, 512, 512), (2, 16, 14, 64, 128),
                                         (3, 10, 14, 64, 192), (1, 12, 12, 32, 48)])
 def test_conv_pool_epilogue_transposed(native_lib, monkeypatch, N, H, W, C, OC):
-    """Pooled-max epilogue with DPP-transposed 8-B stores (epilogue_pool_t) == the per-element stores
-    (DV_NO_POOL_T=1) bit for bit, values and switch codes; partial channel blocks (OC 48) and M tails."""
+    """Pooled-max epilogue with DPP-transposed 8-B stores (epilogue_pool_t) == staged through LDS
+    (epilogue_pool_lds, 16-B stores, DV_POOL_EPI=lds) == the per-element stores (DV_NO_POOL_T=1) bit for bit,
+    values and switch codes; partial channel blocks (OC 48: the 8-B path) and M tails."""
     monkeypatch.setenv("DV_NO_POOL_V3", "1")
     monkeypatch.setenv("DV_NO_HS16", "1")
     monkeypatch.setenv("DV_KW3", "0")
     g = torch.Generator().manual_seed(N * H + OC)
     x = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).to(DEV)
     cwd = _cw(OC, C).to_device(DEV)
-    got_p, got_c = ops.conv2d(x, cwd, relu=True, epilogue="pool")
+    got_p, got_c = ops.conv2d(x, cwd, relu=True, epilogue="pool")  # the register-transposed 8-B stores
+    monkeypatch.setenv("DV_POOL_EPI", "lds")  # LDS-staged 16-B stores where OC % 16 == 0 (opt-in)
+    lds_p, lds_c = ops.conv2d(x, cwd, relu=True, epilogue="pool")
+    monkeypatch.delenv("DV_POOL_EPI")
+    assert torch.equal(got_p, lds_p) and torch.equal(got_c, lds_c)
     monkeypatch.setenv("DV_NO_POOL_T", "1")
     ref_p, ref_c = ops.conv2d(x, cwd, relu=True, epilogue="pool")
     assert torch.equal(got_p, ref_p) and torch.equal(got_c, ref_c)
