@@ -73,6 +73,14 @@ def parse(argv=None):
                     help="DIAGNOSTIC ONLY (not a benchmark number): every step also copies (N-1) x the step's "
                          "mosaics device-to-device on a side stream, overlapping the next step, i.e. the HBM "
                          "writes and CU time an N-rank all-gather of the mosaics costs each rank")
+    ap.add_argument("--emulate-rccl-world", type=int, default=0,
+                    help="DIAGNOSTIC ONLY (not a benchmark number): model an N-rank all-gather of the mosaics on a "
+                         "side stream behind every step as RCCL runs it: --rccl-channels workgroups (CUs) busy "
+                         "for (N-1) x mosaic bytes / --rccl-gbs, writing those bytes to HBM (csrc/misc.hip:"
+                         "paced_copy_kernel), overlapping the next step's compute")
+    ap.add_argument("--rccl-channels", type=int, default=32, help="--emulate-rccl-world: CUs the collective holds")
+    ap.add_argument("--rccl-gbs", type=float, default=300.0,
+                    help="--emulate-rccl-world: all-gather receive bandwidth per GPU (GB/s, xGMI ring)")
     ap.add_argument("--profile", nargs="?", const="trace", default=None, choices=["trace", "pmc"],
                     help="re-run under rocprofv3 and print a per-kernel table (trace) [+ PMC pass]")
     return ap.parse_args(argv)
@@ -256,6 +264,20 @@ def main(argv=None):
             for r in range(emu_n):
                 emu_dst[r * B:(r + 1) * B].copy_(mosaic)
 
+    rccl_n = max(0, args.emulate_rccl_world - 1)
+    rccl_stream = torch.cuda.Stream(dev) if (cuda and rccl_n) else None
+    rccl_dst = torch.empty(rccl_n * B, 2 * S, 2 * S, 3, dtype=torch.uint8, device=dev) if rccl_stream else None
+
+    def emulate_rccl(mosaic):
+        """The all-gather's receive side as RCCL runs it: --rccl-channels CUs busy for the link time of
+        (N-1) mosaic-sized blocks, those bytes written to HBM (a paced copy), behind this step."""
+        ready = torch.cuda.Event()
+        ready.record()
+        rccl_stream.wait_event(ready)
+        mosaic.record_stream(rccl_stream)
+        with torch.cuda.stream(rccl_stream):
+            ops.native.lib().paced_copy(mosaic.contiguous(), rccl_dst, args.rccl_channels, args.rccl_gbs)
+
     def step(i, ev0=None):
         ops.resize_preprocess(images, xbuf)
         hook = (COPY_AT, issue_copy) if cuda and COPY_AT else None
@@ -264,6 +286,8 @@ def main(argv=None):
             issue_copy()  # no-op when the hook already issued step i-1's copy
         if emu_stream is not None:
             emulate_gather(res.mosaic)
+        if rccl_stream is not None:
+            emulate_rccl(res.mosaic)
         slot = i % 2
         if info.backend != "none" and not (JPEG and cuda):
             if pending[slot] is not None:
@@ -378,6 +402,11 @@ def main(argv=None):
     if emu_n:
         line["data"] = f"DIAGNOSTIC: + {emu_n} mosaic-sized D2D copies per step (emulated {emu_n + 1}-rank all-gather)"
         line["emulated_gather_bytes_per_step"] = int(emu_dst.numel())
+    if rccl_n:
+        line["data"] = (f"DIAGNOSTIC: + a paced {rccl_n + 1}-rank all-gather model per step ({args.rccl_channels} CUs, "
+                        f"{args.rccl_gbs} GB/s)")
+        line["emulated_gather_bytes_per_step"] = int(rccl_dst.numel())
+        line["emulated_gather_ms_per_step"] = round(rccl_dst.numel() / (args.rccl_gbs * 1e6), 3)
     if info.is_main:
         print(json.dumps(line), flush=True)
     pdist.shutdown()

@@ -2,8 +2,11 @@
 """DeepDream benchmarks (BASELINE configs 3 and 5; extensions beyond the reference).
 
   config 3: python bench_dream.py --model inception_v3 --batch 64 --size 299 --octaves 4 --steps 20
-  config 5: python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
-                bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 8 --dtype fp16
+  config 5: python bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 8 --dtype fp16   (1 GPU)
+            python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+                bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 32 --dtype fp16   (8 GPUs:
+            batch 32 gives each rank 4-16 (tile, image) units per step; at batch 8 a rank holds 1-4 and runs
+            latency-bound, profiles/dream_c5_r4_virtual_ranks.txt)
 
 One timed run = the whole octave loop (octaves x steps gradient-ascent iterations + octave
 resizes/detail re-injection) over the batch. Prints ONE JSON line (rank 0). Synthetic uint8
@@ -19,6 +22,7 @@ import time
 import torch
 
 from deconv_api_amd import ops
+import deconv_api_amd.engine.deepdream as D
 from deconv_api_amd.engine.deepdream import (RESNET_LAYERS, DeepDream, DreamSettings, TiledDeepDream,
                                              inception_preprocess)
 from deconv_api_amd.parallel import dist as pdist
@@ -41,6 +45,9 @@ def main(argv=None):
                     help="tiled only: time ONE rank's share of a W-rank dream on this GPU (no collective; "
                          "readiness sizing for config 5, not a dream result)")
     ap.add_argument("--virtual-rank", type=int, default=0)
+    ap.add_argument("--xgmi-gbs", type=float, default=300.0,
+                    help="--virtual-world: assumed all-gather receive bandwidth per GPU (GB/s) for the exposed-"
+                         "communication estimate (8 x MI355X RCCL all-gather over xGMI; not measured here)")
     a = ap.parse_args(argv)
     if a.virtual_world:
         return virtual_rank(a)
@@ -145,13 +152,24 @@ def virtual_rank(a) -> dict:
     for i, hw in enumerate(shapes):
         st = dd._tgraphs[(a.batch, hw[0], hw[1])]
         ms = sorted(per_oct[i])[len(per_oct[i]) // 2]
+        step_ms = ms / a.steps
+        gather_bytes = int(st.packs.numel() * st.packs.element_size())
+        # exposed communication estimate at --xgmi-gbs of all-gather receive bandwidth per GPU: one
+        # all-gather after the step (chunks 1) exposes all of it; with C chunks the last chunk's gather
+        # is exposed and the others hide behind the next chunk's network (ms per step)
+        comm = gather_bytes * (a.virtual_world - 1) / a.virtual_world / (a.xgmi_gbs * 1e9) * 1e3
+        C = max(1, min(D.TILE_CHUNKS, st.ucap))
+        exposed_c = comm / C + (C - 1) / C * max(0.0, comm - step_ms)
         rows.append({"octave": list(hw), "tiles": st.ntiles, "units_this_rank": st.mine, "units_all": st.plan.shape[0],
-                     "ms_per_step": round(ms / a.steps, 3), "ms_octave": round(ms, 2),
-                     "allgather_bytes_per_step": int(st.packs.numel() * st.packs.element_size())})
+                     "ms_per_step": round(step_ms, 3), "ms_octave": round(ms, 2),
+                     "allgather_bytes_per_step": gather_bytes, "comm_ms_per_step_est": round(comm, 3),
+                     "exposed_ms_per_step_est": {"chunks_1": round(comm, 3), f"chunks_{C}": round(exposed_c, 3)}})
     out = {"virtual_world": a.virtual_world, "virtual_rank": a.virtual_rank, "model": a.model, "batch": a.batch,
            "size": a.size, "tile": a.tile, "dtype": a.dtype, "octaves": rows,
            "ms_per_dream_batch_compute": round(sum(r["ms_octave"] for r in rows), 1),
-           "note": "one rank's share, no collective: compute-only lower bound of a W-rank dream batch"}
+           "xgmi_gbs_assumed": a.xgmi_gbs,
+           "note": "one rank's share, no collective: compute-only lower bound of a W-rank dream batch; comm / "
+                   "exposed figures are estimates at the assumed all-gather bandwidth, not measurements"}
     print(json.dumps(out), flush=True)
     return out
 

@@ -729,28 +729,32 @@ static void check_plan(const Tensor& plan, const Tensor& shift) {
   TORCH_CHECK(shift.scalar_type() == at::kInt && shift.numel() >= 2 && shift.stride(-1) == 1, "tile shift: int32 [2]");
 }
 
-void tile_gather(Tensor x, Tensor xin, Tensor plan, Tensor shift, int64_t rank, int64_t world) {
+// k0: the chunk's first unit among this rank's units (TiledDeepDream's overlapped all-gather)
+void tile_gather(Tensor x, Tensor xin, Tensor plan, Tensor shift, int64_t rank, int64_t world, int64_t k0) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check_plan(plan, shift);
   TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3, "tile_gather: x");
   TORCH_CHECK(xin.dim() == 4 && xin.size(3) == 8 && xin.is_contiguous(), "tile_gather: xin [U, Th, Tw, 8]");
   const int64_t U = xin.size(0);
-  TORCH_CHECK(world >= 1 && rank >= 0 && rank < world && rank + (U - 1) * world < plan.size(0), "tile_gather: units");
+  TORCH_CHECK(world >= 1 && rank >= 0 && rank < world && k0 >= 0 && rank + (k0 + U - 1) * world < plan.size(0),
+              "tile_gather: units");
   check_rc(dv::tile_gather_launch(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(xin.data_ptr()), plan.data_ptr<int>(),
-                                  shift.data_ptr<int>(), (int)U, (int)rank, (int)world, (int)x.size(1), (int)x.size(2),
-                                  (int)xin.size(1), (int)xin.size(2), dt_of(xin), cur_stream()),
+                                  shift.data_ptr<int>(), (int)U, (int)rank, (int)world, (int)k0, (int)x.size(1),
+                                  (int)x.size(2), (int)xin.size(1), (int)xin.size(2), dt_of(xin), cur_stream()),
            "tile_gather");
 }
 
-void tile_pack(Tensor g, Tensor pack, Tensor plan, Tensor lpart, Tensor lcoef, int64_t ucap, int64_t rank, int64_t world) {
+void tile_pack(Tensor g, Tensor pack, Tensor plan, Tensor lpart, Tensor lcoef, int64_t ucap, int64_t rank, int64_t world,
+               int64_t k0) {
   check_cuda(g, "g");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
   check_cuda(plan, "plan");
   TORCH_CHECK(plan.scalar_type() == at::kInt && plan.is_contiguous() && plan.dim() == 2 && plan.size(1) == 7, "plan");
   TORCH_CHECK(g.dim() == 4 && g.size(3) == 8 && g.is_contiguous(), "tile_pack: g [U, Th, Tw, 8]");
   const int64_t U = g.size(0), Th = g.size(1), Tw = g.size(2);
-  TORCH_CHECK(U <= ucap && rank + (U - 1) * world < plan.size(0), "tile_pack: units");
+  TORCH_CHECK(U <= ucap && k0 >= 0 && world >= 1 && rank >= 0 && rank < world && rank + (k0 + U - 1) * world < plan.size(0),
+              "tile_pack: units");
   TORCH_CHECK(pack.scalar_type() == g.scalar_type() && pack.is_contiguous() &&
                   pack.numel() >= dv::tile_pack_elems((int)ucap, (int)Th, (int)Tw) &&
                   reinterpret_cast<uintptr_t>(pack.data_ptr()) % 16 == 0,
@@ -760,19 +764,22 @@ void tile_pack(Tensor g, Tensor pack, Tensor plan, Tensor lpart, Tensor lcoef, i
   TORCH_CHECK(lcoef.scalar_type() == at::kFloat && lcoef.numel() == lpart.size(0), "tile_pack: lcoef [L]");
   check_rc(dv::tile_pack_launch(reinterpret_cast<const uint16_t*>(g.data_ptr()), reinterpret_cast<uint16_t*>(pack.data_ptr()),
                                 plan.data_ptr<int>(), lpart.data_ptr<float>(), lcoef.data_ptr<float>(), (int)lpart.size(0),
-                                (int)lpart.size(2), (int)U, (int)ucap, (int)rank, (int)world, (int)Th, (int)Tw, dt_of(g),
-                                cur_stream()),
+                                (int)lpart.size(2), (int)U, (int)ucap, (int)rank, (int)world, (int)k0, (int)Th, (int)Tw,
+                                dt_of(g), cur_stream()),
            "tile_pack");
 }
 
+// packs: [chunks][world][tile_pack_elems(ucap)] (chunks inferred), ucap = units per rank and chunk
 void tile_update(Tensor packs, int64_t ucap, Tensor plan, Tensor shift, Tensor x, Tensor done, Tensor loss, double step,
                  double max_loss, int64_t world, int64_t Th, int64_t Tw) {
   check_cuda(packs, "packs");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(packs.device());
   check_plan(plan, shift);
   const long long pe = dv::tile_pack_elems((int)ucap, (int)Th, (int)Tw);
-  TORCH_CHECK(packs.is_contiguous() && packs.numel() == world * pe, "tile_update: packs [world, pack_elems]");
-  TORCH_CHECK(plan.size(0) <= world * ucap, "tile_update: plan larger than the packs");
+  TORCH_CHECK(packs.is_contiguous() && world >= 1 && packs.numel() % (world * pe) == 0,
+              "tile_update: packs [chunks, world, pack_elems]");
+  const int64_t chunks = packs.numel() / (world * pe);
+  TORCH_CHECK(chunks >= 1 && plan.size(0) <= chunks * world * ucap, "tile_update: plan larger than the packs");
   TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3, "tile_update: x");
   TORCH_CHECK(done.scalar_type() == at::kByte && done.numel() == x.size(0) && loss.scalar_type() == at::kFloat &&
                   loss.numel() == x.size(0),
@@ -941,6 +948,17 @@ py::bytes jpeg_encode(Tensor img, int64_t quality) {
     s = dvjpeg::encode_jpeg(img.data_ptr<uint8_t>(), (int)img.size(0), (int)img.size(1), (int)quality);
   }
   return py::bytes(s);
+}
+
+// bench.py --emulate-rccl-world: a paced copy occupying `channels` CUs for bytes / gbs (an all-gather's
+// receive side at a given link bandwidth; misc.hip:paced_copy_kernel)
+void paced_copy(Tensor src, Tensor dst, int64_t channels, double gbs) {
+  check_cuda(src, "src");
+  check_cuda(dst, "dst");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous(), "paced_copy: contiguous tensors");
+  const int64_t sb = src.numel() * src.element_size(), db = dst.numel() * dst.element_size();
+  check_rc(dv::paced_copy_launch(src.data_ptr(), sb, dst.data_ptr(), db, (int)channels, gbs, cur_stream()), "paced_copy");
 }
 
 void softmax_rows(Tensor x, Tensor y) {
@@ -1230,8 +1248,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv", &stem_conv, "strided few-channel stem conv (direct VALU kernels), fwd (dir 0) / dgrad (dir 1)");
   m.def("sumsq_core_bwd", &sumsq_core_bwd, "DeepDream loss gradient (+ optional addend)", py::arg("x"),
         py::arg("scale"), py::arg("gx"), py::arg("b"), py::arg("addend") = py::none(), py::arg("part") = py::none());
-  m.def("tile_gather", &tile_gather, "tiled DeepDream: rolled tile gather into the 16-bit network input");
-  m.def("tile_pack", &tile_pack, "tiled DeepDream: owned-pixel gradient pack + unit loss / sum|g| tail");
+  m.def("tile_gather", &tile_gather, "tiled DeepDream: rolled tile gather into the 16-bit network input", py::arg("x"),
+        py::arg("xin"), py::arg("plan"), py::arg("shift"), py::arg("rank"), py::arg("world"), py::arg("k0") = 0);
+  m.def("tile_pack", &tile_pack, "tiled DeepDream: owned-pixel gradient pack + unit loss / sum|g| tail", py::arg("g"),
+        py::arg("pack"), py::arg("plan"), py::arg("lpart"), py::arg("lcoef"), py::arg("ucap"), py::arg("rank"),
+        py::arg("world"), py::arg("k0") = 0);
   m.def("tile_update", &tile_update, "tiled DeepDream: normalize + update the image from every rank's packs");
   m.def("tile_pack_elems", &tile_pack_elems);
   m.def("dream_update", &dream_update, "fused DeepDream normalize + update + next network input");
@@ -1241,6 +1262,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
   m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");
   m.def("softmax_rows", &softmax_rows, "row softmax (classifier head)");
+  m.def("paced_copy", &paced_copy, "bench: CU-occupying copy paced to a link bandwidth (all-gather interference model)");
   m.def("jpeg_gpu", &jpeg_gpu, "GPU baseline JPEG scans of uint8 [B,H,W,3] (restart per MCU row)");
   m.def("data_url_b64decode", &data_url_b64decode, "data URL payload -> bytes (lenient base64, GIL released)");
   m.def("jpeg_gpu_header", &jpeg_gpu_header, "SOI..SOS of the GPU encoder's streams");

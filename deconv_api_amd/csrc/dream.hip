@@ -233,13 +233,14 @@ __host__ __device__ inline long long tile_ustride(int Th, int Tw) { return ((lon
 // per-unit fp32 tail: {loss, sum |g| of pixel block 0 .. TP-1} (the pack kernel runs TP blocks per unit)
 constexpr int TP = 31, TAILF = TP + 1;
 
-// xin[k] (this rank's k-th unit, global unit u = rank + k * world) <- rolled-image tile, 8-channel 16-bit
+// xin[k] (this rank's (k0 + k)-th unit, global unit u = rank + (k0 + k) * world) <- rolled-image tile,
+// 8-channel 16-bit (k0: the first unit of a chunk of this rank's units, TiledDeepDream's overlapped steps)
 template <int DT>
 __global__ void __launch_bounds__(256) tile_gather_kernel(const float* __restrict__ x, uint16_t* __restrict__ xin,
                                                           const int* __restrict__ plan, const int* __restrict__ shift,
-                                                          int rank, int world, int H, int W, int Th, int Tw) {
+                                                          int rank, int world, int k0, int H, int W, int Th, int Tw) {
   const int k = blockIdx.y;
-  const int* pu = plan + (long long)(rank + k * world) * TPLAN;
+  const int* pu = plan + (long long)(rank + (k0 + k) * world) * TPLAN;
   const int b = pu[0], oy = pu[1], ox = pu[2];
   const int sy = shift[0], sx = shift[1];
   const float* xb = x + (long long)b * H * W * 3;
@@ -261,9 +262,9 @@ template <int DT>
 __global__ void __launch_bounds__(256) tile_pack_kernel(const uint16_t* __restrict__ g, uint16_t* __restrict__ pack,
                                                         const int* __restrict__ plan, const float* __restrict__ lpart,
                                                         const float* __restrict__ lcoef, int L, int lparts, int units,
-                                                        int ucap, int rank, int world, int Th, int Tw) {
+                                                        int ucap, int rank, int world, int k0, int Th, int Tw) {
   const int k = blockIdx.y;
-  const int* pu = plan + (long long)(rank + k * world) * TPLAN;
+  const int* pu = plan + (long long)(rank + (k0 + k) * world) * TPLAN;
   const int y0 = pu[3], y1 = pu[4], x0 = pu[5], x1 = pu[6];
   const int ow = x1 - x0, npix = (y1 - y0) * ow;
   const uint16_t* gk = g + (long long)k * Th * Tw * 8;
@@ -316,6 +317,9 @@ __global__ void __launch_bounds__(256) tile_pack_kernel(const uint16_t* __restri
 // x += step * (!done) * g / max(mean |g|, 1e-7) straight from the gathered packs of every rank
 // (each image pixel is owned by exactly one unit: no races); per-image loss and sum |g| come from
 // the unit tails (every block recomputes them; the done/loss writes are idempotent).
+// Packs are [chunks][world][pack_elems] of units_per_rank (= per chunk) units each: unit v lives on rank
+// v % world as local unit j = v / world, in chunk j / units_per_rank, slot j % units_per_rank (one chunk:
+// the un-chunked layout).
 __global__ void __launch_bounds__(256) tile_update_kernel(const uint16_t* __restrict__ packs, long long pack_elems,
                                                           int units_per_rank, const int* __restrict__ plan,
                                                           int nunits, const int* __restrict__ shift, float* __restrict__ x,
@@ -330,9 +334,11 @@ __global__ void __launch_bounds__(256) tile_update_kernel(const uint16_t* __rest
     float ls = 0.f, as = 0.f;
     for (int v = threadIdx.x; v < nunits; v += 64) {
       if (plan[(long long)v * TPLAN] != b) continue;
-      const float* tail = reinterpret_cast<const float*>(packs + (long long)(v % world) * pack_elems +
+      const int j = v / world;
+      const float* tail = reinterpret_cast<const float*>(packs +
+                                                         ((long long)(j / units_per_rank) * world + v % world) * pack_elems +
                                                          (long long)units_per_rank * tile_ustride(Th, Tw)) +
-                          (long long)TAILF * (v / world);
+                          (long long)TAILF * (j % units_per_rank);
       ls += tail[0];
       for (int q = 0; q < TP; ++q) as += tail[1 + q];
     }
@@ -350,7 +356,9 @@ __global__ void __launch_bounds__(256) tile_update_kernel(const uint16_t* __rest
   const int oy = pu[1], ox = pu[2], y0 = pu[3], y1 = pu[4], x0 = pu[5], x1 = pu[6];
   const int ow = x1 - x0, npix = (y1 - y0) * ow;
   const int sy = shift[0], sx = shift[1];
-  const uint16_t* src = packs + (long long)(u % world) * pack_elems + (long long)(u / world) * tile_ustride(Th, Tw);
+  const int ju = u / world;
+  const uint16_t* src = packs + ((long long)(ju / units_per_rank) * world + u % world) * pack_elems +
+                        (long long)(ju % units_per_rank) * tile_ustride(Th, Tw);
   float* xb = x + (long long)b * H * W * 3;
   for (int p = blockIdx.x * 256 + threadIdx.x; p < npix; p += gridDim.x * 256) {
     const int ty = y0 + p / ow, tx = x0 + p % ow;
@@ -364,31 +372,33 @@ __global__ void __launch_bounds__(256) tile_update_kernel(const uint16_t* __rest
 }
 
 long long tile_pack_elems(int ucap, int Th, int Tw) {
-  return (long long)ucap * (tile_ustride(Th, Tw) + 2 * TAILF + 4);  // + 2 halfs per fp32 tail entry
+  // + 2 halfs per fp32 tail entry; rounded to 8 elements so every pack of a [chunks][world][pack]
+  // buffer starts 16-B aligned (an odd unit count left 68-element tails 8-B aligned only)
+  return ((long long)ucap * (tile_ustride(Th, Tw) + 2 * TAILF + 4) + 7) & ~7LL;
 }
 
 int tile_gather_launch(const float* x, uint16_t* xin, const int* plan, const int* shift, int units, int rank, int world,
-                       int H, int W, int Th, int Tw, int dtype, hipStream_t s) {
-  if (units < 1 || units > 65535) return -1;
+                       int k0, int H, int W, int Th, int Tw, int dtype, hipStream_t s) {
+  if (units < 1 || units > 65535 || k0 < 0) return -1;
   const dim3 grid((unsigned)std::min((Th * Tw + 255) / 256, 512), (unsigned)units);
   if (dtype == DT_F16)
-    hipLaunchKernelGGL(tile_gather_kernel<DT_F16>, grid, dim3(256), 0, s, x, xin, plan, shift, rank, world, H, W, Th, Tw);
+    hipLaunchKernelGGL(tile_gather_kernel<DT_F16>, grid, dim3(256), 0, s, x, xin, plan, shift, rank, world, k0, H, W, Th, Tw);
   else
-    hipLaunchKernelGGL(tile_gather_kernel<DT_BF16>, grid, dim3(256), 0, s, x, xin, plan, shift, rank, world, H, W, Th, Tw);
+    hipLaunchKernelGGL(tile_gather_kernel<DT_BF16>, grid, dim3(256), 0, s, x, xin, plan, shift, rank, world, k0, H, W, Th, Tw);
   return (int)hipGetLastError();
 }
 
 int tile_pack_launch(const uint16_t* g, uint16_t* pack, const int* plan, const float* lpart, const float* lcoef, int L,
-                     int lparts, int units, int ucap, int rank, int world, int Th, int Tw, int dtype, hipStream_t s) {
-  if (units < 1 || units > ucap) return -1;
+                     int lparts, int units, int ucap, int rank, int world, int k0, int Th, int Tw, int dtype, hipStream_t s) {
+  if (units < 1 || units > ucap || k0 < 0) return -1;
   if (units > 65535) return -1;
   const dim3 grid((unsigned)TP, (unsigned)units);
   if (dtype == DT_F16)
     hipLaunchKernelGGL(tile_pack_kernel<DT_F16>, grid, dim3(256), 0, s, g, pack, plan, lpart, lcoef, L, lparts, units,
-                       ucap, rank, world, Th, Tw);
+                       ucap, rank, world, k0, Th, Tw);
   else
     hipLaunchKernelGGL(tile_pack_kernel<DT_BF16>, grid, dim3(256), 0, s, g, pack, plan, lpart, lcoef, L, lparts, units,
-                       ucap, rank, world, Th, Tw);
+                       ucap, rank, world, k0, Th, Tw);
   return (int)hipGetLastError();
 }
 

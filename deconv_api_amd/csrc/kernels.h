@@ -163,10 +163,11 @@ int octave_resize_launch(const float* a, const float* b, const float* c, float* 
 // tiled DeepDream step: rolled tile gather -> owned-pixel pack (+ unit loss / sum|g| tail) ->
 // [all-gather of packs over ranks] -> update of the fp32 image straight from the packs
 int tile_gather_launch(const float* x, uint16_t* xin, const int* plan, const int* shift, int units, int rank, int world,
-                       int H, int W, int Th, int Tw, int dtype, hipStream_t s);
+                       int k0, int H, int W, int Th, int Tw, int dtype, hipStream_t s);
 int tile_pack_launch(const uint16_t* g, uint16_t* pack, const int* plan, const float* lpart, const float* lcoef, int L,
-                     int lparts, int units, int ucap, int rank, int world, int Th, int Tw, int dtype, hipStream_t s);
+                     int lparts, int units, int ucap, int rank, int world, int k0, int Th, int Tw, int dtype, hipStream_t s);
 long long tile_pack_elems(int ucap, int Th, int Tw);  // 16-bit elements of one rank's pack
+// packs: [chunks][world][pack_elems], units_per_rank = units per rank and chunk (dream.hip:tile_update_kernel)
 int tile_update_launch(const uint16_t* packs, long long pack_elems, int units_per_rank, const int* plan, int nunits,
                        const int* shift, float* x, uint8_t* done, float* loss, float step, float max_loss, int world,
                        int H, int W, int Th, int Tw, int dtype, hipStream_t s);
@@ -201,6 +202,9 @@ int jpeg_gpu_launch(const uint8_t* rgb, int B, int H, int W, const void* tables,
                     long long* off, hipStream_t s);
 // row softmax (fp32 [M][N])
 int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s);
+// bench.py --emulate-rccl-world: `channels` workgroups copy `bytes` (src repeated) paced to `gbs` GB/s (misc.hip)
+int paced_copy_launch(const void* src, long long src_bytes, void* dst, long long bytes, int channels, double gbs,
+                      hipStream_t s);
 // halo-tile 3x3/s1/p1 conv for OC tiles of 16/64 at large spatial sizes (optional fused unpool)
 int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, bool* stats_done = nullptr);
 // 3x3 conv 64 -> 64 + bias + ReLU + fused 2x2 max-pool/switch (bf16); < 0 if the shape is unsupported

@@ -695,4 +695,48 @@ int softmax_rows_launch(const float* x, float* y, int M, int N, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ---- RCCL all-gather interference model (bench.py --emulate-rccl-world) ----
+// A collective's kernel occupies its channels' CUs for as long as the data takes to cross the links, not
+// for the HBM time of a local copy (the round-4 D2D-copy emulation ran ~10x shorter than an xGMI transfer
+// of the same bytes). `channels` workgroups (one per RCCL channel) copy `bytes` in 16-B vector chunks,
+// each workgroup pacing itself against the 100 MHz wall clock so that the whole copy takes bytes /
+// bytes_per_us microseconds: the model of an all-gather's receive side (its CUs busy, its bytes written
+// to HBM) at a given link bandwidth, running beside the next step's compute on another stream.
+__global__ void __launch_bounds__(256) paced_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                         long long n16, long long src16, double ticks_per_16b) {
+  const long long per = (n16 + gridDim.x - 1) / gridDim.x;
+  const long long lo = (long long)blockIdx.x * per, hi = min(n16, lo + per);
+  const unsigned long long t0 = wall_clock64();
+  constexpr int CHUNK = 256 * 8;  // 16-B elements per paced chunk (32 KiB)
+  for (long long c = lo; c < hi; c += CHUNK) {
+    // this chunk may start once the pace allows: (c - lo) elements at ticks_per_16b each
+    const unsigned long long due = t0 + (unsigned long long)((double)(c - lo) * ticks_per_16b);
+    for (int guard = 0; wall_clock64() < due && guard < (1 << 20); ++guard) __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const long long i = c + k * 256 + threadIdx.x;
+      if (i < hi) dst[i] = src[i % src16];
+    }
+  }
+}
+
+int paced_copy_launch(const void* src, long long src_bytes, void* dst, long long bytes, int channels, double gbs,
+                      hipStream_t s) {
+  if (channels < 1 || channels > 1024 || bytes < 16 || src_bytes < 16 || gbs <= 0 ||
+      (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15))
+    return -1;
+  const long long n16 = bytes / 16;
+  const long long per = (n16 + channels - 1) / channels;
+  // each workgroup moves `per` 16-B elements in bytes / gbs: ticks (100 MHz) per element
+  const double total_us = (double)bytes / (gbs * 1e3);
+  int dev = 0, khz = 100000;  // wall_clock64 rate (100 MHz on gfx9)
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+      khz <= 0)
+    khz = 100000;
+  const double ticks_per_16b = total_us * (khz / 1000.0) / (double)per;
+  hipLaunchKernelGGL(paced_copy_kernel, dim3((unsigned)channels), dim3(256), 0, s, reinterpret_cast<const uint4*>(src),
+                     reinterpret_cast<uint4*>(dst), n16, src_bytes / 16, ticks_per_16b);
+  return (int)hipGetLastError();
+}
+
 }  // namespace dv

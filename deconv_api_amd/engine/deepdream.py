@@ -63,6 +63,11 @@ LOSS_PARTS = 32
 # DV_DREAM_OCTAVE_RESIZE=0: octave transitions as F.interpolate + ATen adds (A/B); default: one
 # octave_resize HIP launch per transition writing the next octave's static inputs directly
 OCTAVE_RESIZE = os.environ.get("DV_DREAM_OCTAVE_RESIZE", "1") != "0"
+# DV_TILE_CHUNKS: a rank's units per tiled step run as this many chunks when the step all-gathers
+# (several ranks): chunk c's pack all-gather (async, on the collective's own stream; captured into
+# the octave graph) overlaps chunk c+1's network, tile_update waits for all of them. 1: one
+# all-gather after the whole network (round-4 behaviour). Without a collective: always 1.
+TILE_CHUNKS = max(1, int(os.environ.get("DV_TILE_CHUNKS", "2")))
 
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
 
@@ -539,6 +544,21 @@ class TiledDeepDream(DeepDream):
         assert ((plan[:, 5] >= 0) & (plan[:, 5] < plan[:, 6]) & (plan[:, 6] <= Tw)).all()
         return Th, Tw, plan, len(tiles)
 
+    def _chunk_states(self, st, rank: int, mine: int):
+        """Per-chunk sub-states of rank ``rank``'s ``mine`` units (chunk c = local units c*ucc ..):
+        own 16-bit network input / loss partials / scales, its slot of chunk c's packs."""
+        chunks = []
+        for c in range(st.C):
+            cs = type("TileChunk", (), {})()
+            cs.k0 = c * st.ucc
+            cs.n = max(0, min(mine, (c + 1) * st.ucc) - cs.k0)
+            cs.pack = st.packs[c, rank]
+            cs.xin = torch.zeros(max(cs.n, 1), st.Th, st.Tw, 8, dtype=self.dtype, device=self.device, requires_grad=True)
+            cs.lpart = torch.zeros(len(self.s.layers), max(cs.n, 1), LOSS_PARTS, device=self.device)
+            cs.lcoef, cs.scales = None, None
+            chunks.append(cs)
+        return chunks
+
     def _tstate(self, B: int, H: int, W: int):
         key = (B, H, W)
         if key in self._tgraphs:
@@ -554,35 +574,41 @@ class TiledDeepDream(DeepDream):
         mine = len(range(rank, nunits, world))
         st = type("TileState", (), {})()
         st.Th, st.Tw, st.ntiles, st.world, st.rank, st.ucap, st.mine = Th, Tw, ntiles, world, rank, ucap, mine
+        probe = type("P", (), {"world": world})()
+        st.C = min(TILE_CHUNKS, ucap) if self._collective(probe) else 1
+        st.ucc = -(-ucap // st.C)  # units per rank and chunk
         st.plan = plan.to(dev)
         st.x = torch.zeros(B, H, W, 3, device=dev)
         st.done = torch.zeros(B, dtype=torch.uint8, device=dev)
         st.loss = torch.zeros(B, device=dev)
         st.shifts = torch.zeros(self.s.iterations, 2, dtype=torch.int32, device=dev)
-        pe = lib.tile_pack_elems(ucap, Th, Tw)
-        st.packs = torch.zeros(world, pe, dtype=self.dtype, device=dev)
-        st.pack = st.packs[rank]
-        st.xin = torch.zeros(max(mine, 1), Th, Tw, 8, dtype=self.dtype, device=dev, requires_grad=True)
-        st.lpart = torch.zeros(len(self.s.layers), max(mine, 1), LOSS_PARTS, device=dev)
-        st.lcoef, st.scales, st.graph, st.step_graph = None, None, None, None
+        pe = lib.tile_pack_elems(st.ucc, Th, Tw)
+        st.packs = torch.zeros(st.C, world, pe, dtype=self.dtype, device=dev)  # [chunk][rank][pack]
+        st.chunks = self._chunk_states(st, rank, mine)
+        st.graph, st.step_graph = None, None
         self._tgraphs[key] = st
         while len(self._tgraphs) > max(1, self.graph_cache):
             self._tgraphs.popitem(last=False)
             torch.cuda.empty_cache()
         return st
 
-    def _tile_compute(self, st, it: int) -> None:
-        """gather -> network fwd/bwd -> pack, for step ``it`` (shift row it of the device table)."""
-        lib = native.lib()
-        if st.mine == 0:
+    def _tile_compute_chunk(self, st, cs, it: int, rank: int) -> None:
+        """gather -> network fwd/bwd -> pack for one chunk of a rank's units, step ``it``."""
+        if cs.n == 0:
             return
-        lib.tile_gather(st.x, st.xin, st.plan, st.shifts[it], st.rank, st.world)
-        g = self._loss_grad(st, st.xin)
-        lib.tile_pack(g.contiguous(), st.pack, st.plan, st.lpart, st.lcoef, st.ucap, st.rank, st.world)
+        lib = native.lib()
+        lib.tile_gather(st.x, cs.xin, st.plan, st.shifts[it], rank, st.world, cs.k0)
+        g = self._loss_grad(cs, cs.xin)
+        lib.tile_pack(g.contiguous(), cs.pack, st.plan, cs.lpart, cs.lcoef, st.ucc, rank, st.world, cs.k0)
+
+    def _tile_compute(self, st, it: int) -> None:
+        """every chunk of this rank's units for step ``it`` (shift row it of the device table)."""
+        for cs in st.chunks:
+            self._tile_compute_chunk(st, cs, it, st.rank)
 
     def _tile_apply(self, st, it: int) -> None:
         ml = -1.0 if self.s.max_loss is None else float(self.s.max_loss) * st.ntiles
-        native.lib().tile_update(st.packs, st.ucap, st.plan, st.shifts[it], st.x, st.done, st.loss, float(self.s.step),
+        native.lib().tile_update(st.packs, st.ucc, st.plan, st.shifts[it], st.x, st.done, st.loss, float(self.s.step),
                                  ml, st.world, st.Th, st.Tw)
 
     def _collective(self, st) -> bool:
@@ -604,17 +630,34 @@ class TiledDeepDream(DeepDream):
         else:
             self.coll_wait(fn(*args, async_op=True))
 
-    def _tile_steps(self, st, capturing: bool = False) -> None:
+    def _gather_chunk(self, st, c: int):
+        """Async all-gather of chunk c's packs (every rank's slot) -> the work object."""
         import torch.distributed as dist
 
+        return dist.all_gather_into_tensor(st.packs[c].view(-1), st.packs[c, st.rank], async_op=True)
+
+    def _finish(self, work) -> None:
+        if self.coll_wait is None:
+            work.wait()  # stream-ordered: the current stream waits for the collective's stream
+        else:
+            self.coll_wait(work)
+
+    def _tile_steps(self, st, capturing: bool = False) -> None:
+        """The octave's steps. With a collective, chunk c's all-gather is issued right after its pack
+        and runs on the collective's stream while chunk c+1's network runs on this one; the update
+        waits for every chunk's gather (captured as graph edges when ``capturing``)."""
         coll = self._collective(st)
         for it in range(self.s.iterations):
-            self._tile_compute(st, it)
-            if coll:
-                if capturing:  # recorded into the octave graph: nothing to wait for here
-                    dist.all_gather_into_tensor(st.packs.view(-1), st.pack)
+            works = []
+            for c, cs in enumerate(st.chunks):
+                self._tile_compute_chunk(st, cs, it, st.rank)
+                if coll:
+                    works.append(self._gather_chunk(st, c))
+            for w in works:
+                if capturing:
+                    w.wait()  # recorded into the octave graph: nothing to poll here
                 else:
-                    self._coll(dist.all_gather_into_tensor, st.packs.view(-1), st.pack)
+                    self._finish(w)
             self._tile_apply(st, it)
 
     def _stage_shifts(self, st) -> None:
@@ -644,25 +687,69 @@ class TiledDeepDream(DeepDream):
         return capture(fn)[0]
 
     def _gradient_ascent_fused(self, x: torch.Tensor) -> torch.Tensor:
-        import torch.distributed as dist
-
         B, H, W, _ = x.shape
         st = self._tstate(B, H, W)
-        self._stage_shifts(st)
         st.x.copy_(x)
+        self._ascend_tiled(st)
+        return st.x.clone()
+
+    def octave_steps(self, x: torch.Tensor):
+        """The tiled dream's octaves (see DeepDream.octave_steps). On the fused GPU path every octave
+        transition is ONE octave_resize launch straight into the next octave's static fp32 image (the
+        tiles gather their 16-bit inputs from it), as the untiled fused path does; the generic path
+        (F.interpolate x4 + two adds per transition) is the CPU / DV_DREAM_OCTAVE_RESIZE=0 oracle."""
+        if self.tile_fused and x.is_cuda and OCTAVE_RESIZE:
+            yield from self._tiled_octave_steps_fused(x)
+            return
+        yield from DeepDream.octave_steps(self, x)
+
+    def _tiled_octave_steps_fused(self, x: torch.Tensor):
+        lib = native.lib()
+        shapes = self.octave_shapes(x.shape[1], x.shape[2])
+        x = x.contiguous()
+        B = x.shape[0]
+        dev = x.device
+
+        def resized(src, hw):
+            if tuple(hw) == tuple(src.shape[1:3]):
+                return src
+            dst = torch.empty(B, *hw, 3, device=dev)
+            lib.octave_resize(src, None, None, dst, None)
+            return dst
+
+        img = same = up = prev = None
+        for o, hw in enumerate(shapes):
+            st = self._tstate(B, *hw)
+            lib.octave_resize(x if o == 0 else img, same, up, st.x, None)
+            cur = resized(x, hw)
+            same, up = (None, None) if o == 0 else (cur, resized(prev, hw))
+            prev = cur
+            self._ascend_tiled(st)
+            img = st.x
+            if o + 1 < len(shapes):
+                yield img
+        out = torch.empty_like(img)
+        lib.octave_resize(img, same, up, out, None)
+        yield out
+
+    def _ascend_tiled(self, st) -> None:
+        """The octave's ``iterations`` tiled steps on a state whose st.x holds the octave's input."""
+        import torch.distributed as dist
+
+        self._stage_shifts(st)
         st.done.zero_()
         coll = self._collective(st)
         if self.tile_graphs and st.graph is None and st.step_graph is None:
             # warm up on a side stream (autograd / allocator), restore the image, capture the octave
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
-            work = None
+            works = []
             with torch.cuda.stream(s):
                 self._tile_compute(st, 0)
                 if coll:  # the collective's communicator is set up outside the capture
-                    work = dist.all_gather_into_tensor(st.packs.view(-1), st.pack, async_op=True)
+                    works = [self._gather_chunk(st, c) for c in range(st.C)]
             torch.cuda.current_stream(self.device).wait_stream(s)
-            if coll:  # retire the eager warm-up collective before the capture opens
+            for work in works:  # retire the eager warm-up collectives before the capture opens
                 drain_collective(work, self.device, self.coll_wait)
             if not coll or CAPTURE_COLLECTIVE:
                 # the whole octave, all-gathers included (RCCL collectives are graph-capturable):
@@ -682,47 +769,41 @@ class TiledDeepDream(DeepDream):
         elif st.step_graph is not None:
             for it in range(self.s.iterations):
                 st.step_graph[it].replay()
-                self._coll(dist.all_gather_into_tensor, st.packs.view(-1), st.pack)
+                for c in range(st.C):
+                    self._coll(dist.all_gather_into_tensor, st.packs[c].view(-1), st.packs[c, st.rank])
                 self._tile_apply(st, it)
         else:
             self._tile_steps(st)
-        return st.x.clone()
 
-    def virtual_octave(self, x: torch.Tensor, world: int) -> torch.Tensor:
+    def virtual_octave(self, x: torch.Tensor, world: int, chunks: int = TILE_CHUNKS) -> torch.Tensor:
         """One octave of the ``world``-rank fused tiled step on THIS device, without collectives: for
         every step each virtual rank gathers its units, runs the network and packs into its own slot
-        of the packs buffer (exactly what the all-gather assembles on every real rank), then ONE
+        of the packs buffer (chunked as a real rank would: ``chunks`` slices of its units, packs
+        [chunk][rank]), exactly what the all-gathers assemble on every real rank, then ONE
         tile_update with ``world`` packs applies the step. Eager; for tests / tools (the multi-rank
-        kernels' rank/world indexing exercised on a one-GPU box)."""
+        kernels' rank/world/chunk indexing exercised on a one-GPU box)."""
         lib = native.lib()
         B, H, W, _ = x.shape
         Th, Tw, plan, ntiles = self._gplan(B, H, W)
         nunits = plan.shape[0]
         ucap = -(-nunits // world)
         dev = self.device
-        plan = plan.to(dev)
-        pe = lib.tile_pack_elems(ucap, Th, Tw)
-        packs = torch.zeros(world, pe, dtype=self.dtype, device=dev)
         st = type("TileState", (), {})()
-        st.Th, st.Tw, st.ntiles, st.world, st.ucap, st.plan = Th, Tw, ntiles, world, ucap, plan
+        st.Th, st.Tw, st.ntiles, st.world, st.ucap = Th, Tw, ntiles, world, ucap
+        st.C = max(1, min(chunks, ucap))
+        st.ucc = -(-ucap // st.C)
+        st.plan = plan.to(dev)
+        st.packs = torch.zeros(st.C, world, lib.tile_pack_elems(st.ucc, Th, Tw), dtype=self.dtype, device=dev)
         st.x = x.clone()
         st.done = torch.zeros(B, dtype=torch.uint8, device=dev)
         st.loss = torch.zeros(B, device=dev)
         st.shifts = torch.zeros(self.s.iterations, 2, dtype=torch.int32, device=dev)
         self._stage_shifts(st)
-        st.packs = packs
-        st.lcoef, st.scales = None, None
-        ranks = []
-        for r in range(world):
-            rs = type("TileRank", (), {})()
-            rs.__dict__.update(st.__dict__)
-            rs.rank, rs.mine, rs.pack = r, len(range(r, nunits, world)), packs[r]
-            rs.xin = torch.zeros(max(rs.mine, 1), Th, Tw, 8, dtype=self.dtype, device=dev, requires_grad=True)
-            rs.lpart = torch.zeros(len(self.s.layers), max(rs.mine, 1), LOSS_PARTS, device=dev)
-            ranks.append(rs)
+        ranks = [self._chunk_states(st, r, len(range(r, nunits, world))) for r in range(world)]
         for it in range(self.s.iterations):
-            for rs in ranks:
-                self._tile_compute(rs, it)
+            for r, chunks_r in enumerate(ranks):
+                for cs in chunks_r:
+                    self._tile_compute_chunk(st, cs, it, r)
             self._tile_apply(st, it)
         return st.x
 

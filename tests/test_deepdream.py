@@ -415,7 +415,8 @@ def test_gpu_split_batch_streams(native_lib):
 @pytest.mark.parametrize("max_loss", [None, 1e-9])
 def test_gpu_tiled_fused_equals_torch(native_lib, max_loss):
     """Fused tiled step (HIP rolled gather, owned-pixel packs with loss/|g| tails, pack-driven
-    update; one hipGraph per octave incl. all steps) == the torch tiled implementation, on a shape
+    update; one hipGraph per octave incl. all steps; octave transitions as ONE octave_resize launch
+    each) == the torch tiled implementation (F.interpolate + adds between octaves), on a shape
     whose tiles overlap (200 x 260 with 128 tiles -> 2 x 3 tiles of 100 x 87)."""
     net = ResNet50(0).build("cuda", torch.float16)
     x = (torch.rand(2, 200, 260, 3, generator=torch.Generator().manual_seed(8)) * 2 - 1).cuda()
@@ -429,8 +430,9 @@ def test_gpu_tiled_fused_equals_torch(native_lib, max_loss):
             assert dd.tile_fused
             got = dd.run(x)
             assert torch.isfinite(got).all()
-            if max_loss is not None:  # every image stops at its first step: nothing moves
-                assert (got - want).abs().max() < 1e-5, (iters, graphs)
+            if max_loss is not None:  # every image stops at its first step: only the octave arithmetic
+                # (octave_resize vs F.interpolate: fp32 rounding of the same bilinear weights)
+                assert (got - want).abs().max() < 1e-4, (iters, graphs)
             else:  # same gradients up to 16-bit rounding of the first step's inputs (tools/diag_tiled.py)
                 assert _cos(got - x, want - x) > (0.998 if iters == 1 else 0.99), (iters, graphs)
             got2 = dd.run(x)  # replay of the cached state/graph (fresh shifts from the generator)
@@ -556,13 +558,14 @@ def test_gpu_pool_backward_accumulate(native_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_gpu_tiled_virtual_ranks_match_one_rank(native_lib, world):
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 1), (2, 2), (3, 3)])
+def test_gpu_tiled_virtual_ranks_match_one_rank(native_lib, world, chunks):
     """The multi-rank fused tiled step (each rank's tile_gather / network / tile_pack into ITS slot
     of the packs, then tile_update over ``world`` packs) run for virtual ranks on one GPU equals the
     1-rank octave: the rank/world indexing of tile_pack (unit offsets, ucap) and tile_update (world
-    packs) is exercised without a multi-GPU box. Units land in different rank batches, so conv tile
-    choices (and fp32 summation order) differ slightly: compared up to rounding."""
+    packs, chunked [chunk][rank] layouts) is exercised without a multi-GPU box. Units land in different
+    rank / chunk batches, so conv tile choices (and fp32 summation order) differ slightly: compared up
+    to rounding."""
     from deconv_api_amd.models.resnet50 import ResNet50
 
     net = ResNet50(0).build("cuda", torch.float16)
@@ -571,7 +574,7 @@ def test_gpu_tiled_virtual_ranks_match_one_rank(native_lib, world):
     for iters, cos_min, mean_max in ((1, 0.9995, 1e-3), (3, 0.995, 3e-3)):
         s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=1, iterations=iters, max_loss=None)
         ref = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).gradient_ascent(x)
-        got = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).virtual_octave(x, world)
+        got = TiledDeepDream(net, s, tile=128, seed=11, use_graphs=False).virtual_octave(x, world, chunks)
         d = (got - ref).abs()
         c = _cos((got - x).flatten().cpu(), (ref - x).flatten().cpu())
         assert c > cos_min, (iters, c)
@@ -582,7 +585,9 @@ def test_gpu_tiled_virtual_ranks_match_one_rank(native_lib, world):
 def test_gpu_tiled_collective_octave_captured(native_lib):
     """torchrun, one rank, DV_TILE_COLLECTIVE=1: the collective code path of the tiled octave (the
     per-step all-gather of the packs over RCCL) is captured INSIDE the octave's hipGraph and equals
-    the collective-free 1-rank octave bit for bit."""
+    the collective-free 1-rank octave bit for bit; the chunked overlapped step (DV_TILE_CHUNKS=2: each
+    chunk's async all-gather beside the next chunk's network, both captured) equals it up to the conv
+    rounding of the smaller per-chunk batches."""
     import json
     import os
     import socket
@@ -605,6 +610,9 @@ def test_gpu_tiled_collective_octave_captured(native_lib):
     assert out["backend"] == "nccl" and out["collective"] is True, out
     assert out["octave_graph"] is True and out["step_graphs"] is False, out
     assert out["equal"] is True, out
+    # chunked overlap (2 chunks: chunk 0's all-gather captured beside chunk 1's network)
+    assert out["chunks"] == 2 and out["chunked_octave_graph"] is True, out
+    assert out["chunked_cos"] > 0.995 and out["chunked_maxdiff"] < 5e-2, out
 
 
 @pytest.mark.gpu

@@ -21,7 +21,7 @@ for hw in [(71, 93), (200, 260)]:
     for r in range(20):
         dd._tile_compute(st, 0)
         torch.cuda.synchronize()
-        p = st.pack.clone().view(torch.int16)
+        p = st.packs[0, st.rank].clone().view(torch.int16)
         if ref is None:
             ref = p
         elif not torch.equal(p, ref):

@@ -28,11 +28,11 @@ for sh in [(0, 0), (17, -33)]:
     st.shifts[0] = torch.tensor(sh, dtype=torch.int32)
     dd._tile_compute(st, 0)
     torch.cuda.synchronize()
-    pk = st.pack.float().cpu()
+    pk = st.packs[0, st.rank].float().cpu()
     pl = st.plan.cpu()
     us = ((st.Th * st.Tw * 3 + 7) // 8) * 8
     full = torch.zeros(B, H, W, 3)
-    tail = st.pack[st.ucap * us:].view(torch.float32).cpu()[: 32 * pl.shape[0]].view(-1, 32)[:, :2].reshape(-1) if dt == torch.float16 else None
+    tail = st.packs[0, st.rank][st.ucc * us:].view(torch.float32).cpu()[: 32 * pl.shape[0]].view(-1, 32)[:, :2].reshape(-1) if dt == torch.float16 else None
     for u in range(pl.shape[0]):
         b, oy, ox, y0, y1, x0, x1 = pl[u].tolist()
         blk = pk[u * us: u * us + (y1 - y0) * (x1 - x0) * 3].view(y1 - y0, x1 - x0, 3)

@@ -6,7 +6,9 @@
 Runs one octave with the collective path forced on (DV_TILE_COLLECTIVE semantics: the per-step
 all-gather of the packs over the process group) and captured inside the octave's hipGraph, and the
 same octave without collectives; prints one JSON line: backend, whether the collective path ran,
-whether the octave was ONE graph (collectives captured) or per-step graphs, and bit equality."""
+whether the octave was ONE graph (collectives captured) or per-step graphs, and bit equality. Then the
+chunked overlapped step (DV_TILE_CHUNKS semantics: each chunk's async all-gather captured beside the
+next chunk's network): equal to the collective-free octave up to the conv rounding of smaller batches."""
 import json
 import os
 import sys
@@ -29,6 +31,7 @@ def main():
     D.TILE_COLLECTIVE = False
     ref = D.TiledDeepDream(net, s, tile=128, info=info, seed=5).gradient_ascent(x)
     D.TILE_COLLECTIVE = True
+    D.TILE_CHUNKS = 1
     dd = D.TiledDeepDream(net, s, tile=128, info=info, seed=5)
     got = dd.gradient_ascent(x)
     got2 = D.TiledDeepDream(net, s, tile=128, info=info, seed=5).gradient_ascent(x)  # fresh capture, replay
@@ -37,6 +40,16 @@ def main():
     out = {"backend": info.backend, "world": info.world, "collective": dd._collective(st),
            "octave_graph": st.graph is not None, "step_graphs": st.step_graph is not None,
            "equal": bool(torch.equal(got, ref)) and bool(torch.equal(got2, ref))}
+    D.TILE_CHUNKS = 2
+    dc = D.TiledDeepDream(net, s, tile=128, info=info, seed=5)
+    gc = dc.gradient_ascent(x)
+    gc2 = dc.gradient_ascent(x)  # replay of the captured chunked octave (fresh rolls)
+    torch.cuda.synchronize()
+    stc = next(iter(dc._tgraphs.values()))
+    a, b = (gc - x).flatten().double(), (ref - x).flatten().double()
+    out.update({"chunks": stc.C, "chunked_octave_graph": stc.graph is not None,
+                "chunked_cos": float(a @ b / (a.norm() * b.norm() + 1e-30)),
+                "chunked_maxdiff": float((gc - ref).abs().max()), "chunked_rerun_finite": bool(torch.isfinite(gc2).all())})
     if info.is_main:
         print(json.dumps(out), flush=True)
     pdist.shutdown()
