@@ -305,7 +305,7 @@ class DeepDream:
     def run(self, x: torch.Tensor) -> torch.Tensor:
         """x: preprocessed fp32 [B, H, W, 3] on the engine device -> dreamed fp32 image."""
         n = self.split if (self.fused and x.is_cuda) else 1
-        if n <= 1 or x.shape[0] % n or x.shape[0] < n:
+        if n <= 1 or x.shape[0] < n:  # (uneven sub-batches allowed: x.chunk)
             return self._run_one(x)
         cur = torch.cuda.current_stream(self.device)
         while len(self._streams) < n:

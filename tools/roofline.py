@@ -118,22 +118,33 @@ def family(name: str) -> str:
     return re.sub(r"<.*", "", name)
 
 
-def db_families(db: str, last_frac: float):
+def db_families(db: str, last_frac: float, marker: str = "", last_units: int = 0):
+    """Per-family (launches, ms) over the window; with ``marker`` the window is from the first to the last
+    launch of that kernel family in the trace's last fraction, i.e. exactly (markers - 1) units of work."""
     c = sqlite3.connect(db)
-    rows = c.execute("select name, start, end from kernels").fetchall()
+    rows = sorted(c.execute("select name, start, end from kernels").fetchall(), key=lambda r: r[1])
     t0, t1 = min(r[1] for r in rows), max(r[2] for r in rows)
     cut = t1 - (t1 - t0) * last_frac
+    end = None
+    units = None
+    if marker:
+        ms = [r[1] for r in rows if r[1] >= cut and marker in r[0]]
+        if last_units > 0:
+            ms = ms[-(last_units + 1):]
+        if len(ms) >= 2:
+            cut, end, units = ms[0], ms[-1], len(ms) - 1
     agg = defaultdict(lambda: [0, 0.0])
     lo = hi = None
     for n, s, e in rows:
-        if s < cut:
+        if s < cut or (end is not None and s >= end):
             continue
         a = agg[family(n)]
         a[0] += 1
         a[1] += (e - s) / 1e6  # ms
         lo = s if lo is None else min(lo, s)
         hi = e if hi is None else max(hi, e)
-    return agg, (hi - lo) / 1e6
+    span = (end - cut) / 1e6 if end is not None else (hi - lo) / 1e6
+    return agg, span, units
 
 
 def main(argv=None):
@@ -141,9 +152,15 @@ def main(argv=None):
     ap.add_argument("--config", type=int, choices=[2, 3, 5], required=True)
     ap.add_argument("--img-per-s", type=float, default=0.0, help="measured rate (bench JSON value)")
     ap.add_argument("--db", default="", help="rocprofv3 kernel-trace results db")
+    ap.add_argument("--last-units", type=int, default=0, help="db + --unit-marker: only the last N units")
+    ap.add_argument("--marker-per-unit", type=float, default=1.0,
+                    help="db: marker launches per unit (config 3: 160 dream_update per batch; 5: 80 tile_update)")
     ap.add_argument("--db-units", type=float, default=1.0,
                     help="units of work (config-2 steps / dream batches) in the db window")
     ap.add_argument("--last-frac", type=float, default=1.0, help="db: only the last fraction of the trace")
+    ap.add_argument("--unit-marker", default="",
+                    help="db: a kernel launched once per unit of work (config 2: resize_preprocess; 3 / 5: "
+                         "dream_update / tile_update x steps): the window spans whole units between its launches")
     a = ap.parse_args(argv)
     total, rows, imgs = {2: config2, 3: config3, 5: config5}[a.config]()
     unit = {2: "step (256 images, K = 4)", 3: "dream batch (64 images)", 5: "dream batch (8 images)"}[a.config]
@@ -159,9 +176,9 @@ def main(argv=None):
         print(f"measured {a.img_per_s:.1f} img/s = {ms:.2f} ms per unit: {pf:.3f} PF/s = "
               f"{100 * pf / PEAK_PF:.1f} % of the dense MFMA peak")
     if a.db:
-        agg, span = db_families(a.db, a.last_frac)
+        agg, span, units = db_families(a.db, a.last_frac, a.unit_marker, a.last_units)
         busy = sum(v[1] for v in agg.values())
-        per = a.db_units
+        per = units / a.marker_per_unit if units else a.db_units
         print(f"db: {span:.1f} ms window, {busy:.1f} ms kernel-busy ({100 * busy / max(span, 1e-9):.0f} %), "
               f"{per:g} units -> {span / per:.2f} ms wall / {busy / per:.2f} ms busy per unit")
         conv_ms = sum(v[1] for k, v in agg.items() if "conv" in k) / per
