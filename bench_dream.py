@@ -158,12 +158,16 @@ def virtual_rank(a) -> dict:
         # all-gather after the step (chunks 1) exposes all of it; with C chunks the last chunk's gather
         # is exposed and the others hide behind the next chunk's network (ms per step)
         comm = gather_bytes * (a.virtual_world - 1) / a.virtual_world / (a.xgmi_gbs * 1e9) * 1e3
-        C = max(1, min(D.TILE_CHUNKS, st.ucap))
-        exposed_c = comm / C + (C - 1) / C * max(0.0, comm - step_ms)
+        C = st.C
+        # chunks in waves of S concurrent streams: the last wave's gathers are exposed, earlier waves'
+        # hide behind the following waves' networks
+        S = max(1, min(D.TILE_CHUNK_STREAMS, C))
+        waves = -(-C // S)
+        exposed_c = comm / waves + (waves - 1) / waves * max(0.0, comm - step_ms)
         rows.append({"octave": list(hw), "tiles": st.ntiles, "units_this_rank": st.mine, "units_all": st.plan.shape[0],
                      "ms_per_step": round(step_ms, 3), "ms_octave": round(ms, 2),
                      "allgather_bytes_per_step": gather_bytes, "comm_ms_per_step_est": round(comm, 3),
-                     "exposed_ms_per_step_est": {"chunks_1": round(comm, 3), f"chunks_{C}": round(exposed_c, 3)}})
+                     "exposed_ms_per_step_est": {"chunks_1": round(comm, 3), f"chunks_{C}_streams_{S}": round(exposed_c, 3)}})
     out = {"virtual_world": a.virtual_world, "virtual_rank": a.virtual_rank, "model": a.model, "batch": a.batch,
            "size": a.size, "tile": a.tile, "dtype": a.dtype, "octaves": rows,
            "ms_per_dream_batch_compute": round(sum(r["ms_octave"] for r in rows), 1),

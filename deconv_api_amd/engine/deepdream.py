@@ -20,6 +20,7 @@ MI355X design:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -64,10 +65,18 @@ LOSS_PARTS = 32
 # octave_resize HIP launch per transition writing the next octave's static inputs directly
 OCTAVE_RESIZE = os.environ.get("DV_DREAM_OCTAVE_RESIZE", "1") != "0"
 # DV_TILE_CHUNKS: a rank's units per tiled step run as this many chunks when the step all-gathers
-# (several ranks): chunk c's pack all-gather (async, on the collective's own stream; captured into
-# the octave graph) overlaps chunk c+1's network, tile_update waits for all of them. 1: one
-# all-gather after the whole network (round-4 behaviour). Without a collective: always 1.
+# (several ranks): chunk c's pack all-gather is issued (async, captured into the octave graph) right
+# behind chunk c's network, tile_update waits for all of them. 1: one all-gather after the whole
+# network (round-4 behaviour).
 TILE_CHUNKS = max(1, int(os.environ.get("DV_TILE_CHUNKS", "2")))
+# DV_TILE_LOCAL_CHUNKS: the same without a collective (one rank).
+TILE_LOCAL_CHUNKS = max(1, int(os.environ.get("DV_TILE_LOCAL_CHUNKS", "2")))
+# DV_TILE_CHUNK_STREAMS: chunk c runs on stream c % S, forked from and joined back into the step's
+# stream around the networks (graph branches when captured). Chunks run back to back on ONE stream
+# cost +20 % (every launch's fill / drain exposed twice as often, ~105 launches per chunk-step); on
+# two streams they fill each other's gaps: config 5 28.1 -> 31.6 img/s, the 8-rank plan's per-rank
+# compute 189 -> 171 ms per batch (profiles/dream_c5_r5_local_chunks.txt).
+TILE_CHUNK_STREAMS = max(1, int(os.environ.get("DV_TILE_CHUNK_STREAMS", "2")))
 
 DEFAULT_LAYERS = {"mixed2": 0.2, "mixed3": 0.5, "mixed4": 2.0, "mixed5": 1.5}
 
@@ -575,7 +584,9 @@ class TiledDeepDream(DeepDream):
         st = type("TileState", (), {})()
         st.Th, st.Tw, st.ntiles, st.world, st.rank, st.ucap, st.mine = Th, Tw, ntiles, world, rank, ucap, mine
         probe = type("P", (), {"world": world})()
-        st.C = min(TILE_CHUNKS, ucap) if self._collective(probe) else 1
+        # virtual (bench_dream.py --virtual-world): chunked as the real rank's collective step would be
+        coll_like = self._collective(probe) or getattr(self, "virtual", False)
+        st.C = min(TILE_CHUNKS if coll_like else TILE_LOCAL_CHUNKS, ucap)
         st.ucc = -(-ucap // st.C)  # units per rank and chunk
         st.plan = plan.to(dev)
         st.x = torch.zeros(B, H, W, 3, device=dev)
@@ -647,12 +658,25 @@ class TiledDeepDream(DeepDream):
         and runs on the collective's stream while chunk c+1's network runs on this one; the update
         waits for every chunk's gather (captured as graph edges when ``capturing``)."""
         coll = self._collective(st)
+        ns = min(TILE_CHUNK_STREAMS, st.C)
+        if ns > 1 and len(getattr(self, "_cstreams", ())) < ns:
+            self._cstreams = [torch.cuda.Stream(self.device) for _ in range(ns)]
         for it in range(self.s.iterations):
             works = []
+            cur = torch.cuda.current_stream(self.device)
             for c, cs in enumerate(st.chunks):
-                self._tile_compute_chunk(st, cs, it, st.rank)
-                if coll:
-                    works.append(self._gather_chunk(st, c))
+                ctx = contextlib.nullcontext()
+                if ns > 1:  # fork: chunk c on stream c % ns (its all-gather issued behind it there)
+                    sm = self._cstreams[c % ns]
+                    sm.wait_stream(cur)
+                    ctx = torch.cuda.stream(sm)
+                with ctx:
+                    self._tile_compute_chunk(st, cs, it, st.rank)
+                    if coll:
+                        works.append(self._gather_chunk(st, c))
+            if ns > 1:  # join before the update
+                for sm in self._cstreams[:ns]:
+                    cur.wait_stream(sm)
             for w in works:
                 if capturing:
                     w.wait()  # recorded into the octave graph: nothing to poll here

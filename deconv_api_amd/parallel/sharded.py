@@ -484,10 +484,13 @@ class ShardedRunner:
         seq = ctl.post_cmd({"op": "gather", "b": b.bid})
         ctl.wait_acks("done", seq)
         ctl.go("go2", seq)
-        parts = [torch.empty_like(b.mos) for _ in range(self.world)]
         if self.comm_stream is not None:
             self.comm_stream.wait_event(b.ev)
             with torch.cuda.stream(self.comm_stream):
+                # the receive buffers come from comm_stream's pool: a compute-stream block may still
+                # be in use by the NEXT batch's queued engine work (two in flight), which the gather
+                # (ordered only behind THIS batch's event) would overwrite
+                parts = [torch.empty_like(b.mos) for _ in range(self.world)]
                 work = dist.gather(b.mos, gather_list=parts, dst=0, async_op=True)
                 self._await(work, "gather")
                 full = torch.cat(parts)
@@ -496,6 +499,7 @@ class ShardedRunner:
             torch.cuda.current_stream().wait_event(ev)
             full.record_stream(torch.cuda.current_stream())
         else:
+            parts = [torch.empty_like(b.mos) for _ in range(self.world)]
             self._await(dist.gather(b.mos, gather_list=parts, dst=0, async_op=True), "gather")
             full = torch.cat(parts)
         b.host = self._copy_back(b.staged, full, b.n)

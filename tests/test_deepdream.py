@@ -440,6 +440,29 @@ def test_gpu_tiled_fused_equals_torch(native_lib, max_loss):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("chunks,streams", [(2, 1), (3, 2)])
+def test_gpu_tiled_local_chunks_streams(native_lib, monkeypatch, chunks, streams):
+    """DV_TILE_LOCAL_CHUNKS / DV_TILE_CHUNK_STREAMS: one rank's units as several chunks, forked onto
+    side streams and joined before each step's update (inside the octave graph when captured) ==
+    the one-chunk step up to the conv rounding of smaller batches."""
+    import deconv_api_amd.engine.deepdream as D
+
+    net = ResNet50(0).build("cuda", torch.float16)
+    s = DreamSettings(layers=dict(RESNET_LAYERS), octaves=2, iterations=3, max_loss=None)
+    x = (torch.rand(3, 200, 260, 3, generator=torch.Generator().manual_seed(8)) * 2 - 1).cuda()
+    want = TiledDeepDream(net, s, tile=128, seed=3, use_graphs=False).run(x)
+    monkeypatch.setattr(D, "TILE_LOCAL_CHUNKS", chunks)
+    monkeypatch.setattr(D, "TILE_CHUNK_STREAMS", streams)
+    for graphs in (False, True):
+        dd = TiledDeepDream(net, s, tile=128, seed=3, use_graphs=graphs)
+        got = dd.run(x)
+        torch.cuda.synchronize()
+        assert all(st.C == chunks for st in dd._tgraphs.values())
+        assert torch.isfinite(got).all() and _cos(got - x, want - x) > 0.99, graphs
+        assert torch.isfinite(dd.run(x)).all()
+
+
+@pytest.mark.gpu
 def test_gpu_tiled_whole_octave_graph_1024(native_lib):
     """Regression for the round-1 illegal-address fault: one hipGraph holding every step of a tiled
     octave at 1024^2 (tile 512, fp16) replays, twice, and matches the eager fused steps."""
@@ -610,8 +633,8 @@ def test_gpu_tiled_collective_octave_captured(native_lib):
     assert out["backend"] == "nccl" and out["collective"] is True, out
     assert out["octave_graph"] is True and out["step_graphs"] is False, out
     assert out["equal"] is True, out
-    # chunked overlap (2 chunks: chunk 0's all-gather captured beside chunk 1's network)
-    assert out["chunks"] == 2 and out["chunked_octave_graph"] is True, out
+    # chunked (2 chunks on 2 streams, each chunk's all-gather issued from its stream; captured)
+    assert out["chunks"] == 2 and out["chunk_streams"] == 2 and out["chunked_octave_graph"] is True, out
     assert out["chunked_cos"] > 0.995 and out["chunked_maxdiff"] < 5e-2, out
 
 

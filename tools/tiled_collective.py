@@ -8,7 +8,9 @@ all-gather of the packs over the process group) and captured inside the octave's
 same octave without collectives; prints one JSON line: backend, whether the collective path ran,
 whether the octave was ONE graph (collectives captured) or per-step graphs, and bit equality. Then the
 chunked overlapped step (DV_TILE_CHUNKS semantics: each chunk's async all-gather captured beside the
-next chunk's network): equal to the collective-free octave up to the conv rounding of smaller batches."""
+next chunk's network; with DV_TILE_CHUNK_STREAMS=2 (default) the chunks run on two streams and each
+all-gather is issued from its chunk's stream): equal to the collective-free octave up to the conv
+rounding of smaller batches."""
 import json
 import os
 import sys
@@ -29,6 +31,7 @@ def main():
     s = D.DreamSettings(layers=dict(D.RESNET_LAYERS), octaves=1, iterations=4, max_loss=None)
     x = (torch.rand(2, 256, 320, 3, generator=torch.Generator().manual_seed(3)) * 2 - 1).to(info.device)
     D.TILE_COLLECTIVE = False
+    D.TILE_LOCAL_CHUNKS = 1  # the unchunked 1-rank octave is the reference
     ref = D.TiledDeepDream(net, s, tile=128, info=info, seed=5).gradient_ascent(x)
     D.TILE_COLLECTIVE = True
     D.TILE_CHUNKS = 1
@@ -47,7 +50,7 @@ def main():
     torch.cuda.synchronize()
     stc = next(iter(dc._tgraphs.values()))
     a, b = (gc - x).flatten().double(), (ref - x).flatten().double()
-    out.update({"chunks": stc.C, "chunked_octave_graph": stc.graph is not None,
+    out.update({"chunks": stc.C, "chunk_streams": min(D.TILE_CHUNK_STREAMS, stc.C), "chunked_octave_graph": stc.graph is not None,
                 "chunked_cos": float(a @ b / (a.norm() * b.norm() + 1e-30)),
                 "chunked_maxdiff": float((gc - ref).abs().max()), "chunked_rerun_finite": bool(torch.isfinite(gc2).all())})
     if info.is_main:
