@@ -228,7 +228,13 @@ constexpr int V2_C = TH * TW * 128;                      // 32768: bf16 output t
 // Z = D W2^T [N, H, W, 32] bf16 (64 B/px); zsum3x3_kernel finishes the conv as a 9-tap shift-add.
 // Wave w owns tile row w for this GEMM (32 px x 32 Z channels, K = 64: 8 MFMAs); the B operand is the
 // staged output tile read straight from Cst.
-template <bool ZOUT>
+//
+// V (bit mask): 1 = transposed MFMA (D^T = W A^T: a lane holds 4 consecutive channels of one pixel), so
+// the output tile is staged with one ds_write_b64 per fragment instead of four ds_write_b16; 2 = the
+// next tile's halo expansion is issued inside this tile's MFMA loop (the other halo buffer was last
+// read by the previous tile's MFMAs, which every wave finished before this tile's first barrier)
+// instead of between the two barriers with the MFMA pipes idle.
+template <bool ZOUT, int V = 0>
 __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const ConvArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * V2_A + V2_C + (ZOUT ? 32 * 128 : 0)];
   uint8_t* Cst = smem + 2 * V2_A;
@@ -250,12 +256,15 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
       const int k = (s >> 1) * C64 + (s & 1) * 32 + kq * 8;
       bw[s][j] = *reinterpret_cast<const bf16x8*>(a.w + (long long)oc * a.Kpad + k);
     }
-  float biasv[2];
+  constexpr bool TR = (V & 1) != 0, ILV = (V & 2) != 0;
+  float biasv[2][TR ? 4 : 1];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int oc = wc * 32 + j * 16 + col;
-    biasv[j] = (a.bias && oc < a.OC) ? a.bias[oc] : 0.f;
-  }
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < (TR ? 4 : 1); ++r) {
+      const int oc = wc * 32 + j * 16 + (TR ? kq * 4 + r : col);
+      biasv[j][r] = (a.bias && oc < a.OC) ? a.bias[oc] : 0.f;
+    }
   // ZOUT: W2 [32][64] bf16 staged once in LDS (4 KiB, 16-B chunks XOR-swizzled by row; in VGPRs it
   // would spill next to the 144 weight registers); A fragment = row 16 jz + col, K chunk 32 ks + 8 kq
   if constexpr (ZOUT) {
@@ -356,25 +365,50 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
       for (int i = 0; i < 4; ++i) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ab[i] + off);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[s][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[s][j], af, acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[s][j], acc[i][j], 0, 0, 0);
+      }
+      if constexpr (ILV) {
+        if (s == 12 && t < ntiles) store_tile(smem + (cur ^ 1) * V2_A, t);  // behind the remaining MFMAs
       }
     }
     __syncthreads();  // every wave is done with the previous tile's Cst reads and this halo
     // ---- output tile -> Cst (bias, ReLU); C row = pixel, C col = channel ----
+    if constexpr (TR) {  // lane (col, kq): pixel col of fragment i, channels j*16 + kq*4 .. + 3
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ch = wc * 32 + j * 16 + col;
+        for (int j = 0; j < 2; ++j) {
+          const int ch = wc * 32 + j * 16 + kq * 4;
+          const int pix = (2 * wr + (i >> 1)) * TW + (i & 1) * 16 + col;
+          float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int pix = (2 * wr + (i >> 1)) * TW + (i & 1) * 16 + kq * 4 + r;
-          float v = acc[i][j][r] + biasv[j];
-          if (a.relu) v = fmaxf(v, 0.f);
-          *reinterpret_cast<uint16_t*>(Cst + pix * 128 + ((((ch >> 3) ^ (pix & 7))) << 4) + (ch & 7) * 2) = f2bf(v);
+          for (int r = 0; r < 4; ++r) {
+            v[r] = acc[i][j][r] + biasv[j][r];
+            if (a.relu) v[r] = fmaxf(v[r], 0.f);
+          }
+          *reinterpret_cast<uint2*>(Cst + pix * 128 + ((((ch >> 3) ^ (pix & 7))) << 4) + (ch & 7) * 2) =
+              make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
         }
-      }
-    if (t < ntiles) store_tile(smem + (cur ^ 1) * V2_A, t);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int ch = wc * 32 + j * 16 + col;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int pix = (2 * wr + (i >> 1)) * TW + (i & 1) * 16 + kq * 4 + r;
+            float v = acc[i][j][r] + biasv[j][0];
+            if (a.relu) v = fmaxf(v, 0.f);
+            *reinterpret_cast<uint16_t*>(Cst + pix * 128 + ((((ch >> 3) ^ (pix & 7))) << 4) + (ch & 7) * 2) = f2bf(v);
+          }
+        }
+    }
+    if constexpr (!ILV) {
+      if (t < ntiles) store_tile(smem + (cur ^ 1) * V2_A, t);
+    }
     __syncthreads();
     if constexpr (ZOUT) {  // ---- Z = D W2^T for tile row `wave`, 8-B stores (4 Z channels of one px) ----
       int b = tcur;
@@ -1129,7 +1163,14 @@ int conv3x3_unpool_z_launch(const ConvArgs& a, hipStream_t s) {
   }();
   const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   if (ntiles <= 0 || ntiles > 0x7fffffffLL) return -2;
-  hipLaunchKernelGGL(conv3x3_unpool_c64_v2_kernel<true>, dim3((unsigned)std::min<long long>(ntiles, cus)), dim3(512), 0, s, a);
+  // DV_TAIL_V: variant bits (see the kernel); 3 by default, 0 = the round-4 schedule (A/B)
+  const char* tve = std::getenv("DV_TAIL_V");  // per launch: tests switch it in one process
+  const int tv = tve ? (std::atoi(tve) & 3) : 3;
+  const dim3 g((unsigned)std::min<long long>(ntiles, cus));
+  if (tv == 0) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 0>), g, dim3(512), 0, s, a);
+  else if (tv == 1) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 1>), g, dim3(512), 0, s, a);
+  else if (tv == 2) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 2>), g, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 3>), g, dim3(512), 0, s, a);
   return (int)hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ filter sums) on top of the same machinery.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -31,6 +32,11 @@ from ..models.vgg16 import VGG16Runtime, LayerSpec
 from ..utils import tracing
 
 VALID_MODES = ("all", "max")
+# DV_DECONV_STREAMS=S: a GPU batch of >= DV_DECONV_SPLIT_MIN images runs as S sub-batches on S streams
+# forked from and joined back into the caller's stream (graph branches when captured); per-image top-k
+# makes the halves independent
+DECONV_STREAMS = max(1, int(os.environ.get("DV_DECONV_STREAMS", "1")))
+DECONV_SPLIT_MIN = int(os.environ.get("DV_DECONV_SPLIT_MIN", "64"))
 
 
 class UnknownLayerError(KeyError):
@@ -256,6 +262,35 @@ class DeconvNet:
             batch_topk: str = "per_image", mosaic: bool = True, hook=None) -> DeconvResult:
         if mode not in VALID_MODES:
             raise ValueError(f"Illegal visualize mode {mode!r}; use 'all' or 'max'")
+        S = DECONV_STREAMS
+        if S > 1 and x.is_cuda and batch_topk == "per_image" and x.shape[0] >= max(DECONV_SPLIT_MIN, S):
+            return self._run_split(x, layer, k, mode, mosaic, hook, S)
+        return self._run1(x, layer, k, mode, batch_topk, mosaic, hook)
+
+    def _run_split(self, x, layer, k, mode, mosaic, hook, S) -> DeconvResult:
+        dev = x.device
+        if len(getattr(self, "_streams", ())) < S:
+            self._streams = [torch.cuda.Stream(dev) for _ in range(S)]
+        cur = torch.cuda.current_stream(dev)
+        parts = []
+        for i, xp in enumerate(x.chunk(S)):
+            sm = self._streams[i]
+            sm.wait_stream(cur)
+            with torch.cuda.stream(sm):
+                parts.append(self._run1(xp, layer, k, mode, "per_image", mosaic, hook if i == 0 else None))
+        for sm in self._streams[:S]:
+            cur.wait_stream(sm)
+        for r in parts:  # read on the caller's stream from here on
+            for t in (r.recon, r.filters, r.sums, r.mosaic):
+                if t is not None:
+                    t.record_stream(cur)
+        res = DeconvResult(torch.cat([r.recon for r in parts]), torch.cat([r.filters for r in parts]),
+                           torch.cat([r.sums for r in parts]))
+        if parts[0].mosaic is not None:
+            res.mosaic = torch.cat([r.mosaic for r in parts])
+        return res
+
+    def _run1(self, x, layer, k, mode, batch_topk, mosaic, hook) -> DeconvResult:
         with tracing.range_("dv.forward"):
             st = self.forward(x, layer, hook=hook)
         with tracing.range_("dv.select"):

@@ -20,7 +20,6 @@ MI355X design:
 """
 from __future__ import annotations
 
-import contextlib
 import os
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -664,19 +663,28 @@ class TiledDeepDream(DeepDream):
         for it in range(self.s.iterations):
             works = []
             cur = torch.cuda.current_stream(self.device)
-            for c, cs in enumerate(st.chunks):
-                ctx = contextlib.nullcontext()
-                if ns > 1:  # fork: chunk c on stream c % ns (its all-gather issued behind it there)
-                    sm = self._cstreams[c % ns]
-                    sm.wait_stream(cur)
-                    ctx = torch.cuda.stream(sm)
-                with ctx:
+            if ns == 1:
+                for c, cs in enumerate(st.chunks):
                     self._tile_compute_chunk(st, cs, it, st.rank)
                     if coll:
                         works.append(self._gather_chunk(st, c))
-            if ns > 1:  # join before the update
-                for sm in self._cstreams[:ns]:
-                    cur.wait_stream(sm)
+            else:
+                # fork: chunk c on stream c % ns. Its all-gather is issued from THIS stream behind an event
+                # of the chunk (a collective issued from a forked capture stream is not seen as captured
+                # by the process group, whose watchdog then queries a captured event and aborts)
+                done = []
+                for c, cs in enumerate(st.chunks):
+                    sm = self._cstreams[c % ns]
+                    sm.wait_stream(cur)
+                    with torch.cuda.stream(sm):
+                        self._tile_compute_chunk(st, cs, it, st.rank)
+                    ev = torch.cuda.Event()
+                    ev.record(sm)
+                    done.append(ev)
+                for c, ev in enumerate(done):
+                    cur.wait_event(ev)
+                    if coll:
+                        works.append(self._gather_chunk(st, c))
             for w in works:
                 if capturing:
                     w.wait()  # recorded into the octave graph: nothing to poll here

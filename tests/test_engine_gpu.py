@@ -90,6 +90,30 @@ def test_graphed_engine_equals_eager(native_lib):
         assert (gm.float() - un.mosaic.float()).abs().mean() < 0.5
 
 
+def test_split_streams_equals_one_stream(native_lib, monkeypatch):
+    """DV_DECONV_STREAMS: a batch split into sub-batches on forked streams (eager and captured) gives
+    the unsplit batch's filters; mosaics up to rounding (smaller M changes split-K / tile choices of
+    small-M layers, which can flip near-tied switches: compared on the mean as above)."""
+    import deconv_api_amd.engine.deconvnet as dn
+    from deconv_api_amd.engine.graphs import GraphedDeconv
+
+    m = VGG16.random(0, include_top=False)
+    eng = DeconvNet(m.build("cuda", torch.bfloat16))
+    x = _x8(8, 224, 6).to(torch.bfloat16).cuda()
+    one = eng.run(x, "block5_conv3", k=4)
+    monkeypatch.setattr(dn, "DECONV_STREAMS", 2)
+    monkeypatch.setattr(dn, "DECONV_SPLIT_MIN", 5)  # the 8-image batch splits, its 4-image halves do not
+    two = eng.run(x, "block5_conv3", k=4)
+    assert two.recon.shape == one.recon.shape and two.mosaic.shape == one.mosaic.shape
+    assert torch.equal(two.filters, one.filters)
+    assert (two.mosaic.float() - one.mosaic.float()).abs().mean() < 0.5
+    # each half alone gives exactly its half of the split batch
+    half = eng.run(x[:4], "block5_conv3", k=4)
+    assert torch.equal(half.mosaic, two.mosaic[:4])
+    g = GraphedDeconv(eng).run(x, "block5_conv3")  # fork / join captured as graph branches
+    assert torch.equal(g.mosaic, two.mosaic) and torch.equal(g.filters, two.filters)
+
+
 def test_service_end_to_end_gpu(native_lib):
     """The HTTP path on the GPU: decode -> GPU resize -> graphed engine -> D2H -> JPEG."""
     import asyncio

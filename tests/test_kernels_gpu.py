@@ -1063,6 +1063,15 @@ def test_deconv_tail_fused(native_lib, N, H, W, div):
     a, b = got.flatten().double().cpu(), two.flatten().double().cpu()
     assert float(a @ b / (a.norm() * b.norm())) > 0.9999
     assert _rel(got, two) < 2e-2
+    # the tail kernel's schedules (DV_TAIL_V bits: transposed MFMA / expansion inside the MFMA loop)
+    # compute the same dot products in the same K order: bit-identical to the round-4 schedule
+    for v in ("0", "1", "2"):
+        os.environ["DV_TAIL_V"] = v
+        try:
+            alt = ops.deconv_tail(pd, cd, div, midd, lastd)
+        finally:
+            del os.environ["DV_TAIL_V"]
+        assert torch.equal(alt, got), v
 
 
 @pytest.mark.parametrize("N,H,W", [(3, 64, 64), (2, 60, 70)])
