@@ -116,11 +116,14 @@ int64_t device_cus() {
 
 // geom: N,H,W,C, OH,OW,OC,OCpad, KH,KW,stride,pad_h,pad_w, K,Kpad, M, relu,relu_in,accumulate,
 //       code_div, x_ld, mask_ld, out_ld
-void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
-          c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
-          int64_t epi, int64_t impl, c10::optional<Tensor> res, c10::optional<Tensor> emask,
-          c10::optional<Tensor> stats, int64_t stats_div, c10::optional<Tensor> ucode, int64_t ucode_div,
-          int64_t relu_cols, c10::optional<Tensor> out2, int64_t split_col) {
+// Returns bit flags: 1 = obits written, 2 = ebits used (both only on the persistent 1x1 kernel; otherwise
+// the caller's emask applies and obits stays unwritten).
+int64_t conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optional<Tensor> out_code,
+             c10::optional<Tensor> code, c10::optional<Tensor> mask, std::vector<int64_t> g, int64_t amode,
+             int64_t epi, int64_t impl, c10::optional<Tensor> res, c10::optional<Tensor> emask,
+             c10::optional<Tensor> stats, int64_t stats_div, c10::optional<Tensor> ucode, int64_t ucode_div,
+             int64_t relu_cols, c10::optional<Tensor> out2, int64_t split_col, c10::optional<Tensor> obits,
+             c10::optional<Tensor> ebits) {
   TORCH_CHECK(g.size() == 23, "conv: geometry vector must have 23 entries");
   check_cuda(x, "x");
   check_cuda(w, "w");
@@ -301,6 +304,28 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
                                       (long long)a.stats_div * a.OH * a.OW * a.OC, a.N / a.stats_div, cur_stream()),
                "recon_stats");
   };
+  // 1-bit ReLU masks ([M, OC / 8] bytes, csrc/kernels.h): set on a COPY of the args handed to a kernel whose
+  // epilogue honours them (the persistent 1x1 kernel, the halo-stream LDS-staged epilogues); returns the
+  // flags to report if that kernel runs with them (every other path ignores obits / ebits: emask applies)
+  auto with_bits = [&](dv::ConvArgs& ap) -> int64_t {
+    int64_t f = 0;
+    auto ok = [&](const Tensor& b) {
+      check_cuda(b, "bits");
+      return b.scalar_type() == at::kByte && b.is_contiguous() && a.OC % 8 == 0 && a.ucode == nullptr &&
+             a.out2 == nullptr && a.out_ld == a.OC && b.numel() >= (int64_t)a.M * (a.OC / 8);
+    };
+    if (obits.has_value() && ok(*obits)) {
+      ap.obits = obits->data_ptr<uint8_t>();
+      ap.obits_ld = a.OC / 8;
+      f |= 1;
+    }
+    if (ebits.has_value() && a.emask != nullptr && ok(*ebits)) {
+      ap.ebits = ebits->data_ptr<uint8_t>();
+      ap.ebits_ld = a.OC / 8;
+      f |= 2;
+    }
+    return f;
+  };
   // Kernel choice. impl: 0 auto, 1 register-staged (conv_igemm), 2 LDS-DMA (conv_dma), 3 halo-tile.
   //  * halo-tile (3x3 s1 p1, OC tile <= 64, >= 56x56 maps): input staged once per tile, unpool fused
   //  * LDS-DMA: FWD / TRANSPOSE (optionally ReLU-masked); an unpool input is first materialized
@@ -326,7 +351,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     if (rc >= 0) {
       check_rc(rc, "conv_pool_v3");
       finish_stats();
-      return;
+      return 0;
     }
   }
   // first layer (8-channel padded RGB image -> 64 channels): row-streaming, output-write bound
@@ -337,7 +362,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     if (rc >= 0) {
       check_rc(rc, "conv_c8_stream");
       finish_stats();
-      return;
+      return 0;
     }
   }
   // unpool -> conv (64/128 out, full-res sides % 16): hs16 with the pooled halo expanded in LDS
@@ -346,7 +371,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     if (rc >= 0) {
       check_rc(rc, "conv_halo_stream_unpool");
       finish_stats();
-      return;
+      return 0;
     }
   }
   if (impl == 3 || (impl == 0 && halo_auto)) {
@@ -354,7 +379,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     check_rc(dv::conv3x3_halo_launch(a, amode == dv::CONV_A_UNPOOL ? 1 : 0, (int)epi, cur_stream(), &stats_done),
              "conv_halo");
     finish_stats();
-    return;
+    return 0;
   }
   // ReLU-masked A (dgrad): the DMA kernel stages the mask with x's offsets, so it needs mask_ld == x_ld
   const bool mask_dma = mask.has_value() && a.mask_ld == a.x_ld && epi == dv::CONV_E_BF16 &&
@@ -408,11 +433,14 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
         !mask.has_value() && !a.res && !a.ucode && !a.accumulate && a.relu_cols <= 0 &&
         (int64_t)a.H * a.W >= hs_min_w * hs_min_w && a.W >= hs_min_w && (!a.emask || !hs_emask_off) &&
         (a.pad_h == 1 || !hs_pad_off)) {
-      const int rc = dv::conv3x3_hs_launch(a, (int)epi, cur_stream());
+      dv::ConvArgs ap = a;
+      const int64_t want = with_bits(ap);
+      bool lepi = false;
+      const int rc = dv::conv3x3_hs_launch(ap, (int)epi, cur_stream(), &lepi);
       if (rc >= 0) {
         check_rc(rc, "conv_halo_stream");
         finish_stats();
-        return;
+        return lepi ? want : 0;
       }
     }
     // the DMA kernel addresses A with 32-bit offsets relative to the tile's first image
@@ -423,7 +451,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       const int cfg = dv::conv_dma_group_cfg(a, (int)amode, (int)epi);
       if (cfg != 0) {  // recorded (no split-K: the group runs its problems side by side); launched by conv_group_end
         g_group.push_back(PendingConv{a, (int)amode, (int)epi, cfg});
-        return;
+        return 0;
       }
     }
     // split-K when the tile grid would leave most CUs idle (plain epilogues only)
@@ -437,11 +465,13 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
       a.ksplit = ks;
     }
     if (ks == 1 && (impl == 0 || impl == 2) && amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16 && !mask.has_value()) {
-      const int rc = dv::conv_pw_launch(a, cur_stream());  // large-M 1x1 convs: persistent pipeline
+      dv::ConvArgs ap = a;
+      const int64_t flags = with_bits(ap);
+      const int rc = dv::conv_pw_launch(ap, cur_stream());  // large-M 1x1 convs: persistent pipeline
       if (rc >= 0) {
         check_rc(rc, "conv_pw");
         finish_stats();
-        return;
+        return flags;
       }
     }
     // KW3P stream-K workspace (conv_dma_impl.h:kw3_sk_ok decides whether it is used): one fp32 partial-tile
@@ -463,6 +493,7 @@ void conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::optio
     check_rc(dv::conv_igemm_launch(a, (int)amode, (int)epi, cur_stream()), "conv_igemm");
   }
   finish_stats();
+  return 0;
 }
 
 // kind 0 max / 1 avg; dir 0 fwd (in=x, out=y) / 1 bwd (in=gy, out=gx); geom = N,H,W,C,OH,OW,k,s,pad.
@@ -1234,7 +1265,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mask"), py::arg("geom"), py::arg("amode"), py::arg("epi"), py::arg("impl"),
         py::arg("res") = py::none(), py::arg("emask") = py::none(), py::arg("stats") = py::none(),
         py::arg("stats_div") = 1, py::arg("ucode") = py::none(), py::arg("ucode_div") = 1,
-        py::arg("relu_cols") = 0, py::arg("out2") = py::none(), py::arg("split_col") = 0);
+        py::arg("relu_cols") = 0, py::arg("out2") = py::none(), py::arg("split_col") = 0,
+        py::arg("obits") = py::none(), py::arg("ebits") = py::none());
   m.def("conv_group_begin", &conv_group_begin, "start recording groupable small-problem convs (this thread)");
   m.def("conv_group_pause", [](bool p) { g_group_paused = p; }, "suspend / resume recording (dependent convs)");
   m.def("conv_group_end", &conv_group_end, "launch the recorded convs as grouped kernels; returns the launch count");

@@ -133,6 +133,23 @@ __device__ __forceinline__ uint32_t mask_pos_pk(uint32_t a, uint32_t m) {
   return a & __umul24(pos >> 15, 0xFFFFu);
 }
 __device__ __forceinline__ uint32_t mask_pos_bf2(uint32_t v, uint32_t m) { return mask_pos_pk(v, m); }
+// 1-bit ReLU masks: bit e of the byte = element e of an 8-element chunk is > 0 (the mask_pos_pk predicate
+// on the stored 16-bit value, so masking by the bits equals masking by the values)
+__device__ __forceinline__ uint32_t pos_bits2(uint32_t v) {
+  const uint32_t pos = (((v & 0x7FFF7FFFu) + 0x7FFF7FFFu) & ~v) & 0x80008000u;
+  return ((pos >> 15) & 1u) | (pos >> 30);
+}
+__device__ __forceinline__ uint32_t pos_bits8(uint4 v) {
+  return pos_bits2(v.x) | (pos_bits2(v.y) << 2) | (pos_bits2(v.z) << 4) | (pos_bits2(v.w) << 6);
+}
+// keep the two 16-bit elements of a whose bits (two: bit 0 low, bit 1 high) are set
+__device__ __forceinline__ uint32_t mask_bits_pk(uint32_t a, uint32_t two) {
+  return a & (__umul24(two & 1u, 0xFFFFu) | (__umul24(two >> 1, 0xFFFFu) << 16));
+}
+__device__ __forceinline__ uint4 mask_bits8(uint4 v, uint32_t b) {
+  return make_uint4(mask_bits_pk(v.x, b & 3u), mask_bits_pk(v.y, (b >> 2) & 3u), mask_bits_pk(v.z, (b >> 4) & 3u),
+                    mask_bits_pk(v.w, b >> 6));
+}
 
 // Bijective XCD-aware workgroup remap (MI355X: 8 XCDs, consecutive dispatch ids go to
 // different XCDs). After the remap logically-adjacent tiles share an XCD (and its L2).

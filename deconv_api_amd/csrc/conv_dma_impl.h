@@ -775,11 +775,13 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
   // epilogue-latency bound. DV_NO_EPI_BATCH=1 (host) falls back to the per-chunk loop (A/B).
   constexpr int ITER = (BM * CPR + NT - 1) / NT;
   if constexpr (ITER <= 8) {
-    if (a.epi_batch && a.ucode == nullptr && (post || a.emask != nullptr)) {
+    if (a.epi_batch && a.ucode == nullptr && (post || a.emask != nullptr || a.ebits != nullptr || a.obits != nullptr)) {
       uint4 rv[ITER], av[ITER], mv[ITER];
+      uint32_t eb[ITER];
 #pragma unroll
       for (int it = 0; it < ITER; ++it) {
         rv[it] = av[it] = mv[it] = uint4{0u, 0u, 0u, 0u};
+        eb[it] = 0u;
         const int c = tid + it * NT;
         const int row = c / CPR, cc = c % CPR;
         const int grow = m0 + row, gcol = n0 + cc * 8;
@@ -789,8 +791,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
           av[it] = *reinterpret_cast<const uint4*>(out + o);
         if (a.res && DV_BOUNDS((long long)grow * a.res_ld + gcol, 8, a.res_elems, "conv_dma epilogue_lds res load"))
           rv[it] = *reinterpret_cast<const uint4*>(a.res + (long long)grow * a.res_ld + gcol);
-        if (a.emask &&
-            DV_BOUNDS((long long)grow * a.emask_ld + gcol, 8, a.emask_elems, "conv_dma epilogue_lds emask load"))
+        if (a.ebits)
+          eb[it] = a.ebits[(long long)grow * a.ebits_ld + (gcol >> 3)];
+        else if (a.emask &&
+                 DV_BOUNDS((long long)grow * a.emask_ld + gcol, 8, a.emask_elems, "conv_dma epilogue_lds emask load"))
           mv[it] = *reinterpret_cast<const uint4*>(a.emask + (long long)grow * a.emask_ld + gcol);
       }
 #pragma unroll
@@ -807,13 +811,16 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
         }
         if (!DV_BOUNDS(o, 8, a.out_elems, "conv_dma epilogue_lds out")) continue;
         if (post) v = epi_combine<DT>(a, v, av[it], rv[it]);
-        if (a.emask) {
+        if (a.ebits) {
+          v = mask_bits8(v, eb[it]);
+        } else if (a.emask) {
           v.x = mask_pos_pk(v.x, mv[it].x);
           v.y = mask_pos_pk(v.y, mv[it].y);
           v.z = mask_pos_pk(v.z, mv[it].z);
           v.w = mask_pos_pk(v.w, mv[it].w);
         }
         *reinterpret_cast<uint4*>(out + o) = v;
+        if (a.obits) a.obits[(long long)grow * a.obits_ld + (gcol >> 3)] = (uint8_t)pos_bits8(v);
       }
       return;
     }
@@ -872,13 +879,16 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&ac
       }
       v = uint4{ov[0], ov[1], ov[2], ov[3]};
     }
-    if (a.emask) {
+    if (a.ebits) {
+      v = mask_bits8(v, a.ebits[(long long)grow * a.ebits_ld + (gcol >> 3)]);
+    } else if (a.emask) {
       const uint4 em = *reinterpret_cast<const uint4*>(a.emask + (long long)grow * a.emask_ld + gcol);
       v.x = mask_pos_pk(v.x, em.x);
       v.y = mask_pos_pk(v.y, em.y);
       v.z = mask_pos_pk(v.z, em.z);
       v.w = mask_pos_pk(v.w, em.w);
     }
+    if (a.obits) a.obits[(long long)grow * a.obits_ld + (gcol >> 3)] = (uint8_t)pos_bits8(v);
     if (a.ucode) {  // max-unpool: the value goes to the window position its switch code names, 0 elsewhere
       const int hw = a.OH * a.OW;
       const int n = grow / hw, rem = grow - n * hw;

@@ -252,23 +252,29 @@ __global__ void __launch_bounds__(512, NB1 && OCT == 64 ? 4 : 1) conv3x3_hs_kern
         const int lp = t * PPI + lane / CPR, lc = pc ^ (lp & (CPR - 1)), x = tx0 + lp;
         const long long pix = ((long long)n * a.OH + oy) * a.OW + x;
         em[t] = make_uint4(0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u);  // any > 0
-        if (a.emask && oy < a.OH && x < a.OW && lc * 8 < a.OC &&
-            DV_BOUNDS(pix * a.emask_ld + lc * 8, 8, a.emask_elems, "halo-stream emask"))
+        if (a.ebits && oy < a.OH && x < a.OW && lc * 8 < a.OC)  // 1-bit mask: one byte per chunk
+          em[t].x = a.ebits[pix * a.ebits_ld + lc];
+        else if (a.emask && oy < a.OH && x < a.OW && lc * 8 < a.OC &&
+                 DV_BOUNDS(pix * a.emask_ld + lc * 8, 8, a.emask_elems, "halo-stream emask"))
           em[t] = *reinterpret_cast<const uint4*>(a.emask + pix * a.emask_ld + lc * 8);
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int lp = t * PPI + lane / CPR, lc = pc ^ (lp & (CPR - 1)), x = tx0 + lp;
         uint4 v = *reinterpret_cast<const uint4*>(wreg + lp * ROWB + pc * 16);
-        if (a.emask) {
+        if (a.ebits) {
+          v = mask_bits8(v, em[t].x);
+        } else if (a.emask) {
           v.x = mask_pos_pk(v.x, em[t].x);
           v.y = mask_pos_pk(v.y, em[t].y);
           v.z = mask_pos_pk(v.z, em[t].z);
           v.w = mask_pos_pk(v.w, em[t].w);
         }
         const long long pix = ((long long)n * a.OH + oy) * a.OW + x;
-        if (oy < a.OH && x < a.OW && lc * 8 < a.OC && DV_BOUNDS(pix * a.out_ld + lc * 8, 8, a.out_elems, "halo-stream out"))
+        if (oy < a.OH && x < a.OW && lc * 8 < a.OC && DV_BOUNDS(pix * a.out_ld + lc * 8, 8, a.out_elems, "halo-stream out")) {
           *reinterpret_cast<uint4*>(out + pix * a.out_ld + lc * 8) = v;
+          if (a.obits) a.obits[pix * a.obits_ld + lc] = (uint8_t)pos_bits8(v);
+        }
       }
     }
     return;
@@ -712,7 +718,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
       const int lc = pc ^ (lp & (CPR - 1));
       const long long pix = ((long long)n * a.OH + ty0 + 4 * wave + (lp >> 4)) * a.OW + tx0 + (lp & 15);
       em[t] = make_uint4(0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u);  // any > 0
-      if (a.emask && lc * 8 < a.OC && DV_BOUNDS(pix * a.emask_ld + lc * 8, 8, a.emask_elems, "hs16 emask"))
+      if (a.ebits && lc * 8 < a.OC)  // 1-bit mask: one byte per chunk
+        em[t].x = a.ebits[pix * a.ebits_ld + lc];
+      else if (a.emask && lc * 8 < a.OC && DV_BOUNDS(pix * a.emask_ld + lc * 8, 8, a.emask_elems, "hs16 emask"))
         em[t] = *reinterpret_cast<const uint4*>(a.emask + pix * a.emask_ld + lc * 8);
     }
 #pragma unroll
@@ -721,14 +729,18 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
       const int lc = pc ^ (lp & (CPR - 1));
       const long long pix = ((long long)n * a.OH + ty0 + 4 * wave + (lp >> 4)) * a.OW + tx0 + (lp & 15);
       uint4 v = *reinterpret_cast<const uint4*>(wreg + lp * ROWB + pc * 16);
-      if (a.emask) {
+      if (a.ebits) {
+        v = mask_bits8(v, em[t].x);
+      } else if (a.emask) {
         v.x = mask_pos_pk(v.x, em[t].x);
         v.y = mask_pos_pk(v.y, em[t].y);
         v.z = mask_pos_pk(v.z, em[t].z);
         v.w = mask_pos_pk(v.w, em[t].w);
       }
-      if (lc * 8 < a.OC && DV_BOUNDS(pix * a.out_ld + lc * 8, 8, a.out_elems, "hs16 out"))
+      if (lc * 8 < a.OC && DV_BOUNDS(pix * a.out_ld + lc * 8, 8, a.out_elems, "hs16 out")) {
         *reinterpret_cast<uint4*>(out + pix * a.out_ld + lc * 8) = v;
+        if (a.obits) a.obits[pix * a.obits_ld + lc] = (uint8_t)pos_bits8(v);
+      }
     }
     return;
   }
@@ -779,7 +791,8 @@ static int hs_ring() {
       hipLaunchKernelGGL((conv3x3_hs_kernel<DT_, OCT_, POOL_, 3>), grid, block, 0, s, a, tx, ty);      \
   } while (0)
 
-int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
+int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used) {
+  if (lepi_used) *lepi_used = false;  // set when the LDS-staged epilogue (the only one with 1-bit masks) runs
   if (std::getenv("DV_NO_HS") != nullptr) return -4;
   // 192 / 256 padded output channels (InceptionV3 conv2d_5: 96 -> 192): two launches over the
   // channel halves [0, 128) and [128, OCpad), each re-reading the (small) input halo
@@ -797,6 +810,8 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
       a2.emask = a.emask + 128;
       a2.emask_elems = a.emask_elems - 128;
     }
+    a1.obits = a2.obits = nullptr;  // no 1-bit masks on the channel-split form
+    a1.ebits = a2.ebits = nullptr;
     if (a2.OC % 4 != 0) return -4;
     // both halves must be supported before either launches
     const int r1 = conv3x3_hs_launch(a1, epi, s);
@@ -832,6 +847,7 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
     const bool lepi = !pool && !(he && std::strcmp(he, "reg") == 0) && a.OC % 8 == 0 && a.out_ld % 8 == 0 &&
                       !(reinterpret_cast<uintptr_t>(a.out) & 15) &&
                       (!a.emask || (a.emask_ld % 8 == 0 && !(reinterpret_cast<uintptr_t>(a.emask) & 15)));
+    if (lepi_used) *lepi_used = lepi;
     if (pool) {
       if (a.OCpad == 128) HS16(DT_BF16, 128, true, false);
       else HS16(DT_BF16, 64, true, false);
@@ -865,6 +881,7 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s) {
   const bool lepi = !pool && ring == 3 && !(he && std::strcmp(he, "reg") == 0) && a.OC % 8 == 0 && a.out_ld % 8 == 0 &&
                     !(reinterpret_cast<uintptr_t>(a.out) & 15) &&
                     (!a.emask || (a.emask_ld % 8 == 0 && !(reinterpret_cast<uintptr_t>(a.emask) & 15)));
+  if (lepi_used) *lepi_used = lepi;
 #define HS_LEPI(DT_, OCT_, NB1_) \
   hipLaunchKernelGGL((conv3x3_hs_kernel<DT_, OCT_, false, 3, NB1_, true>), grid, block, 0, s, a, tx, ty)
   if (pool) {

@@ -146,7 +146,9 @@ int conv_pw_launch(const ConvArgs& a, hipStream_t s) {
   // persistence pays once every CU has a tile: round 4 (kernel without spills) moved the default from 4 to 1 tile
   // per CU (config 5 +0.7 %, config 3 unchanged, profiles/dream_r4_pw_min_tiles.txt)
   if (tiles_total < (min_tiles > 0 ? min_tiles : cus) || tiles_total > 0x7fffffffLL) return -4;
-  const unsigned G = (unsigned)std::min<long long>(tiles_total, 2 * cus);
+  // DV_PW_WG_PER_CU: persistent workgroups per CU (2 by default: each holds 64 KiB of LDS ring)
+  static const long long wpc = std::getenv("DV_PW_WG_PER_CU") ? std::max(1LL, std::atoll(std::getenv("DV_PW_WG_PER_CU"))) : 2;
+  const unsigned G = (unsigned)std::min<long long>(tiles_total, wpc * cus);
   if (BN == 128) {
     if (a.dtype == DT_F16)
       hipLaunchKernelGGL((conv_pw_kernel<DT_F16, 4, 2, 2, 4>), dim3(G), dim3(512), 0, s, a, tiles_n, (int)tiles_total);

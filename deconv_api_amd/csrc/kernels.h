@@ -70,6 +70,13 @@ struct ConvArgs {
                           //   the transposed pooled-max epilogue (conv_dma_impl.h:epilogue_pool_t)
   float* skw;             // optional: KW3P stream-K workspace, kSkSlotFloats fp32 per workgroup (partial tiles)
   unsigned* skflag;       //   + one ready flag per workgroup; zeroed by the launcher before each launch
+  // 1-bit ReLU masks (LDS-staged epilogue only; host: OC % 8 == 0): bit c % 8 of byte c / 8 of row m.
+  // obits: written with the output, bit = (stored 16-bit value > 0); ebits: replaces emask (read 1/16
+  // of its bytes). The launcher sets them only on kernels whose epilogue is epilogue_lds (conv_pw).
+  uint8_t* obits;
+  long long obits_ld;     // bytes per row
+  const uint8_t* ebits;
+  long long ebits_ld;
 };
 // KW3P stream-K: fp32 partial-tile slot per workgroup (BM x BN = 65536 for both KW3P tile shapes)
 constexpr long long kSkSlotFloats = 256LL * 256LL;
@@ -219,7 +226,7 @@ int zsum3x3_launch(const uint16_t* z, float* out, int N, int H, int W, double* s
 int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s);
 // halo-stream 3x3 s1 p1 conv, C % 32 == 0 -> OCpad 64 / 128, 16-bit out or fused 2x2 max-pool +
 // switch (epi CONV_E_BF16 / CONV_E_POOL; < 0: unsupported)
-int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s);
+int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used = nullptr);
 // unpool (pooled map + switch codes, input ReLU) -> 3x3 conv, 16-bit out, on the hs16 kernel (< 0: unsupported)
 int conv3x3_hs_unpool_launch(const ConvArgs& a, hipStream_t s);
 }  // namespace dv

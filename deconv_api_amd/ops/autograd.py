@@ -19,8 +19,11 @@ import torch
 import torch.nn.functional as F
 
 from . import native
-from .conv import ConvWeights, conv2d, pad_channels_oihw, transpose_subpixel
+from .conv import ConvWeights, bits_flags, conv2d, pad_channels_oihw, transpose_subpixel
 
+# DV_RELU_BITS=0: bottleneck outputs keep no 1-bit ReLU masks (the next block's input-gradient epilogue
+# reads the 16-bit activation as its mask again; A/B)
+RELU_BITS = os.environ.get("DV_RELU_BITS", "1") != "0"
 # DV_SUBPIXEL=0 falls back to the direct transposed gather for strided dgrads (A/B testing)
 SUBPIXEL = os.environ.get("DV_SUBPIXEL", "1") != "0"
 # DV_COL2IM=0 disables the GEMM + col2im input gradient of few-channel strided convs (A/B testing)
@@ -182,11 +185,13 @@ class _ConvFn(torch.autograd.Function):
         return gx, None
 
 
-def _dgrad(unit: ConvUnit, gy, mask, in_hw, emask=None):
+def _dgrad(unit: ConvUnit, gy, mask, in_hw, emask=None, ebits=None):
     """Input gradient of one conv unit: A-operand ReLU mask ``mask`` (its output, or None) and
-    output mask ``emask`` (its input, when a ReLU output; applied in the epilogue when possible)."""
+    output mask ``emask`` (its input, when a ReLU output; applied in the epilogue when possible;
+    ``ebits``: its 1-bit form, read instead where the kernel supports it)."""
     if unit.stride == 1:
-        return conv2d(gy, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, mask=mask, use_bias=False, emask=emask)
+        return conv2d(gy, unit.bwd, stride=1, pad=unit.bwd_pad, relu=False, mask=mask, use_bias=False, emask=emask,
+                      ebits=ebits if emask is not None else None)
     gx = _dgrad_strided(unit, gy, mask, in_hw)
     return gx if emask is None else torch.ops.aten.threshold_backward(gx, emask, 0)
 
@@ -440,15 +445,29 @@ class _BottleneckFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, units):
+    def forward(ctx, x, units, box):
         c1, c2, c3, sh = units
-        y1 = conv2d(x, c1.fwd, stride=c1.stride, pad=c1.pad, relu=True)
-        y2 = conv2d(y1, c2.fwd, stride=c2.stride, pad=c2.pad, relu=True)
+        # 1-bit ReLU masks (bit = value > 0, [pixels, C / 8]) written by the same epilogues as y1, y2, y:
+        # the backward's masked input gradients read them instead of the 16-bit maps (16x fewer bytes);
+        # None where the kernel that ran has no such epilogue. y's mask is the NEXT block's (box[0]).
+        def relu_conv(inp, w, stride, pad, **kw):
+            bits = None
+            if RELU_BITS and inp.is_cuda and w.cout % 8 == 0:
+                OH = (inp.shape[1] + 2 * pad[0] - w.KH) // stride + 1
+                OW = (inp.shape[2] + 2 * pad[1] - w.KW) // stride + 1
+                bits = torch.empty(inp.shape[0] * OH * OW, w.cout // 8, dtype=torch.uint8, device=inp.device)
+            out = conv2d(inp, w, stride=stride, pad=pad, relu=True, obits=bits, **kw)
+            return out, (bits if bits is not None and bits_flags() & 1 else None)
+
+        y1, y1b = relu_conv(x, c1.fwd, c1.stride, c1.pad)
+        y2, y2b = relu_conv(y1, c2.fwd, c2.stride, c2.pad)
         sc = x if sh is None else conv2d(x, sh.fwd, stride=sh.stride, pad=sh.pad, relu=False)
-        y = conv2d(y2, c3.fwd, stride=1, pad=c3.pad, relu=True, res=sc)
+        y, box[0] = relu_conv(y2, c3.fwd, 1, c3.pad, res=sc)
+        ctx.y1b, ctx.y2b = y1b, y2b
         ctx.units = units
         ctx.premasked = _PREMASKED[0]
         ctx.x_relu = _is_relu_out(x) and x.is_contiguous()
+        ctx.xbits = getattr(x, "_dv_bits", None)  # x's mask, when the previous block wrote one
         ctx.save_for_backward(x, y1, y2, y)
         return y
 
@@ -460,8 +479,10 @@ class _BottleneckFn(torch.autograd.Function):
         gy = gy.contiguous()
         pm = ctx.premasked
         gm = gy if pm else torch.ops.aten.threshold_backward(gy, y, 0)
-        g2 = conv2d(gm, c3.bwd, stride=1, pad=c3.bwd_pad, relu=False, use_bias=False, emask=y2 if pm else None)
-        g1 = _dgrad(c2, g2, None if pm else y2, (y1.shape[1], y1.shape[2]), emask=y1 if pm else None)
+        g2 = conv2d(gm, c3.bwd, stride=1, pad=c3.bwd_pad, relu=False, use_bias=False, emask=y2 if pm else None,
+                    ebits=ctx.y2b if pm else None)
+        g1 = _dgrad(c2, g2, None if pm else y2, (y1.shape[1], y1.shape[2]), emask=y1 if pm else None,
+                    ebits=ctx.y1b if pm else None)
         emask = x if (pm and ctx.x_relu) else None
         a_mask = None if pm else y1
         if c1.stride > 1 and sh is not None and _pw_strided(c1) and _pw_strided(sh) and sh.stride == c1.stride \
@@ -474,16 +495,16 @@ class _BottleneckFn(torch.autograd.Function):
             gx = torch.empty_like(x)
             native.lib().subpixel_scatter(E[..., : x.shape[3]].contiguous() if E.shape[3] != x.shape[3] else E,
                                           emask, gx, c1.stride)
-            return gx, None
+            return gx, None, None
         gs = gm if sh is None else _dgrad(sh, gm, None, in_hw)
         if c1.stride == 1:
             gx = conv2d(g1, c1.bwd, stride=1, pad=c1.bwd_pad, relu=False, mask=a_mask, use_bias=False, res=gs,
-                        emask=emask)
+                        emask=emask, ebits=ctx.xbits if emask is not None else None)
         else:
             gx = _dgrad_strided(c1, g1, a_mask, in_hw) + gs
             if emask is not None:
                 gx = torch.ops.aten.threshold_backward(gx, emask, 0)
-        return gx, None
+        return gx, None, None
 
 
 def _pw_strided(u: ConvUnit) -> bool:
@@ -495,6 +516,10 @@ def _pw_strided(u: ConvUnit) -> bool:
 def bottleneck(x: torch.Tensor, c1: ConvUnit, c2: ConvUnit, c3: ConvUnit, short: Optional[ConvUnit]) -> torch.Tensor:
     """ReLU(c3(c2(c1(x))) + short(x)) (c1, c2 with ReLU; c3, short linear)."""
     if x.is_cuda:
-        return _tag(_BottleneckFn.apply(x, (c1, c2, c3, short)), True)
+        box = [None]
+        y = _BottleneckFn.apply(x, (c1, c2, c3, short), box)
+        if box[0] is not None:
+            y._dv_bits = box[0]
+        return _tag(y, True)
     sc = short(x) if short is not None else x
     return torch.relu(c3(c2(c1(x))) + sc)

@@ -13,8 +13,8 @@ Reference semantics being implemented (rashanarshad/deconv_api):
 from __future__ import annotations
 
 import contextlib
-
 import os
+import threading
 from dataclasses import dataclass
 from typing import Optional
 
@@ -218,7 +218,8 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
            out: Optional[torch.Tensor] = None, accumulate: bool = False, out_hw=None,
            use_bias: bool = True, res: Optional[torch.Tensor] = None, emask: Optional[torch.Tensor] = None,
            stats: Optional[torch.Tensor] = None, stats_div: int = 1, unpool_out: Optional[torch.Tensor] = None,
-           unpool_div: int = 1, relu_cols: int = 0, out2: Optional[torch.Tensor] = None, split_col: int = 0):
+           unpool_div: int = 1, relu_cols: int = 0, out2: Optional[torch.Tensor] = None, split_col: int = 0,
+           obits: Optional[torch.Tensor] = None, ebits: Optional[torch.Tensor] = None):
     """NHWC convolution.
 
     x: [N, H, W, C] (channel-slice views allowed: stride(3) == 1). For ``in_mode='unpool'`` x is
@@ -235,6 +236,10 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     ``out2`` / ``split_col`` (GPU, plain 16-bit forward): output channels >= split_col go to ``out2``
     (channel c -> out2[..., c - split_col]) and only the leading ones to ``out`` - one merged GEMM
     feeding two consumers (InceptionV3: the b1 branch's concat slice and the heads buffer).
+    ``obits`` (GPU, uint8 [M, OC / 8]): also write the output's 1-bit ReLU mask (bit = value > 0);
+    ``ebits`` (GPU, with ``emask``): the 1-bit mask of ``emask`` to read instead of it. Both ride only on
+    the persistent 1x1 kernel: ``bits_flags()`` tells whether the last call on this thread wrote obits
+    (1) / used ebits (2); otherwise obits is unwritten and emask applied as usual.
     """
     if pad is None:
         pad = (cw.KH // 2, cw.KW // 2)
@@ -260,7 +265,8 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     if x.is_cuda:
         return _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
                            mask, epilogue, out, accumulate, use_bias, res, emask, stats, stats_div, unpool_out,
-                           unpool_div, relu_cols, out2, split_col)
+                           unpool_div, relu_cols, out2, split_col, obits, ebits)
+    _tls.bits = 0  # CPU: no bit masks
     assert stats is None, "conv2d: stats are produced by the GPU kernels only"
     if out2 is not None:  # CPU: the full result, split between the two destinations
         y = _conv2d_ref(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div,
@@ -372,9 +378,17 @@ def conv_group_paused():
         lib.conv_group_pause(False)
 
 
+_tls = threading.local()
+
+
+def bits_flags() -> int:
+    """1-bit mask flags of this thread's last conv2d: 1 = obits written, 2 = ebits used."""
+    return getattr(_tls, "bits", 0)
+
+
 def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mode, code, code_div, mask,
                 epilogue, out, accumulate, use_bias, res=None, emask=None, stats=None, stats_div=1,
-                unpool_out=None, unpool_div=1, relu_cols=0, out2=None, split_col=0):
+                unpool_out=None, unpool_div=1, relu_cols=0, out2=None, split_col=0, obits=None, ebits=None):
     lib = native.lib()
     dt = x.dtype
     assert dt in (torch.bfloat16, torch.float16) and x.stride(3) == 1, \
@@ -421,9 +435,10 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
         (emask is not None and _policy["impl"] not in ("auto",))
     if _group_open[0]:
         _group_refs.append((x, cw, out, code, mask, res, emask, out2))
-    lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
-             IMPL["dma"] if dma_only else IMPL[_policy["impl"]],  # DMA-only epilogue features
-             res, emask, stats, stats_div, unpool_out, unpool_div, relu_cols, out2, split_col)
+    _tls.bits = lib.conv(x, cw.w_gemm, bias, out, out_code, code, mask, geom, AMODE[in_mode], EPI[epilogue],
+                         IMPL["dma"] if dma_only else IMPL[_policy["impl"]],  # DMA-only epilogue features
+                         res, emask, stats, stats_div, unpool_out, unpool_div, relu_cols, out2, split_col,
+                         obits, ebits)
     if epilogue == "pool":
         return out, out_code
     return out

@@ -273,6 +273,86 @@ def test_gpu_bottleneck_block_grad(native_lib, stride, proj, premasked):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gpu_relu_bits_conv_pw(native_lib, dt):
+    """1-bit ReLU masks on the persistent 1x1 kernel: obits == packbits(out > 0) (bit c % 8 of byte c / 8);
+    a masked input gradient with ebits == the same with the 16-bit emask, bit for bit."""
+    import numpy as np
+
+    from deconv_api_amd import ops
+    from deconv_api_amd.ops import autograd as AG
+
+    g = torch.Generator().manual_seed(5)
+    u = AG.ConvUnit("c", torch.randn(256, 64, 1, 1, generator=g) / 8, torch.randn(256, generator=g) * 0.1, 1, (0, 0),
+                    relu=True).build("cuda", dt)
+    x = torch.randn(4, 128, 128, 64, generator=g).to(dt).cuda()
+    ob = torch.zeros(4 * 128 * 128, 32, dtype=torch.uint8, device="cuda")
+    y = ops.conv2d(x, u.fwd, relu=True, obits=ob)
+    assert ops.conv.bits_flags() == 1
+    want = np.packbits((y.float() > 0).cpu().numpy().reshape(-1, 256), axis=1, bitorder="little")
+    assert np.array_equal(ob.cpu().numpy(), want)
+    gs = torch.randn(4, 128, 128, 256, generator=g).to(dt).cuda()
+    ref = ops.conv2d(x, u.fwd, relu=False, use_bias=False, res=gs, emask=y)
+    assert ops.conv.bits_flags() == 0
+    got = ops.conv2d(x, u.fwd, relu=False, use_bias=False, res=gs, emask=y, ebits=ob)
+    assert ops.conv.bits_flags() == 2 and torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,cout", [(128, 64), (66, 64), (64, 128)])
+def test_gpu_relu_bits_halo_stream(native_lib, hw, cout):
+    """1-bit masks on the halo-stream 3x3 kernels' LDS-staged epilogues (hs16 at sides % 16, the 16 x 32
+    kernel otherwise): obits == packbits(out > 0); ebits == emask bit for bit."""
+    import numpy as np
+
+    from deconv_api_amd import ops
+    from deconv_api_amd.ops import autograd as AG
+
+    g = torch.Generator().manual_seed(hw + cout)
+    u = AG.ConvUnit("c", torch.randn(cout, 64, 3, 3, generator=g) / 24, torch.randn(cout, generator=g) * 0.1, 1,
+                    (1, 1), relu=True).build("cuda", torch.float16)
+    x = torch.randn(3, hw, hw, 64, generator=g).to(torch.float16).cuda()
+    ob = torch.zeros(3 * hw * hw, cout // 8, dtype=torch.uint8, device="cuda")
+    y = ops.conv2d(x, u.fwd, relu=True, obits=ob)
+    assert ops.conv.bits_flags() == 1
+    want = np.packbits((y.float() > 0).cpu().numpy().reshape(-1, cout), axis=1, bitorder="little")
+    assert np.array_equal(ob.cpu().numpy(), want)
+    gy = torch.randn(3, hw, hw, cout, generator=g).to(torch.float16).cuda()
+    w = AG.ConvUnit("d", torch.randn(cout, cout, 3, 3, generator=g) / 24, None, 1, (1, 1), relu=False).build(
+        "cuda", torch.float16)
+    ref = ops.conv2d(gy, w.fwd, relu=False, use_bias=False, emask=y)
+    got = ops.conv2d(gy, w.fwd, relu=False, use_bias=False, emask=y, ebits=ob)
+    assert ops.conv.bits_flags() == 2 and torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_gpu_relu_bits_bottleneck_chain_identical(native_lib, monkeypatch):
+    """Two chained bottlenecks (premasked): the second block's input gradient masked by the first block's
+    1-bit mask == masked by its 16-bit output (DV_RELU_BITS=0), bit for bit."""
+    from deconv_api_amd.ops import autograd as AG
+
+    g = torch.Generator().manual_seed(9)
+    mk = lambda n, ci, co, k, p, relu: AG.ConvUnit(  # noqa: E731
+        n, torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5, torch.randn(co, generator=g) * 0.1, 1, (p, p),
+        relu=relu).build("cuda", torch.float16)
+    blocks = [[mk("c1", 256, 64, 1, 0, True), mk("c2", 64, 64, 3, 1, True), mk("c3", 64, 256, 1, 0, False), None]
+              for _ in range(2)]
+    x = torch.randn(8, 64, 64, 256, generator=g).clamp_min(0).to(torch.float16).cuda()
+    gy = torch.randn(8, 64, 64, 256, generator=g).to(torch.float16).cuda()
+    out = {}
+    for bits in (True, False):
+        monkeypatch.setattr(AG, "RELU_BITS", bits)
+        xd = x.clone().requires_grad_(True)
+        with AG.premasked_grads():
+            y = AG.bottleneck(AG.tag_relu_output(xd), *blocks[0])
+            assert (getattr(y, "_dv_bits", None) is not None) == bits
+            z = AG.bottleneck(y, *blocks[1])
+        (gx,) = torch.autograd.grad(z, xd, gy * (z.detach() > 0))
+        out[bits] = gx
+    assert torch.equal(out[True], out[False])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bi,hw", [(0, 11), (3, 11), (4, 9), (8, 9), (9, 5)])
 @pytest.mark.parametrize("premasked", [False, True])
 @pytest.mark.parametrize("strided_direct", [True, False])
