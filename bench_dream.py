@@ -6,7 +6,8 @@
             python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
                 bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 32 --dtype fp16   (8 GPUs:
             batch 32 gives each rank 4-16 (tile, image) units per step; at batch 8 a rank holds 1-4 and runs
-            latency-bound, profiles/dream_c5_r4_virtual_ranks.txt)
+            latency-bound, profiles/dream_c5_r4_virtual_ranks.txt; a rank's units run as 2 chunks on two
+            forked streams, each chunk's pack all-gather issued behind it: profiles/dream_c5_r5_local_chunks.txt)
 
 One timed run = the whole octave loop (octaves x steps gradient-ascent iterations + octave
 resizes/detail re-injection) over the batch. Prints ONE JSON line (rank 0). Synthetic uint8
