@@ -1234,10 +1234,16 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
       r_po[u] = valid ? ((uint32_t)((n - n_base) * HW + oh * W + px) << 12) | (uint32_t)oh : ~0u;
     }
   };
+  // SV 3 / 4 (timing ablations, WRONG outputs): after the first step, no DMA at all / no weight (B) DMA:
+  // how much of a launch waits on operand staging (tools/kw3_ab.py VAR 20 / 21)
+  bool abl_first = true;
   auto issue = [&](int step, int buf) {
     const int kh = step % 3, cc = step / 3;  // kh innermost (see the KW3 header)
     uint8_t* As = smem + 2 * B_BYTES + buf * A_BYTES;
     uint8_t* Bs = smem + buf * B_BYTES;
+    const bool abl_skip = (SV == 3 || SV == 4) && !abl_first;
+    abl_first = false;
+    if (SV == 3 && abl_skip) return;
 #pragma unroll
     for (int u = 0; u < A_I; ++u) {
       if ((u * NW + wave) * 16 >= nslots) continue;
@@ -1247,6 +1253,7 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
           ok ? ((uint32_t)(pix + (kh - 1) * W) * (uint32_t)a.x_ld + (uint32_t)(cc * 32 + lchunk * 8)) * 2u : kOOB;
       dma16(xr, As + (u * NW + wave) * 1024, voff);
     }
+    if (SV == 4 && abl_skip) return;
 #pragma unroll
     for (int u = 0; u < B_I; ++u) {
       const int vv = u * NW + wave;
@@ -1643,7 +1650,7 @@ static int kw3_mode() {
 static int kw3_var() {
   const char* e = std::getenv("DV_KW3_VAR");
   const int v = e ? std::atoi(e) : kKw3DefaultVar;
-  if (v == 8 || v == 9 || v == 10) {
+  if (v == 8 || v == 9 || v == 10 || v == 20 || v == 21) {
     static bool warned = false;
     if (std::getenv("DV_ALLOW_WRONG_ABLATION") == nullptr) {
       if (!warned) fprintf(stderr, "deconv_api_amd: DV_KW3_VAR=%d ignored (needs DV_ALLOW_WRONG_ABLATION=1)\n", v);
@@ -1705,7 +1712,7 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
     const dim3 grid((unsigned)nwg);
     if constexpr (EPI == CONV_E_BF16) {
       // VAR 10 / 11 (bf16 only): KW3P without epilogue stores (timing ablation) / with nt stores
-      const bool pvar = var == 2 || (DT == DT_BF16 && (var == 10 || var == 11));
+      const bool pvar = var == 2 || (DT == DT_BF16 && (var == 10 || var == 11 || var == 20 || var == 21));
       auto launch_p = [&](auto em) -> int {
         constexpr int U = decltype(em)::value;
         const unsigned g = (unsigned)(nwg < (long long)num_cus() ? nwg : (long long)num_cus());
@@ -1716,6 +1723,13 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
           }
           if (var == 11) {
             hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 2>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg, kw3p_pre());
+            return (int)hipGetLastError();
+          }
+          if (var == 20 || var == 21) {
+            if (var == 20)
+              hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 3>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg, 0);
+            else
+              hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 4>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg, 0);
             return (int)hipGetLastError();
           }
         }
@@ -1886,6 +1900,13 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
   const long long cus = num_cus();
   auto nwg = [&](int BM, int BN) { return (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN); };
   if (a.OCpad % 256 == 0 && a.OC > 128) {
+    {  // DV_KW3_TILE=512x128 (per launch): the 512 x 128 KW3P tile for these shapes too (A/B)
+      const char* kt = std::getenv("DV_KW3_TILE");
+      if (kt && std::strcmp(kt, "512x128") == 0) {
+        const int rc = kw3_try<DT, AMODE, EPI, 128, 512>(a, s);
+        if (rc != -4) return rc;
+      }
+    }
     if (kw3_mode() == 2) {
       const int rc = kw3_try<DT, AMODE, EPI>(a, s);
       if (rc != -4) return rc;

@@ -64,8 +64,9 @@ def main():
             # 2: KW3P as selected (stream-K where it applies, step-1 DMA ahead of the epilogue stores);
             # 12: whole tiles (DV_NO_KW3_SK=1); 13: whole tiles without the early DMA (+ DV_KW3P_NO_PRE=1);
             # 14: stream-K without the early DMA; 15: whole tiles with the register-transposed 8-B store epilogue;
-            # 16: stream-K on every eligible grid (DV_KW3_SK=all)
-            os.environ["DV_KW3_VAR"] = str(2 if v in (12, 13, 14, 15, 16) else v)
+            # 16: stream-K on every eligible grid (DV_KW3_SK=all); 20 / 21: KW3P ablations without any DMA after
+            # the first step / without the weight DMA (WRONG outputs: how much of a launch waits on staging)
+            os.environ["DV_KW3_VAR"] = str(2 if v in (12, 13, 14, 15, 16, 22) else v)
             for k, on in (("DV_NO_KW3_SK", v in (12, 13, 15)), ("DV_KW3P_NO_PRE", v in (13, 14))):
                 if on:
                     os.environ[k] = "1"
@@ -79,6 +80,10 @@ def main():
                 os.environ["DV_KW3_SK"] = "all"
             else:
                 os.environ.pop("DV_KW3_SK", None)
+            if v == 22:  # the 512 x 128 KW3P tile on 256 / 512-channel outputs
+                os.environ["DV_KW3_TILE"] = "512x128"
+            else:
+                os.environ.pop("DV_KW3_TILE", None)
             if unp:  # a fresh unpooled output per call (as the engine does)
                 out[v] = ops.conv2d(x, cw, relu=True, use_bias=False, unpool_out=code, unpool_div=4)
                 return out[v]
@@ -87,7 +92,7 @@ def main():
         for v in variants:  # warm up every variant (and check the real ones agree)
             run(v)
         torch.cuda.synchronize()
-        real = [v for v in variants if v < 8 or v in (11, 12, 13, 14, 15, 16)]
+        real = [v for v in variants if v < 8 or v in (11, 12, 13, 14, 15, 16, 22)]
         for v in real[1:]:
             same = torch.equal(out[v], out[real[0]])
             if not same:  # stream-K vs whole tiles: split tiles round differently
