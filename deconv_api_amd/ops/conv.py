@@ -238,8 +238,9 @@ def conv2d(x: torch.Tensor, cw: ConvWeights, *, stride: int = 1, pad=None, relu:
     feeding two consumers (InceptionV3: the b1 branch's concat slice and the heads buffer).
     ``obits`` (GPU, uint8 [M, OC / 8]): also write the output's 1-bit ReLU mask (bit = value > 0);
     ``ebits`` (GPU, with ``emask``): the 1-bit mask of ``emask`` to read instead of it. Both ride only on
-    the persistent 1x1 kernel: ``bits_flags()`` tells whether the last call on this thread wrote obits
-    (1) / used ebits (2); otherwise obits is unwritten and emask applied as usual.
+    the persistent 1x1 kernel and the halo-stream kernels' LDS-staged epilogues: ``bits_flags()`` tells
+    whether the last call on this thread wrote obits (1) / used ebits (2); otherwise obits is unwritten
+    and emask applied as usual.
     """
     if pad is None:
         pad = (cw.KH // 2, cw.KW // 2)
