@@ -1,5 +1,6 @@
 """CPU: the trace / layout analysis tools behind the committed profiles (tools/kstats.py,
-tools/kseq.py, tools/lds_bank_check.py, tools/spill_diff.py) on synthetic inputs."""
+tools/kseq.py, tools/lds_bank_check.py, tools/spill_diff.py, tools/dream_gaps.py, tools/roofline.py) on
+synthetic inputs."""
 import os
 import sqlite3
 import sys
@@ -97,3 +98,24 @@ def test_native_extension_links():
 
     lib = native.load()
     assert lib is not None and hasattr(native.lib(), "conv")
+
+
+def test_dream_gaps_idle_and_queues(trace_db, capsys):
+    """tools/dream_gaps.py: per-queue gaps and device-wide idle (no kernel on any queue) of a trace."""
+    import dream_gaps
+
+    dream_gaps.main([trace_db])
+    out = capsys.readouterr().out
+    assert "queue 1:" in out and "queue 2:" in out
+    # the two queues start 1 us apart and run the same 1-us-gapped sequence: they overlap almost fully
+    assert "recorded concurrency" in out and "device idle" in out
+
+
+def test_roofline_counts_config2_flops(capsys):
+    """tools/roofline.py prices config 2 from torch's flop formulas on the engine's CPU path (one image,
+    scaled): 38.41 TFLOP per 256-image step, the number the committed roofline tables quote."""
+    import roofline
+
+    roofline.main(["--config", "2", "--img-per-s", "7600"])
+    out = capsys.readouterr().out
+    assert "38.41 TFLOP" in out and "1.140 PF/s" in out
