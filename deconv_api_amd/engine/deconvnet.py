@@ -37,6 +37,10 @@ VALID_MODES = ("all", "max")
 # makes the halves independent
 DECONV_STREAMS = max(1, int(os.environ.get("DV_DECONV_STREAMS", "1")))
 DECONV_SPLIT_MIN = int(os.environ.get("DV_DECONV_SPLIT_MIN", "64"))
+# DV_UNPOOL_CONSUMER_MAXC: conv-downs consuming an unpooled map with at most this many input channels
+# expand the unpool themselves (64: block1_conv2.down's fused tail; 128 adds block2_conv2.down on the
+# hs16 unpool path, which also needs DV_HSU=1); wider consumers get the map from the producer's epilogue
+UNPOOL_CONSUMER_MAXC = int(os.environ.get("DV_UNPOOL_CONSUMER_MAXC", "64"))
 
 
 class UnknownLayerError(KeyError):
@@ -229,7 +233,7 @@ class DeconvNet:
             below = self.specs[j - 1] if j >= 2 else None
             fuse_unpool = (below is not None and below.kind == "pool" and j >= 3 and pending_code is None and
                            cl.dec.cout % 8 == 0 and
-                           (not d.is_cuda or self.rt.convs[self.specs[j - 2].name].dec.cin != 64))
+                           (not d.is_cuda or self.rt.convs[self.specs[j - 2].name].dec.cin > UNPOOL_CONSUMER_MAXC))
             if pending_code is not None and j == 2 and self.specs[1].kind == "conv" and d.is_cuda:
                 # unpool -> block1_conv2.down -> block1_conv1.down as two kernels (the 64-channel map
                 # stays on chip: ops.deconv_tail); None if the shape is not the kernel's
