@@ -781,8 +781,8 @@ class TiledDeepDream(DeepDream):
                 if coll:  # the collective's communicator is set up outside the capture
                     works = [self._gather_chunk(st, c) for c in range(st.C)]
             torch.cuda.current_stream(self.device).wait_stream(s)
-            for work in works:  # retire the eager warm-up collectives before the capture opens
-                drain_collective(work, self.device, self.coll_wait)
+            for i, work in enumerate(works):  # retire the eager warm-up collectives before the capture opens
+                drain_collective(work, self.device, self.coll_wait, settle=i + 1 == len(works))
             if not coll or CAPTURE_COLLECTIVE:
                 # the whole octave, all-gathers included (RCCL collectives are graph-capturable):
                 # one replay per octave instead of `iterations` replays + eager collectives

@@ -17,6 +17,7 @@ collective (work.wait + device sync) before a capture that follows it.
 """
 from __future__ import annotations
 
+import time
 from typing import Callable, Optional
 
 import torch
@@ -31,14 +32,20 @@ def capture(fn: Callable[[], object], graph: Optional[torch.cuda.CUDAGraph] = No
     return g, out
 
 
-def drain_collective(work, device, wait=None) -> None:
+def drain_collective(work, device, wait=None, settle: bool = True) -> None:
     """Retire an eager (async_op=True) collective before a capture: wait for its work object
     (``wait(work)`` when given: the caller's polled wait under its failure deadlines), then
-    synchronize the device so its end event has completed before the capture opens (the watchdog
-    may still hold the work; with thread-local capture its poll is legal either way, and a
-    completed event makes the poll trivially succeed)."""
+    synchronize the device so its end event has completed before the capture opens, and (``settle``,
+    once after the last of several) give the process group's watchdog time to drop it (below)."""
     if work is not None:
         if wait is not None:
             wait(work)
         work.wait()
     torch.cuda.synchronize(device)
+    if work is not None and settle:
+        # ... and let ProcessGroupNCCL's watchdog (which wakes every 100 ms) drop the completed work from its
+        # list first: HIP refuses hipEventQuery on an event of a stream that is capturing NOW, even one
+        # recorded before the capture, so a watchdog poll of this work's end event once the captured
+        # collectives have pulled the NCCL stream into the capture aborts the process (hipErrorCapturedEvent,
+        # intermittently in tests/test_deepdream.py::test_gpu_tiled_collective_octave_captured)
+        time.sleep(0.3)
