@@ -257,6 +257,9 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
       bw[s][j] = *reinterpret_cast<const bf16x8*>(a.w + (long long)oc * a.Kpad + k);
     }
   constexpr bool TR = (V & 1) != 0, ILV = (V & 2) != 0;
+  // timing ablations (WRONG outputs, DV_TAIL_V with DV_ALLOW_WRONG_ABLATION=1, tools/tail_ab.py): 4 = no Z
+  // GEMM / Z stores, 8 = no halo expansion (the MFMAs read a stale halo)
+  constexpr bool NO_Z = (V & 4) != 0, NO_EXP = (V & 8) != 0;
   float biasv[2][TR ? 4 : 1];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -370,7 +373,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
                          : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[s][j], acc[i][j], 0, 0, 0);
       }
       if constexpr (ILV) {
-        if (s == 12 && t < ntiles) store_tile(smem + (cur ^ 1) * V2_A, t);  // behind the remaining MFMAs
+        if (!NO_EXP && s == 12 && t < ntiles) store_tile(smem + (cur ^ 1) * V2_A, t);  // behind the remaining MFMAs
       }
     }
     __syncthreads();  // every wave is done with the previous tile's Cst reads and this halo
@@ -410,7 +413,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_unpool_c64_v2_kernel(const Con
       if (t < ntiles) store_tile(smem + (cur ^ 1) * V2_A, t);
     }
     __syncthreads();
-    if constexpr (ZOUT) {  // ---- Z = D W2^T for tile row `wave`, 8-B stores (4 Z channels of one px) ----
+    if constexpr (NO_Z) {  // ablation: no Z GEMM and no output stores at all
+    } else if constexpr (ZOUT) {  // ---- Z = D W2^T for tile row `wave`, 8-B stores (4 Z channels of one px) ----
       int b = tcur;
       const int tx = b % tiles_w;
       b /= tiles_w;
@@ -1165,12 +1169,16 @@ int conv3x3_unpool_z_launch(const ConvArgs& a, hipStream_t s) {
   if (ntiles <= 0 || ntiles > 0x7fffffffLL) return -2;
   // DV_TAIL_V: variant bits (see the kernel); 3 by default, 0 = the round-4 schedule (A/B)
   const char* tve = std::getenv("DV_TAIL_V");  // per launch: tests switch it in one process
-  const int tv = tve ? (std::atoi(tve) & 3) : 3;
+  int tv = tve ? std::atoi(tve) : 3;
+  if ((tv & ~3) && std::getenv("DV_ALLOW_WRONG_ABLATION") == nullptr) tv &= 3;  // ablation bits: tools only
   const dim3 g((unsigned)std::min<long long>(ntiles, cus));
   if (tv == 0) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 0>), g, dim3(512), 0, s, a);
   else if (tv == 1) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 1>), g, dim3(512), 0, s, a);
   else if (tv == 2) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 2>), g, dim3(512), 0, s, a);
-  else hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 3>), g, dim3(512), 0, s, a);
+  else if (tv == 3) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 3>), g, dim3(512), 0, s, a);
+  else if (tv == 3 + 4) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 3 + 4>), g, dim3(512), 0, s, a);
+  else if (tv == 3 + 8) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 3 + 8>), g, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 3 + 4 + 8>), g, dim3(512), 0, s, a);
   return (int)hipGetLastError();
 }
 
