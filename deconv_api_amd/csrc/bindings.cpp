@@ -826,6 +826,36 @@ int64_t tile_pack_elems(int64_t ucap, int64_t Th, int64_t Tw) { return dv::tile_
 
 // geom: KH, KW, stride, pad_h, pad_w, Cr; cols [N, OH, OW, J_ld] (J = KH*KW*Cr), gx [N, H, W, 8]
 // g = KH, KW, stride, pad, Cr; false: not the fused kernel's geometry (caller falls back)
+// ResNet-50 conv1 forward on the tap-paired MFMA kernel (conv_stem7.hip): x [N,H,W,8], w [64][224]
+// (kh, kw 0..7, c 0..3; zero where kw = 7 or c = 3), bias fp32 >= 64, out [N,OH,OW,64], all dense.
+// Returns false when the geometry is not covered (the caller takes the implicit GEMM).
+bool stem7_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, int64_t relu) {
+  check_cuda(x, "x");
+  check_cuda(w, "w");
+  check_cuda(out, "out");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 4 && out.dim() == 4 && x.size(3) == 8 && out.size(3) == 64 && x.is_contiguous() &&
+                  out.is_contiguous() && w.is_contiguous() && w.numel() == 64 * 224 &&
+                  x.scalar_type() == out.scalar_type() && w.scalar_type() == x.scalar_type() &&
+                  out.size(0) == x.size(0),
+              "stem7_fwd: x [N,H,W,8], w [64][224], out [N,OH,OW,64], dense, one 16-bit dtype");
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() >= 64,
+                "stem7_fwd: bias fp32");
+    bp = bias->data_ptr<float>();
+  }
+  const int rc = dv::stem7_fwd_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                      reinterpret_cast<const uint16_t*>(w.data_ptr()), bp,
+                                      reinterpret_cast<uint16_t*>(out.data_ptr()), (int)x.size(0), (int)x.size(1),
+                                      (int)x.size(2), (int)out.size(1), (int)out.size(2), (int)relu, dt_of(x),
+                                      cur_stream());
+  if (rc == -4) return false;
+  check_rc(rc, "stem7_fwd");
+  return true;
+}
+
 bool stem_dgrad_fused(Tensor gy, c10::optional<Tensor> mask, Tensor w, Tensor gx, std::vector<int64_t> g) {
   check_cuda(gy, "gy");
   check_cuda(w, "w");
@@ -1290,6 +1320,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dream_update", &dream_update, "fused DeepDream normalize + update + next network input");
   m.def("octave_resize", &octave_resize, "DeepDream octave transition: corner-aligned bilinear resize of (a + b - c)",
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("y"), py::arg("yin") = py::none());
+  m.def("stem7_fwd", &stem7_fwd, "ResNet-50 conv1 forward (7x7 / 2, RGB -> 64) on the tap-paired MFMA kernel");
   m.def("stem_dgrad_fused", &stem_dgrad_fused, "fused GEMM + col2im input gradient of a 7x7/2 RGB stem conv");
   m.def("col2im", &col2im, "col2im of a strided few-channel conv's input gradient");
   m.def("jpeg_data_urls", &jpeg_data_urls, "native JPEG + base64/quote data URLs (GIL released)");

@@ -196,6 +196,10 @@ int col2im_launch(const uint16_t* cols, uint16_t* gx, const Col2ImGeom& g, int d
 struct StemDgradGeom {
   int N, H, W, OH, OW, C, KH, KW, stride, pad, Cr, w_rows, w_ld;
 };
+// ResNet-50 conv1 forward (7x7 / 2, pad 3, RGB -> 64) on the tap-paired MFMA kernel (conv_stem7.hip);
+// < 0: not its geometry
+int stem7_fwd_launch(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W, int OH,
+                     int OW, int relu, int dtype, hipStream_t s);
 int stem_dgrad_fused_launch(const uint16_t* gy, const uint16_t* mask, const uint16_t* wb, uint16_t* gx,
                             const StemDgradGeom& g, int dtype, hipStream_t s);
 // GPU baseline JPEG encode of B same-size RGB images (jpeg_gpu.hip): entropy-coded scans (restart

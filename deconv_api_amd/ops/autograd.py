@@ -32,6 +32,9 @@ COL2IM = os.environ.get("DV_COL2IM", "1") != "0"
 STEM_DIRECT = os.environ.get("DV_STEM_DIRECT", "1") != "0"
 # DV_STEM_FUSED=0: ResNet-50 conv1's input gradient as GEMM (cols to HBM) + col2im (A/B)
 STEM_FUSED = os.environ.get("DV_STEM_FUSED", "1") != "0"
+# DV_STEM7=0: ResNet-50 conv1's forward on the generic implicit GEMM instead of the tap-paired MFMA
+# kernel (csrc/conv_stem7.hip) (A/B)
+STEM7 = os.environ.get("DV_STEM7", "1") != "0"
 
 
 _PREMASKED = [False]
@@ -127,6 +130,13 @@ class ConvUnit:
                 if STEM_DIRECT and cr == 3 and self.stride == 2 and w8.shape[1] == 8 and kh == kw == 3 and \
                         self.cout == 32:
                     self.stem_w = self.w.permute(2, 3, 1, 0).contiguous().to(self.device)
+                # ResNet-50 conv1 (3 -> 64, 7x7 / 2, pad 3) forward: [64][kh][kw 0..7][c 0..3] weights
+                # (kw = 7 and c = 3 zero) for the tap-paired MFMA kernel (csrc/conv_stem7.hip)
+                self.stem7_w = None
+                if cr == 3 and kh == kw == 7 and self.stride == 2 and tuple(self.pad) == (3, 3) and self.cout == 64:
+                    w4 = torch.zeros(64, 7, 8, 4)
+                    w4[:, :, :7, :3] = self.w.permute(0, 2, 3, 1).float()
+                    self.stem7_w = w4.reshape(64, 224).to(self.device, dtype).contiguous()
                 # sub-pixel classes: s^2 stride-1 convs instead of one s^2-times-wasteful gather
                 self.bwd_sub = []
                 for rh, rw, ws, pd in transpose_subpixel(w8, self.stride, self.pad):
@@ -144,9 +154,16 @@ class ConvUnit:
 
 
 def _stem_fwd(x, unit: ConvUnit):
-    """conv2d_1-style strided few-channel conv on the direct kernel, or None (geometry not covered)."""
+    """Strided few-channel stem conv on its own kernel, or None (geometry not covered): ResNet-50's
+    conv1 on the tap-paired MFMA kernel, conv2d_1-style 3x3 convs on the direct VALU kernel."""
+    w7 = getattr(unit, "stem7_w", None)
+    if STEM7 and w7 is not None and x.shape[3] == 8 and x.is_contiguous():
+        N, H, W, _ = x.shape
+        y = torch.empty(N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 64, dtype=x.dtype, device=x.device)
+        if native.lib().stem7_fwd(x, w7, unit.fwd.bias_pad, y, int(unit.relu)):
+            return y
     if getattr(unit, "stem_w", None) is None or unit.pad[0] != unit.pad[1] or unit.w.shape[2] != 3:
-        return None  # (the 7x7 forward stays on the implicit GEMM: 386 TF/s there)
+        return None
     N, H, W, C = x.shape
     OH = (H + 2 * unit.pad[0] - 3) // unit.stride + 1
     OW = (W + 2 * unit.pad[1] - 3) // unit.stride + 1

@@ -597,6 +597,35 @@ def test_gpu_stem_conv_direct(native_lib, p, H, W):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W,bias", [(2, 37, 41, True), (1, 64, 96, True), (3, 150, 133, False), (2, 224, 224, True)])
+def test_gpu_stem7_fwd(native_lib, monkeypatch, dt, N, H, W, bias):
+    """ResNet-50 conv1 forward (3 -> 64, 7x7 / 2, pad 3, bias + ReLU) on the tap-paired MFMA kernel
+    (csrc/conv_stem7.hip) vs an fp32 PyTorch conv of the same rounded operands and vs the implicit
+    GEMM path of the same unit (a different fp32 summation order: equal up to one 16-bit rounding);
+    odd sizes and partial output tiles."""
+    from deconv_api_amd.ops import autograd as AG
+
+    g = torch.Generator().manual_seed(N * H + W)
+    w = (torch.randn(64, 3, 7, 7, generator=g) / (3 * 49) ** 0.5).to(dt).float()
+    b = torch.randn(64, generator=g) * 0.1 if bias else None
+    x = torch.randn(N, H, W, 3, generator=g).to(dt).float()
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, stride=2, padding=3).relu().permute(0, 2, 3, 1)
+    gpu = AG.ConvUnit("u", w, b, 2, (3, 3), relu=True).build("cuda", dt)
+    assert gpu.stem7_w is not None
+    x8 = torch.nn.functional.pad(x, (0, 5)).to(dt).cuda()
+    y7 = AG._stem_fwd(x8, gpu)
+    assert y7 is not None and y7.shape == ref.shape
+    monkeypatch.setattr(AG, "STEM7", False)
+    assert AG._stem_fwd(x8, gpu) is None
+    yg = gpu(x8).float().cpu()
+    y7 = y7.float().cpu()
+    tol = (8e-3 if dt == torch.float16 else 2e-2) * ref.abs().max()
+    assert (y7 - ref).abs().max() < tol
+    assert (y7 - yg).abs().max() < tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("H,W,premasked", [(37, 41, True), (64, 96, True), (150, 133, False), (224, 224, True)])
 def test_gpu_stem_dgrad_fused(native_lib, monkeypatch, dt, H, W, premasked):
     """ResNet-50 conv1 (3 -> 64, 7x7 / 2, pad 3) input gradient: the fused MFMA GEMM + col2im kernel
