@@ -30,11 +30,56 @@ constexpr int SD_PROW = 244;                   // P^T row stride in 16-bit eleme
 
 __device__ __forceinline__ int floor_div(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
+template <int DT, int KH, int KW, int S, int KH0, int KW0, int RN, int CN>
+__device__ __forceinline__ void col2im_taps(const uint16_t* __restrict__ P, uint16_t* __restrict__ gx,
+                                            const StemDgradGeom& g, int n, int ih0, int iw0, int oh_lo, int ow_lo,
+                                            int py, int px, int lane) {
+  constexpr int NH = (KH - KH0 + S - 1) / S, NW = (KW - KW0 + S - 1) / S;  // taps of this parity class
+  constexpr int cw_ = SD_TW / S;                                          // class columns per tile row
+#pragma unroll
+  for (int q = lane; q < SD_TH * SD_TW / 4; q += 64) {
+    const int p = ((q / cw_) * S + py) * SD_TW + (q % cw_) * S + px;
+    const int ih = ih0 + p / SD_TW, iw = iw0 + p % SD_TW;
+    // window row / column of tap (KH0, KW0); tap (KH0 + S a, KW0 + S b) sits a rows / b columns before it
+    const int r0 = (ih + g.pad - KH0) / S - oh_lo, c0 = (iw + g.pad - KW0) / S - ow_lo;
+    const uint16_t* base = P + r0 * CN + c0;
+    uint16_t v[NH][NW][3];
+#pragma unroll
+    for (int a = 0; a < NH; ++a)
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        const int j = ((KH0 + S * a) * KW + KW0 + S * b) * 3;
+        const int off = j * SD_PROW - (a * CN + b);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[a][b][c] = base[off + c * SD_PROW];
+      }
+    if (ih >= g.H || iw >= g.W) continue;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int a = 0; a < NH; ++a)
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        a0 += to_f<DT>(v[a][b][0]);
+        a1 += to_f<DT>(v[a][b][1]);
+        a2 += to_f<DT>(v[a][b][2]);
+      }
+    uint4 o;
+    o.x = pack2<DT>(a0, a1);
+    o.y = pack2<DT>(a2, 0.f);
+    o.z = 0u;
+    o.w = 0u;
+    const long long dst = (((long long)n * g.H + ih) * g.W + iw) * 8;
+    if (DV_BOUNDS(dst, 8, (long long)g.N * g.H * g.W * 8, "stem_dgrad_fused gx"))
+      *reinterpret_cast<uint4*>(gx + dst) = o;
+  }
+}
+
 template <int DT, int KH, int KW, int S, int JP>
-__global__ void __launch_bounds__(256) stem_dgrad_fused_kernel(const uint16_t* __restrict__ gy,
-                                                              const uint16_t* __restrict__ mask,
-                                                              const uint16_t* __restrict__ wb,
-                                                              uint16_t* __restrict__ gx, StemDgradGeom g) {
+// waves_per_eu(2): two workgroups per CU (the LDS allows two); without it the 40 accumulator tiles
+// took 80 VGPRs + 212 AGPRs and ONE workgroup per CU ran its serial phases with nothing to overlap
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+stem_dgrad_fused_kernel(const uint16_t* __restrict__ gy, const uint16_t* __restrict__ mask, const uint16_t* __restrict__ wb,
+                        uint16_t* __restrict__ gx, StemDgradGeom g) {
   typedef typename Vec8<DT>::type v8;
   constexpr int RN = (SD_TH + KH - 2) / S + 2, CN = (SD_TW + KW - 2) / S + 2;  // dy rows / cols a tile reads
   static_assert(RN * CN <= 240 && JP % 16 == 0 && JP * SD_PROW * 2 <= 81920, "window / P^T must fit");
@@ -131,40 +176,19 @@ __global__ void __launch_bounds__(256) stem_dgrad_fused_kernel(const uint16_t* _
 
   // ---- 3. col2im from LDS: each dx pixel gathers its taps (same order as col2im_kernel) ----
   // Pixels are dealt by stride-S parity class: wave w owns the pixels with (ih % S, iw % S) = class w
-  // (S * S == 4 waves), so every lane of a wave walks the same tap subset (no divergent tap loop)
-  static_assert(S * S == 4 || S == 1, "parity-class assignment needs S*S == 4 waves");
-  for (int q = lane; q < SD_TH * SD_TW / 4; q += 64) {
-    const int py = S == 1 ? 0 : (wave / S), px = S == 1 ? 0 : (wave % S);
-    const int cw_ = SD_TW / S;  // class columns per tile row
-    const int p = S == 1 ? (wave * (SD_TH * SD_TW / 4) + q)
-                         : ((q / cw_) * S + py) * SD_TW + (q % cw_) * S + px;
-    const int ih = ih0 + p / SD_TW, iw = iw0 + p % SD_TW;
-    if (ih >= g.H || iw >= g.W) continue;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    const int kh0 = (ih + g.pad) % S, kw0 = (iw + g.pad) % S;
-#pragma unroll
-    for (int kh = 0; kh < KH; ++kh) {
-      if ((kh - kh0) % S != 0) continue;
-      const int r = (ih + g.pad - kh) / S - oh_lo;
-#pragma unroll
-      for (int kw = 0; kw < KW; ++kw) {
-        if ((kw - kw0) % S != 0) continue;
-        const int c = (iw + g.pad - kw) / S - ow_lo;
-        const int row = r * CN + c;
-        const int j = (kh * KW + kw) * 3;
-        a0 += to_f<DT>(P[j * SD_PROW + row]);
-        a1 += to_f<DT>(P[(j + 1) * SD_PROW + row]);
-        a2 += to_f<DT>(P[(j + 2) * SD_PROW + row]);
-      }
-    }
-    uint4 o;
-    o.x = pack2<DT>(a0, a1);
-    o.y = pack2<DT>(a2, 0.f);
-    o.z = 0u;
-    o.w = 0u;
-    const long long dst = (((long long)n * g.H + ih) * g.W + iw) * 8;
-    if (DV_BOUNDS(dst, 8, (long long)g.N * g.H * g.W * 8, "stem_dgrad_fused gx"))
-      *reinterpret_cast<uint4*>(gx + dst) = o;
+  // (S * S == 4 waves), so every lane of a wave walks the same tap subset. That subset is a template
+  // parameter (col2im_taps<KH0, KW0>): every tap's P^T offset is a compile-time constant from one
+  // per-pixel base, so all of a pixel's LDS reads issue back to back instead of one dependent read per
+  // tap behind runtime tap predicates (~4 us of serialized LDS latency per workgroup)
+  static_assert(S == 2, "parity-class assignment needs S*S == 4 waves");
+  const int py = wave / S, px = wave % S;
+  const int kh0 = (ih0 + py + g.pad) % S, kw0 = (iw0 + px + g.pad) % S;  // ih0, iw0 even: uniform per wave
+  if (kh0 == 0) {
+    if (kw0 == 0) col2im_taps<DT, KH, KW, S, 0, 0, RN, CN>(P, gx, g, n, ih0, iw0, oh_lo, ow_lo, py, px, lane);
+    else col2im_taps<DT, KH, KW, S, 0, 1, RN, CN>(P, gx, g, n, ih0, iw0, oh_lo, ow_lo, py, px, lane);
+  } else {
+    if (kw0 == 0) col2im_taps<DT, KH, KW, S, 1, 0, RN, CN>(P, gx, g, n, ih0, iw0, oh_lo, ow_lo, py, px, lane);
+    else col2im_taps<DT, KH, KW, S, 1, 1, RN, CN>(P, gx, g, n, ih0, iw0, oh_lo, ow_lo, py, px, lane);
   }
 }
 
