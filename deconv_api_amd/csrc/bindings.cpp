@@ -1095,11 +1095,11 @@ void seed_deconv3x3(Tensor S, Tensor f, Tensor wt, Tensor out) {
   const int64_t Cin = wt.size(3);
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == B * H * W * Cin,
               "seed: out [B,H,W,Cin] bf16");
-  // f values are validated on the host side (ops layer clamps to [-1, F))
+  // f values >= F are clamped to F - 1 in the kernel; < 0 gives a zero map
   check_rc(dv::seed_deconv3x3_launch(S.data_ptr<float>(), f.data_ptr<int>(),
                                      reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                                      reinterpret_cast<uint16_t*>(out.data_ptr()), (int)B, (int)H, (int)W, (int)Cin,
-                                     cur_stream()),
+                                     (int)wt.size(0), cur_stream()),
            "seed_deconv3x3");
 }
 
@@ -1231,6 +1231,58 @@ bool conv_unpool_z(Tensor x, Tensor code, int64_t code_div, Tensor w, Tensor w2,
   return true;
 }
 
+// fused VGG16 stem: x bf16 [N, H, W, 8] (preprocessed RGB, channels 3..7 zero) -> conv1 (w1 [64][>= 96],
+// b1) + ReLU -> conv2 (w2 [64][>= 576], b2) + ReLU -> 2x2 max-pool: out bf16 [N, H/2, W/2, 64] + switch
+// codes u8 (the layout conv(..., CONV_E_POOL) writes). false: shape unsupported (caller runs 2 launches)
+bool conv_stem_pool(Tensor x, Tensor w1, c10::optional<Tensor> b1, Tensor w2, c10::optional<Tensor> b2, Tensor out,
+                    Tensor out_code) {
+  check_cuda(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.size(3) == 8,
+              "conv_stem_pool: x bf16 [N, H, W, 8]");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "conv_stem_pool: even H, W");
+  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.size(0) == N &&
+                  out.size(1) == H / 2 && out.size(2) == W / 2 && out.size(3) == 64,
+              "conv_stem_pool: out bf16 [N, H/2, W/2, 64]");
+  TORCH_CHECK(out_code.scalar_type() == at::kByte && out_code.is_contiguous() && out_code.numel() == out.numel(),
+              "conv_stem_pool: out_code u8 [N, H/2, W/2, 64]");
+  TORCH_CHECK(w1.scalar_type() == at::kBFloat16 && w1.is_contiguous() && w1.dim() == 2 && w1.size(0) == 64 &&
+                  w1.size(1) >= 96,
+              "conv_stem_pool: w1 bf16 [64, Kpad >= 96]");
+  TORCH_CHECK(w2.scalar_type() == at::kBFloat16 && w2.is_contiguous() && w2.dim() == 2 && w2.size(0) == 64 &&
+                  w2.size(1) >= 576,
+              "conv_stem_pool: w2 bf16 [64, Kpad >= 576]");
+  for (const auto* b : {&b1, &b2})
+    if (b->has_value())
+      TORCH_CHECK((*b)->scalar_type() == at::kFloat && (*b)->is_contiguous() && (*b)->numel() >= 64 && (*b)->is_cuda(),
+                  "conv_stem_pool: bias fp32 [>= 64] on the device");
+  check_cuda(w1, "w1");
+  check_cuda(w2, "w2");
+  check_cuda(out, "out");
+  check_cuda(out_code, "out_code");
+  dv::ConvArgs a{};
+  a.N = (int)N; a.H = a.OH = (int)H; a.W = a.OW = (int)W; a.C = 64;
+  a.OC = a.OCpad = 64; a.KH = a.KW = 3; a.stride = 1; a.pad_h = a.pad_w = 1;
+  a.K = 576; a.Kpad = (int)w2.size(1); a.M = (int)(N * H * W);
+  a.relu = 1; a.code_div = 1; a.x_ld = 8; a.out_ld = 64;
+  a.dtype = dv::DT_BF16;
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.w = reinterpret_cast<const uint16_t*>(w2.data_ptr());
+  a.bias = b2.has_value() ? b2->data_ptr<float>() : nullptr;
+  a.w2 = reinterpret_cast<const uint16_t*>(w1.data_ptr());
+  a.bias2 = b1.has_value() ? b1->data_ptr<float>() : nullptr;
+  a.kpad2 = (int)w1.size(1);
+  a.out = out.data_ptr();
+  a.out_code = out_code.data_ptr<uint8_t>();
+  a.x_elems = avail_bytes(x) / 2;
+  a.out_elems = avail_bytes(out) / 2;
+  const int rc = dv::conv3x3_stem_pool_launch(a, cur_stream());
+  if (rc == -4) return false;
+  check_rc(rc, "conv_stem_pool");
+  return true;
+}
+
 // out fp32 [N, H, W, 3] = ReLU(9-tap shift-add of z [N, H, W, 32]); optional per-image stats
 void zsum3x3(Tensor z, Tensor out, c10::optional<Tensor> stats, int64_t stats_div) {
   check_cuda(z, "z");
@@ -1343,6 +1395,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("preprocess_u8", &preprocess_u8, "resized RGB u8 -> caffe-preprocessed bf16 network input");
   m.def("maxpool2x2", &maxpool2x2);
   m.def("unpool2x2", &unpool2x2);
+  m.def("conv_stem_pool", &conv_stem_pool, "fused VGG16 stem: conv 8->64 -> conv 64->64 -> 2x2 max-pool + switches");
   m.def("conv_unpool_z", &conv_unpool_z, "unpool -> conv3x3 64->64 -> ReLU -> per-tap products of the next 64->3 conv");
   m.def("zsum3x3", &zsum3x3, "9-tap shift-add of a per-tap product map (+ ReLU, per-image stats)");
   m.attr("ARCH") = "gfx950";

@@ -422,9 +422,16 @@ constexpr int HU_PBUF = HU_PI * 4 * 1024, HU_CBUF = HU_CI * 4 * 1024;
 // whole 16-B chunks, OCT / 8 lanes per pixel row: each store instruction writes 4 (OCT 128) or 8 pixels'
 // complete 256 / 128-B rows instead of 16 pixels x 32 B (the register layout's 8-B stores). The same
 // change on the persistent KW3P kernel took 9-13 % off its launches (profiles/kw3_epi_ab_r5.txt).
-template <int DT, int OCT, bool POOL, bool UNPOOL, int TPS = 1, bool LEPI = false>
+// STEM (VGG16 block1_conv1 -> block1_conv2 -> pool, conv3x3_stem_pool_launch): a.x is the 8-channel RGB
+// image; both 32-channel halo buffers are COMPUTED in the prologue as the first conv (a.w2 / a.bias2) of
+// the tile's 18 x 18 halo from a 20 x 20 RGB window, instead of DMA'd from its 64-channel output map. The
+// first conv runs exactly as conv3x3_c8_stream_kernel does it (same MFMA operands and K order, bias,
+// ReLU, bf16 rounding), so the result is bit-identical to the two-launch path while the 2 x 128 B/px of
+// that map's HBM write + read disappear.
+template <int DT, int OCT, bool POOL, bool UNPOOL, int TPS = 1, bool LEPI = false, bool STEM = false>
 __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
   static_assert(!LEPI || !POOL, "LDS epilogue: plain / emask outputs");
+  static_assert(!STEM || (TPS == 3 && POOL && !UNPOOL && DT == DT_BF16), "fused stem: 64 -> 64 + pool, bf16");
   static_assert(TPS == 1 || (TPS == 3 && OCT == 64 && !UNPOOL), "3-tap steps: 64 output channels, no unpool");
   constexpr int FN = OCT / 16;                // output-channel blocks
   constexpr int BI = OCT / 64 * TPS;          // weight DMA instructions per wave and step (TPS*OCT*64 B / 4 KiB)
@@ -552,7 +559,68 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
   // pixel reads: halo pixel (4 wave + i + kh) * 18 + px + kw; its swizzle term varies with kw only
   // through (px + kw) (the row term 18 * r shifts bit 2 too, so it is folded per (i + kh) at compile
   // time via the row's base pixel index)
-  issue_halo(0, 0);
+  if constexpr (!STEM) issue_halo(0, 0);
+  if constexpr (STEM) {
+    // RGB window rows ty0 - 2 .., cols tx0 - 2 .. (20 x 20 px x 16 B, zero outside the image) -> weight
+    // ring slot 1, which the first weight DMA into it (issue_w(1), after step 0's barrier) overwrites
+    uint8_t* rgb = ring + BSLOT;
+    const uint16_t* xs = a.x + (long long)n * H * W * 8;
+    for (int e = tid; e < 400; e += 256) {
+      const int ry = e / 20, rx = e - 20 * (e / 20);
+      const int y = ty0 - 2 + ry, x = tx0 - 2 + rx;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W &&
+          DV_BOUNDS(((long long)n * H * W + (long long)y * W + x) * 8, 8, a.x_elems, "stem rgb"))
+        v = *reinterpret_cast<const uint4*>(xs + ((long long)y * W + x) * 8);
+      *reinterpret_cast<uint4*>(rgb + e * 16) = v;
+    }
+    // first conv's weights (A = weights, K-step s = taps 4s .. 4s+3 x 8 channels; taps >= 9 are zero
+    // columns of the packed matrix) and bias: lane (q, px) -> output channel 16 j + px / 16 j + 4 q + r
+    v8 wa[3][4];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        wa[s][j] = *reinterpret_cast<const v8*>(a.w2 + (long long)(j * 16 + px) * a.kpad2 + s * 32 + q * 8);
+    float b1[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b1[j][r] = a.bias2 ? a.bias2[j * 16 + q * 4 + r] : 0.f;
+    __syncthreads();
+    // halo pixel p = 16 f + px (18 x 18, row-major): 21 fragments round-robin over the 4 waves
+    for (int f = wave; f < 21; f += 4) {
+      const int p = f * 16 + px;
+      const int hy = p / H16_HW, hx = p - H16_HW * (p / H16_HW);
+      f32x4 c1[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int t = 4 * s + q;
+        const int kh = t / 3, kw = t - 3 * (t / 3);
+        uint4 bv = make_uint4(0u, 0u, 0u, 0u);
+        if (t < 9 && p < H16_HW * H16_HW) bv = *reinterpret_cast<const uint4*>(rgb + ((hy + kh) * 20 + hx + kw) * 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c1[j] = mfma16x16x32<DT>(wa[s][j], __builtin_bit_cast(v8, bv), c1[j]);
+      }
+      if (p < H16_HW * H16_HW) {
+        const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;  // the second conv's zero padding outside the image
+        const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = in ? fmaxf(c1[j][r] + b1[j][r], 0.f) : 0.f;
+          // channel 16 j + 4 q + r: halo buffer j / 2, 16-B chunk (j & 1) * 2 + q / 2, byte 8 (q & 1)
+          const int ch = (j & 1) * 2 + (q >> 1);
+          *reinterpret_cast<uint2*>(halo + (j >> 1) * H16_HBUF + p * 64 + ((ch ^ h16_swz(p)) << 4) + (q & 1) * 8) =
+              make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before every reader by step 0's barrier
+  }
   if constexpr (UNPOOL) {
     hs_wait<0>();
     __builtin_amdgcn_s_barrier();  // every wave's share of the staging DMA has landed
@@ -569,11 +637,11 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const int k = c * 3 + kh;
-        if (kh == 1) hs_wait<HI>();
+        if (kh == 1 && !STEM) hs_wait<HI>();
         else hs_wait<0>();
         __builtin_amdgcn_s_barrier();
         issue_w(k + 1);
-        if (kh == 0) issue_halo(c + 1, (c + 1) & 1);
+        if (kh == 0 && !STEM) issue_halo(c + 1, (c + 1) & 1);
         const uint8_t* wb = ring + (k % RING) * BSLOT + wrd;
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
@@ -942,6 +1010,28 @@ int conv3x3_hs_unpool_launch(const ConvArgs& a, hipStream_t s) {
     if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_BF16, 128, false, true>), g16, b16, 0, s, a, t16x, t16y);
     else hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_BF16, 64, false, true>), g16, b16, 0, s, a, t16x, t16y);
   }
+  return (int)hipGetLastError();
+}
+
+
+// fused VGG16 stem (block1_conv1 -> block1_conv2 -> 2x2 max-pool + switch): the hs16 pool kernel with the
+// halo computed from the RGB image (STEM above). a: the SECOND conv's geometry (C = OC = 64, pad 1)
+// with a.x = the 8-channel image (x_ld 8), a.w2 / a.bias2 / a.kpad2 the first conv's packed weights.
+// Forward-only and bf16; DV_STEM_FUSE=0 (Python side) keeps the two-launch path.
+int conv3x3_stem_pool_launch(const ConvArgs& a, hipStream_t s) {
+  if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.C != 64 || a.OC != 64 ||
+      a.OCpad != 64 || a.x_ld != 8 || a.H != a.OH || a.W != a.OW || a.H % 16 || a.W % 16 || a.H <= 0 || a.W <= 0 ||
+      a.N <= 0 || a.dtype != DT_BF16 || a.w2 == nullptr || a.kpad2 < 96 || a.Kpad < 9 * 64 || a.out_code == nullptr ||
+      a.out_ld != 64 || a.relu != 1 || a.relu_in || a.accumulate || a.mask || a.code || a.res || a.emask || a.ws ||
+      a.ucode || (reinterpret_cast<uintptr_t>(a.x) & 15) || (reinterpret_cast<uintptr_t>(a.out) & 7) ||
+      (reinterpret_cast<uintptr_t>(a.out_code) & 3) || (reinterpret_cast<uintptr_t>(a.w2) & 15) ||
+      (long long)a.H * a.W * 8 * 2 > 0x7FFFFFF0LL)
+    return -4;
+  const int tx = a.W / 16, ty = a.H / 16;
+  const long long nwg = (long long)a.N * tx * ty;
+  if (nwg > 0x7fffffffLL) return -2;
+  hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_BF16, 64, true, false, 3, false, true>), dim3((unsigned)nwg), dim3(256), 0,
+                     s, a, tx, ty);
   return (int)hipGetLastError();
 }
 

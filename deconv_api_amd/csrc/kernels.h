@@ -77,6 +77,10 @@ struct ConvArgs {
   long long obits_ld;     // bytes per row
   const uint8_t* ebits;
   long long ebits_ld;
+  // fused stem (conv3x3_stem_pool_launch): the first conv's packed weights are w2 ([64][kpad2], K index
+  // tap * 8 + c of the 8-channel RGB input) and its fp32 bias bias2
+  const float* bias2;
+  int kpad2;
 };
 // KW3P stream-K: fp32 partial-tile slot per workgroup (BM x BN = 65536 for both KW3P tile shapes)
 constexpr long long kSkSlotFloats = 256LL * 256LL;
@@ -122,7 +126,7 @@ int channel_sum_launch(const uint16_t* x, float* sums, int N, int HW, int C, hip
 int topk_pos_launch(const float* v, int* idx, float* val, int N, int C, int k, hipStream_t s);
 // one-channel seeded deconv: out[b][h][w][ci] = relu(sum_taps S[b][h+kh-1][w+kw-1] * wt[f_b][kh][kw][ci])
 int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint16_t* out,
-                          int B, int H, int W, int Cin, hipStream_t s);
+                          int B, int H, int W, int Cin, int F, hipStream_t s);
 // fp32 recon [B*4][224][224][3] -> u8 mosaic [B][448][448][3] (channel-reversed), Keras deprocess
 int deprocess_mosaic_launch(const float* recon, uint8_t* out, int B, int H, int W, int tiles,
                             int reverse_channels, hipStream_t s);
@@ -228,6 +232,10 @@ int conv3x3_unpool_z_launch(const ConvArgs& a, hipStream_t s);
 int zsum3x3_launch(const uint16_t* z, float* out, int N, int H, int W, double* stats, int stats_div, hipStream_t s);
 // first layer: 3x3 conv of an 8-channel image -> <= 64 channels, bias + ReLU, bf16 (< 0: unsupported)
 int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s);
+// fused VGG16 stem: 3x3 conv 8 (RGB) -> 64 + ReLU (weights a.w2 / a.bias2), 3x3 conv 64 -> 64 + ReLU
+// (a.w / a.bias) and the 2x2 max-pool with switches, one hs16 launch; the 64-channel map between the two
+// convs lives only in LDS (conv_halo_stream.hip; < 0: unsupported)
+int conv3x3_stem_pool_launch(const ConvArgs& a, hipStream_t s);
 // halo-stream 3x3 s1 p1 conv, C % 32 == 0 -> OCpad 64 / 128, 16-bit out or fused 2x2 max-pool +
 // switch (epi CONV_E_BF16 / CONV_E_POOL; < 0: unsupported)
 int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used = nullptr);

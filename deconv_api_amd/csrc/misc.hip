@@ -110,24 +110,29 @@ int topk_pos_launch(const float* v, int* idx, float* val, int N, int C, int k, h
 // reference: app/deepdream.py:80-89). 1/C_out of the work of a dense conv-transpose.
 // f_b < 0 (fewer positive filters than requested) produces a zero map.
 // ---------------------------------------------------------------------------------------
+// f_b is clamped to [-1, F) here (one ALU op; the host no longer runs a clamp launch). Index math is
+// 32-bit (the launcher checks B*H*W*Cin/8 < 2^31): the 64-bit div/mod chain per 16-B chunk made this
+// memory-bound kernel ALU-bound (141 us for 205 MB at block5, profiles/kseq_c2_r5.txt).
 __global__ void __launch_bounds__(256) seed_deconv3x3_kernel(const float* __restrict__ S,
                                                              const int* __restrict__ f,
                                                              const uint16_t* __restrict__ wt,
                                                              uint16_t* __restrict__ out, int B, int H,
-                                                             int W, int Cin) {
-  const int cpp = Cin >> 3;
-  const long long total = (long long)B * H * W * cpp;
-  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total; g += (long long)gridDim.x * 256) {
-    const int chunk = (int)(g % cpp);
-    long long pix = g / cpp;
-    const int w = (int)(pix % W);
-    const int h = (int)((pix / W) % H);
-    const int b = (int)(pix / ((long long)W * H));
-    const int fb = f[b];
+                                                             int W, int Cin, int F) {
+  const unsigned cpp = (unsigned)Cin >> 3;
+  const unsigned total = (unsigned)B * H * W * cpp;
+  for (unsigned g = blockIdx.x * 256u + threadIdx.x; g < total; g += gridDim.x * 256u) {
+    const unsigned pix = g / cpp;
+    const unsigned chunk = g - pix * cpp;
+    const unsigned hw = (unsigned)H * W;
+    const unsigned b = pix / hw;
+    const unsigned r = pix - b * hw;
+    const int h = (int)(r / (unsigned)W);
+    const int w = (int)(r - (unsigned)h * W);
+    const int fb = min(f[b], F - 1);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (fb >= 0) {
-      const float* Sb = S + (long long)b * H * W;
-      const uint16_t* wf = wt + (long long)fb * 9 * Cin + chunk * 8;
+      const float* Sb = S + (size_t)b * hw;
+      const uint16_t* wf = wt + (size_t)fb * 9 * Cin + chunk * 8;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const int ih = h + kh - 1;
@@ -151,17 +156,18 @@ __global__ void __launch_bounds__(256) seed_deconv3x3_kernel(const float* __rest
     o.y = pack_bf2(fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
     o.z = pack_bf2(fmaxf(acc[4], 0.f), fmaxf(acc[5], 0.f));
     o.w = pack_bf2(fmaxf(acc[6], 0.f), fmaxf(acc[7], 0.f));
-    *reinterpret_cast<uint4*>(out + pix * Cin + chunk * 8) = o;
+    *reinterpret_cast<uint4*>(out + (size_t)g * 8) = o;
   }
 }
 
 int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint16_t* out, int B, int H,
-                          int W, int Cin, hipStream_t s) {
-  if (Cin % 8 != 0 || B <= 0) return -1;
+                          int W, int Cin, int F, hipStream_t s) {
+  if (Cin % 8 != 0 || B <= 0 || F <= 0) return -1;
   const long long total = (long long)B * H * W * (Cin / 8);
+  if (total >= (1LL << 31) || (long long)F * 9 * Cin >= (1LL << 31)) return -2;
   const long long blocks = std::min<long long>((total + 255) / 256, 256LL * 16);
   hipLaunchKernelGGL(seed_deconv3x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, S, f, wt, out, B, H,
-                     W, Cin);
+                     W, Cin, F);
   return (int)hipGetLastError();
 }
 

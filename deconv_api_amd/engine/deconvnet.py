@@ -114,6 +114,17 @@ class DeconvNet:
             if s.kind == "conv":
                 cl = self.rt.convs[s.name]
                 nxt = seq[i + 1] if i + 1 < len(seq) else None
+                # conv -> conv -> pool at the first layer (VGG16 block1): one fused launch whose
+                # intermediate 64-channel map stays in LDS (ops.conv.stem_pool)
+                if (i == 0 and fuse_pools and not keep_all and x.is_cuda and i + 2 < len(seq) and
+                        nxt.kind == "conv" and seq[i + 2].kind == "pool" and
+                        (hook is None or hook[0] != nxt.name)):
+                    r = ops.stem_pool(x, cl.fwd, self.rt.convs[nxt.name].fwd)
+                    if r is not None:
+                        x, code = r
+                        st.codes[seq[i + 2].name] = code
+                        i += 3
+                        continue
                 if fuse_pools and not keep_all and nxt is not None and nxt.kind == "pool":
                     x, code = ops.conv2d(x, cl.fwd, relu=True, epilogue="pool")
                     st.codes[nxt.name] = code

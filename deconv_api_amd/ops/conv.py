@@ -449,6 +449,36 @@ def _conv2d_hip(x, cw, N, H, W, C, OH, OW, OC, stride, pad, relu, relu_in, in_mo
 FUSED_TAIL = os.environ.get("DV_FUSED_TAIL", "1") != "0"
 
 
+# DV_STEM_FUSE=0 turns off the fused VGG16 stem (conv 8->64 -> conv 64->64 -> pool as one launch)
+STEM_FUSE = os.environ.get("DV_STEM_FUSE", "1") != "0"
+
+
+def stem_ok(x: torch.Tensor, c1: ConvWeights, c2: ConvWeights) -> bool:
+    """Shapes the fused stem takes: an 8-channel bf16 NHWC image with sides % 16 == 0, 3x3 8 -> 64 -> 64."""
+    return (STEM_FUSE and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[3] == 8 and
+            x.shape[1] % 16 == 0 and x.shape[2] % 16 == 0 and x.is_contiguous() and
+            c1.kind == "fwd" and c1.KH == 3 and c1.KW == 3 and c1.cin == 8 and c1.cout == 64 and
+            c2.kind == "fwd" and c2.KH == 3 and c2.KW == 3 and c2.cin == 64 and c2.cout == 64 and
+            c1.w_gemm is not None and c2.w_gemm is not None and c1.w_gemm.dtype == torch.bfloat16)
+
+
+def stem_pool(x: torch.Tensor, c1: ConvWeights, c2: ConvWeights):
+    """VGG16 block1_conv1 -> block1_conv2 -> block1_pool as ONE launch (``conv3x3_hs16_kernel`` STEM):
+    each 16 x 16 output tile computes its 18 x 18 x 64 conv1 halo from the RGB image straight into LDS,
+    so the 64-channel 224^2 map between the two convs (2 x 1.6 GB of HBM traffic per 256 images) is never
+    written. Bit-identical to ``conv2d(conv2d(x, c1), c2, epilogue='pool')``. Returns ``(pooled, codes)``,
+    or None when the device kernel does not take the shape (the caller runs the separate launches).
+    Reference: app/deepdream.py:99 (the per-layer conv up of the deconvnet's forward)."""
+    if not stem_ok(x, c1, c2):
+        return None
+    N, H, W, _ = x.shape
+    out = torch.empty(N, H // 2, W // 2, 64, dtype=x.dtype, device=x.device)
+    code = torch.empty(N, H // 2, W // 2, 64, dtype=torch.uint8, device=x.device)
+    if not native.lib().conv_stem_pool(x, c1.w_gemm, c1.bias_pad, c2.w_gemm, c2.bias_pad, out, code):
+        return None
+    return out, code
+
+
 def tail_w2(last: ConvWeights) -> torch.Tensor:
     """[32, 64] matrix of a 64 -> 3 (3x3) conv's taps: row (kh*3 + kw)*3 + c = W[c, :, kh, kw]
     (rows 27..31 zero), in the dtype of the packed GEMM matrix. Cached on ``last``."""

@@ -103,7 +103,7 @@ def seed_deconv3x3(S: torch.Tensor, f: torch.Tensor, wt: torch.Tensor) -> torch.
     B, H, W = S.shape
     F_, _, _, Cin = wt.shape
     if S.is_cuda:
-        f = f.to(torch.int32).clamp(-1, F_ - 1).contiguous()
+        f = f.to(torch.int32).contiguous()  # values >= F are clamped in the kernel
         out = torch.empty(B, H, W, Cin, dtype=wt.dtype, device=S.device)
         native.lib().seed_deconv3x3(S.float().contiguous(), f, wt.contiguous(), out)
         return out

@@ -588,6 +588,17 @@ def test_seed_deconv(native_lib):
     got = ops.seed_deconv3x3(S.to(DEV), f.to(DEV), wt.to(DEV))
     assert _rel(got, ref) < 1e-2
     assert got[3].abs().sum() == 0
+    # an out-of-range filter index is clamped to F - 1 inside the kernel (no host clamp launch)
+    f_hi = f.clone()
+    f_hi[2] = 4096
+    got_hi = ops.seed_deconv3x3(S.to(DEV), f_hi.to(DEV), wt.to(DEV))
+    assert torch.equal(got_hi, got)
+    # a block5-sized map (B*K = 1024 signals x 14^2 x 512): 32-bit index math over 12.8 M chunks
+    Sb = torch.relu(torch.randn(1024, 14, 14, generator=g))
+    fb = torch.randint(-1, 512, (1024,), generator=g, dtype=torch.int32)
+    gb = ops.seed_deconv3x3(Sb.to(DEV), fb.to(DEV), wt.to(DEV))
+    for i in (0, 511, 1023):
+        assert _rel(gb[i:i + 1], ops.seed_deconv3x3(Sb[i:i + 1], fb[i:i + 1], wt)) < 1e-2
 
 
 @pytest.mark.parametrize("pool", [False, True])
