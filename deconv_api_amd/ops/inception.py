@@ -275,14 +275,6 @@ class _InceptionFn(torch.autograd.Function):
             state["written"] = True
             state["masked"] = emask is not None
 
-        def contribute_tensor(t):
-            if state["written"]:
-                gx.add_(t)
-            else:
-                gx.copy_(t)
-            state["written"] = True
-            state["masked"] = False
-
         def dgrad_into(u, g, inp, out=None, accumulate=False):
             """gradient w.r.t. ``inp`` (a ReLU output) of conv unit u, masked by inp > 0"""
             if u.stride == 1:
@@ -298,13 +290,11 @@ class _InceptionFn(torch.autograd.Function):
             gsl = gY[..., off:off + wdt]
             if kind == "max":
                 idx = saved[info[0]]
-                if state["written"]:
-                    t = torch.empty_like(x)
-                    lib.pool(gsl, t, idx, 0, 1, _pool_geom(N, H, W, Cin, 3, 2, 0))
-                    contribute_tensor(t)
-                else:
-                    lib.pool(gsl, gx, idx, 0, 1, _pool_geom(N, H, W, Cin, 3, 2, 0))
-                    state["written"] = True
+                # written before: the kernel adds its window sums to gx in the same pass (no separate
+                # pool-into-temporary + ATen add launch)
+                lib.pool(gsl, gx, idx, 0, 1, _pool_geom(N, H, W, Cin, 3, 2, 0), accumulate=state["written"])
+                state["written"] = True
+                state["masked"] = False
                 continue
             if kind == "avg":
                 u = blk.units[info[0]]

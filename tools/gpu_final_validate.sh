@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-end validation in one gpurun call: GPU suite, smoke, config-2 bench x3, configs 3 and 5
+set -o pipefail
+O=gpurun_out/final
+mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_all.log 2>&1 || exit 1
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 2
+for i in 1 2 3; do timeout -k 10 200 python bench.py > $O/bench_$i.log 2>&1 || exit 3; done
+timeout -k 10 300 python bench_dream.py --model inception_v3 --batch 64 --size 299 > $O/dream_c3.log 2>&1 || exit 4
+timeout -k 10 300 python bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 8 --dtype fp16 > $O/dream_c5.log 2>&1 || exit 5
+echo done
