@@ -561,21 +561,26 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
   // time via the row's base pixel index)
   if constexpr (!STEM) issue_halo(0, 0);
   if constexpr (STEM) {
-    // RGB window rows ty0 - 2 .., cols tx0 - 2 .. (20 x 20 px x 16 B, zero outside the image) -> weight
-    // ring slot 1, which the first weight DMA into it (issue_w(1), after step 0's barrier) overwrites
+    // step 0's weights (slot 0) go out first: their DMA latency overlaps the prologue instead of following it
+    issue_w(0);
+    // RGB window rows ty0 - 2 .., cols tx0 - 2 ..
     uint8_t* rgb = ring + BSLOT;
     const uint16_t* xs = a.x + (long long)n * H * W * 8;
-    for (int e = tid; e < 400; e += 256) {
+    // every global read of the prologue is issued before the first use (one memory round trip, not
+    // one per dependent load): the RGB window, then the first conv's weights (A = weights, K-step s =
+    // taps 4s .. 4s+3 x 8 channels; taps >= 9 are zero columns) and bias (lane (q, px) -> output
+    // channel 16 j + px / 16 j + 4 q + r)
+    uint4 rv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 256 * u;
       const int ry = e / 20, rx = e - 20 * (e / 20);
       const int y = ty0 - 2 + ry, x = tx0 - 2 + rx;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W &&
+      rv[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (e < 400 && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W &&
           DV_BOUNDS(((long long)n * H * W + (long long)y * W + x) * 8, 8, a.x_elems, "stem rgb"))
-        v = *reinterpret_cast<const uint4*>(xs + ((long long)y * W + x) * 8);
-      *reinterpret_cast<uint4*>(rgb + e * 16) = v;
+        rv[u] = *reinterpret_cast<const uint4*>(xs + ((long long)y * W + x) * 8);
     }
-    // first conv's weights (A = weights, K-step s = taps 4s .. 4s+3 x 8 channels; taps >= 9 are zero
-    // columns of the packed matrix) and bias: lane (q, px) -> output channel 16 j + px / 16 j + 4 q + r
     v8 wa[3][4];
 #pragma unroll
     for (int s = 0; s < 3; ++s)
@@ -587,6 +592,11 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) b1[j][r] = a.bias2 ? a.bias2[j * 16 + q * 4 + r] : 0.f;
+    // -> weight ring slot 1 (20 x 20 px x 16 B, zero outside the image), which the first weight DMA into it
+    // (issue_w(1), after step 0's barrier) overwrites
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tid + 256 * u < 400) *reinterpret_cast<uint4*>(rgb + (tid + 256 * u) * 16) = rv[u];
     __syncthreads();
     // halo pixel p = 16 f + px (18 x 18, row-major): 21 fragments round-robin over the 4 waves
     for (int f = wave; f < 21; f += 4) {
@@ -631,7 +641,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
     // step k = (chunk c, kernel row kh): weights W(k) -> slot k % 2, issued at step k - 1 right after
     // its barrier, BEFORE that step's halo(c + 1) DMAs (kh == 0), so the wait for W(k) leaves the
     // younger halo in flight at kh == 1 and drains it at kh == 2 (two steps to land)
-    issue_w(0);
+    if constexpr (!STEM) issue_w(0);
     for (int c = 0; c < nch; ++c) {
       const uint8_t* hb = halo + (c & 1) * H16_HBUF;
 #pragma unroll
