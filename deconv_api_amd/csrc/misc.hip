@@ -1,5 +1,6 @@
 // Small gfx950 kernels around the conv core: filter selection, seeded first deconv step,
 // mosaic deprocess, fused resize+preprocess, standalone pool/unpool.
+#include <cstdlib>
 #include "common.h"
 #include "kernels.h"
 
@@ -131,24 +132,25 @@ __global__ void __launch_bounds__(256) seed_deconv3x3_kernel(const float* __rest
     const int fb = min(f[b], F - 1);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (fb >= 0) {
+      // all 9 taps' S values and weight chunks are loaded before the first FMA (one memory round trip;
+      // a zero-skip branch on each loaded S made every weight load wait for it). A wave is one pixel's
+      // 64 chunks: the S loads are wave-uniform, the weight loads 1 KiB coalesced rows.
       const float* Sb = S + (size_t)b * hw;
       const uint16_t* wf = wt + (size_t)fb * 9 * Cin + chunk * 8;
+      float sv[9];
+      uint4 wv[9];
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const int ih = h + kh - 1;
-        if ((unsigned)ih >= (unsigned)H) continue;
+      for (int t = 0; t < 9; ++t) {
+        const int ih = h + t / 3 - 1, iw = w + t % 3 - 1;
+        sv[t] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? Sb[ih * W + iw] : 0.f;
+        wv[t] = *reinterpret_cast<const uint4*>(wf + t * Cin);
+      }
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int iw = w + kw - 1;
-          if ((unsigned)iw >= (unsigned)W) continue;
-          const float sv = Sb[ih * W + iw];
-          if (sv == 0.f) continue;
-          const uint4 wv = *reinterpret_cast<const uint4*>(wf + (kh * 3 + kw) * Cin);
-          acc[0] += sv * bf2f(wv.x & 0xFFFF); acc[1] += sv * bf2f(wv.x >> 16);
-          acc[2] += sv * bf2f(wv.y & 0xFFFF); acc[3] += sv * bf2f(wv.y >> 16);
-          acc[4] += sv * bf2f(wv.z & 0xFFFF); acc[5] += sv * bf2f(wv.z >> 16);
-          acc[6] += sv * bf2f(wv.w & 0xFFFF); acc[7] += sv * bf2f(wv.w >> 16);
-        }
+      for (int t = 0; t < 9; ++t) {
+        acc[0] += sv[t] * bf2f(wv[t].x & 0xFFFF); acc[1] += sv[t] * bf2f(wv[t].x >> 16);
+        acc[2] += sv[t] * bf2f(wv[t].y & 0xFFFF); acc[3] += sv[t] * bf2f(wv[t].y >> 16);
+        acc[4] += sv[t] * bf2f(wv[t].z & 0xFFFF); acc[5] += sv[t] * bf2f(wv[t].z >> 16);
+        acc[6] += sv[t] * bf2f(wv[t].w & 0xFFFF); acc[7] += sv[t] * bf2f(wv[t].w >> 16);
       }
     }
     uint4 o;
@@ -160,11 +162,62 @@ __global__ void __launch_bounds__(256) seed_deconv3x3_kernel(const float* __rest
   }
 }
 
+// One workgroup per signal b for small maps (H*W <= 4096, e.g. block5's 14^2): the map S[b] is staged in
+// LDS once, each thread keeps its chunk's 9 weight vectors in registers and walks the pixels (a group of
+// Cin/8 lanes per pixel: 1 KiB coalesced stores at Cin = 512), so the per-pixel traffic is one LDS
+// broadcast per tap instead of 9 weight rows from L1. Same taps in the same order as the kernel above.
+constexpr int kSeedMaxHW = 4096;
+__global__ void __launch_bounds__(256) seed_deconv3x3_smallmap_kernel(const float* __restrict__ S,
+                                                                      const int* __restrict__ f,
+                                                                      const uint16_t* __restrict__ wt,
+                                                                      uint16_t* __restrict__ out, int H, int W,
+                                                                      int Cin, int F) {
+  __shared__ float Ss[kSeedMaxHW];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int hw = H * W, cpp = Cin >> 3, groups = 256 / cpp;
+  const int chunk = t % cpp, grp = t / cpp;
+  const int fb = min(f[b], F - 1);
+  const float* Sb = S + (size_t)b * hw;
+  for (int i = t; i < hw; i += 256) Ss[i] = Sb[i];
+  uint4 wv[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+    wv[k] = fb >= 0 ? *reinterpret_cast<const uint4*>(wt + ((size_t)fb * 9 + k) * Cin + chunk * 8) : make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  if (grp >= groups) return;
+  uint16_t* ob = out + (size_t)b * hw * Cin + chunk * 8;
+  for (int pix = grp; pix < hw; pix += groups) {
+    const int h = pix / W, w = pix - (pix / W) * W;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (fb >= 0) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int ih = h + k / 3 - 1, iw = w + k % 3 - 1;
+        const float sv = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? Ss[ih * W + iw] : 0.f;
+        acc[0] += sv * bf2f(wv[k].x & 0xFFFF); acc[1] += sv * bf2f(wv[k].x >> 16);
+        acc[2] += sv * bf2f(wv[k].y & 0xFFFF); acc[3] += sv * bf2f(wv[k].y >> 16);
+        acc[4] += sv * bf2f(wv[k].z & 0xFFFF); acc[5] += sv * bf2f(wv[k].z >> 16);
+        acc[6] += sv * bf2f(wv[k].w & 0xFFFF); acc[7] += sv * bf2f(wv[k].w >> 16);
+      }
+    }
+    uint4 o;
+    o.x = pack_bf2(fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f));
+    o.y = pack_bf2(fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
+    o.z = pack_bf2(fmaxf(acc[4], 0.f), fmaxf(acc[5], 0.f));
+    o.w = pack_bf2(fmaxf(acc[6], 0.f), fmaxf(acc[7], 0.f));
+    *reinterpret_cast<uint4*>(ob + (size_t)pix * Cin) = o;
+  }
+}
+
 int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint16_t* out, int B, int H,
                           int W, int Cin, int F, hipStream_t s) {
   if (Cin % 8 != 0 || B <= 0 || F <= 0) return -1;
   const long long total = (long long)B * H * W * (Cin / 8);
   if (total >= (1LL << 31) || (long long)F * 9 * Cin >= (1LL << 31)) return -2;
+  if ((long long)H * W <= kSeedMaxHW && Cin / 8 <= 256 && std::getenv("DV_SEED_V1") == nullptr) {
+    hipLaunchKernelGGL(seed_deconv3x3_smallmap_kernel, dim3((unsigned)B), dim3(256), 0, s, S, f, wt, out, H, W, Cin, F);
+    return (int)hipGetLastError();
+  }
   const long long blocks = std::min<long long>((total + 255) / 256, 256LL * 16);
   hipLaunchKernelGGL(seed_deconv3x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, S, f, wt, out, B, H,
                      W, Cin, F);

@@ -41,6 +41,9 @@ DECONV_SPLIT_MIN = int(os.environ.get("DV_DECONV_SPLIT_MIN", "64"))
 # expand the unpool themselves (64: block1_conv2.down's fused tail; 128 adds block2_conv2.down on the
 # hs16 unpool path, which also needs DV_HSU=1); wider consumers get the map from the producer's epilogue
 UNPOOL_CONSUMER_MAXC = int(os.environ.get("DV_UNPOOL_CONSUMER_MAXC", "64"))
+# DV_POOL_SPLIT=name,...: these convs run WITHOUT the fused pool epilogue (plain conv, which may take the
+# persistent KW3P kernel, then the standalone 2x2 max-pool/switch kernel) on the GPU
+POOL_SPLIT = frozenset(n for n in os.environ.get("DV_POOL_SPLIT", "").split(",") if n)
 
 
 class UnknownLayerError(KeyError):
@@ -125,7 +128,8 @@ class DeconvNet:
                         st.codes[seq[i + 2].name] = code
                         i += 3
                         continue
-                if fuse_pools and not keep_all and nxt is not None and nxt.kind == "pool":
+                if (fuse_pools and not keep_all and nxt is not None and nxt.kind == "pool" and
+                        not (x.is_cuda and s.name in POOL_SPLIT)):
                     x, code = ops.conv2d(x, cl.fwd, relu=True, epilogue="pool")
                     st.codes[nxt.name] = code
                     i += 2

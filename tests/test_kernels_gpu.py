@@ -599,6 +599,18 @@ def test_seed_deconv(native_lib):
     gb = ops.seed_deconv3x3(Sb.to(DEV), fb.to(DEV), wt.to(DEV))
     for i in (0, 511, 1023):
         assert _rel(gb[i:i + 1], ops.seed_deconv3x3(Sb[i:i + 1], fb[i:i + 1], wt)) < 1e-2
+    # the one-workgroup-per-signal small-map kernel (default at <= 4096 px) == the grid-stride kernel
+    os.environ["DV_SEED_V1"] = "1"
+    try:
+        g1 = ops.seed_deconv3x3(Sb.to(DEV), fb.to(DEV), wt.to(DEV))
+        w64 = wt[..., :64].contiguous()
+        h1 = ops.seed_deconv3x3(S.to(DEV), f.to(DEV), w64.to(DEV))
+    finally:
+        del os.environ["DV_SEED_V1"]
+    # (same taps in the same order; the compilers' FMA contraction differs between the two bodies, so
+    # a value may differ in its last bf16 bit)
+    assert _rel(g1, gb) < 4e-3
+    assert _rel(h1, ops.seed_deconv3x3(S.to(DEV), f.to(DEV), w64.to(DEV))) < 4e-3  # Cin 64: 32 pixel groups
 
 
 @pytest.mark.parametrize("pool", [False, True])

@@ -8,4 +8,8 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 for i in 1 2 3; do timeout -k 10 200 python bench.py > $O/bench_$i.log 2>&1 || exit 3; done
 timeout -k 10 300 python bench_dream.py --model inception_v3 --batch 64 --size 299 > $O/dream_c3.log 2>&1 || exit 4
 timeout -k 10 300 python bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 8 --dtype fp16 > $O/dream_c5.log 2>&1 || exit 5
-echo done
+echo validated
+# config-2 kernel trace of the validated tree (summaries are copied into profiles/ by hand)
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_final -o bench -- python3 bench.py --steps 5 --warmup 2 > $O/prof.log 2>&1 || exit 6
+echo profiled
