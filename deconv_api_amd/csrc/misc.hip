@@ -644,9 +644,59 @@ __global__ void __launch_bounds__(256) maxpool2x2_kernel(const uint16_t* __restr
   }
 }
 
+// Vectorized form (C % 8 == 0, 16-B aligned rows): one thread per (pooled pixel, 8-channel chunk), four
+// 16-B window loads, one 16-B value store and one 8-B code store; 32-bit index math. The same first-max
+// rule per channel as the scalar kernel (strict > over the window in (0,0), (0,1), (1,0), (1,1) order).
+__global__ void __launch_bounds__(256) maxpool2x2_vec_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out,
+                                                             uint8_t* __restrict__ code, int N, int H, int W, int C) {
+  const unsigned PH = H >> 1, PW = W >> 1, cpp = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * PH * PW * cpp;
+  for (unsigned g = blockIdx.x * 256u + threadIdx.x; g < total; g += gridDim.x * 256u) {
+    const unsigned pix = g / cpp, ch = g - pix * cpp;
+    const unsigned pw = pix % PW, t = pix / PW;
+    const unsigned ph = t % PH, n = t / PH;
+    const uint16_t* x0 = x + ((size_t)(n * H + 2 * ph) * W + 2 * pw) * C + ch * 8;
+    uint4 v[4];
+    v[0] = *reinterpret_cast<const uint4*>(x0);
+    v[1] = *reinterpret_cast<const uint4*>(x0 + C);
+    v[2] = *reinterpret_cast<const uint4*>(x0 + (size_t)W * C);
+    v[3] = *reinterpret_cast<const uint4*>(x0 + (size_t)W * C + C);
+    uint32_t ob[4], cb[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float best = -INFINITY;
+      uint32_t bc = 0, bits = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t wd = (&v[r].x)[e >> 1];
+        const uint32_t h16 = (e & 1) ? (wd >> 16) : (wd & 0xFFFFu);
+        const float f = bf2f(h16);
+        if (f > best) {
+          best = f;
+          bc = r;
+          bits = h16;
+        }
+      }
+      if (bc == 0 && !(best > -INFINITY)) bits = f2bf(best);  // nothing beat -inf: the scalar kernel's f2bf(-inf)
+      if (e & 1) ob[e >> 1] |= bits << 16;
+      else ob[e >> 1] = bits;
+      cb[e >> 2] |= bc << (8 * (e & 3));
+    }
+    *reinterpret_cast<uint4*>(out + (size_t)pix * C + ch * 8) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+    *reinterpret_cast<uint2*>(code + (size_t)pix * C + ch * 8) = make_uint2(cb[0], cb[1]);
+  }
+}
+
 int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C, hipStream_t s) {
   if ((H | W) & 1) return -1;
   const long long total = (long long)N * (H / 2) * (W / 2) * C;
+  if (C % 8 == 0 && total / 8 < (1LL << 31) && (long long)N * H * W * C < (1LL << 32) &&
+      !(reinterpret_cast<uintptr_t>(x) & 15) && !(reinterpret_cast<uintptr_t>(out) & 15) &&
+      !(reinterpret_cast<uintptr_t>(code) & 7)) {
+    const long long blocks = std::min<long long>((total / 8 + 255) / 256, 256LL * 32);
+    hipLaunchKernelGGL(maxpool2x2_vec_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
+    return (int)hipGetLastError();
+  }
   const long long blocks = std::min<long long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(maxpool2x2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
   return (int)hipGetLastError();

@@ -686,6 +686,13 @@ def test_pool_unpool_standalone(native_lib):
     v, c = ops.maxpool2x2(x.to(DEV))
     rv, rc = ops.maxpool2x2(x)
     assert torch.equal(v.cpu(), rv) and torch.equal(c.cpu(), rc)
+    # signed values, -inf windows and a 256-channel map (vectorized kernel), and C = 12 (scalar kernel)
+    for shape in ((3, 28, 28, 256), (2, 6, 8, 12)):
+        y = torch.randn(*shape, generator=g).to(torch.bfloat16)
+        y[0, :2, :2] = float("-inf")
+        yv, yc = ops.maxpool2x2(y.to(DEV))
+        ry, rcy = ops.maxpool2x2(y)
+        assert torch.equal(yv.cpu(), ry) and torch.equal(yc.cpu(), rcy), shape
     p = torch.randn(4, 6, 5, 64, generator=g).to(torch.bfloat16)
     u = ops.unpool2x2(p.to(DEV), c, code_div=2, relu=True)
     assert torch.equal(u.cpu(), ops.unpool2x2(p, c.cpu(), code_div=2, relu=True))
