@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-end validation in one gpurun call: GPU suite, smoke, config-2 bench (default vs DV_POOL_SPLIT
-# pairs), configs 3 and 5, then a config-2 kernel trace (summaries are copied into profiles/ by hand)
+# pairs), then a config-2 kernel trace (summaries are copied into profiles/ by hand)
 set -o pipefail
 O=gpurun_out/final2
 mkdir -p $O
@@ -10,9 +10,7 @@ for i in 1 2; do
   timeout -k 10 200 python bench.py > $O/bench_$i.log 2>&1 || exit 3
   DV_POOL_SPLIT=block3_conv3,block4_conv3 timeout -k 10 200 python bench.py > $O/bench_split_$i.log 2>&1 || exit 3
 done
-timeout -k 10 300 python bench_dream.py --model inception_v3 --batch 64 --size 299 > $O/dream_c3.log 2>&1 || exit 4
-timeout -k 10 300 python bench_dream.py --model resnet50 --size 1024 --tile 512 --batch 8 --dtype fp16 > $O/dream_c5.log 2>&1 || exit 5
 echo validated
 export TMPDIR=/tmp
-DV_POOL_SPLIT=block3_conv3,block4_conv3 timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_final2 -o bench -- python3 bench.py --steps 5 --warmup 2 > $O/prof.log 2>&1 || exit 6
+timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_final2 -o bench -- python3 bench.py --steps 5 --warmup 2 > $O/prof.log 2>&1 || exit 6
 echo profiled
