@@ -360,6 +360,8 @@ def main(argv=None):
     pdist.barrier(info)
     sync()
     elapsed = time.perf_counter() - t_start
+    if cuda:  # outside the clock: no stream-K tile of the timed steps was finished without its partner
+        ops.conv.check_stream_k()
     elapsed = pdist.all_reduce_max(elapsed, info)
     if cuda:
         per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))

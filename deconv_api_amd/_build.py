@@ -6,13 +6,21 @@ headers; both are linked into ``deconv_api_amd/_C<EXT_SUFFIX>`` next to this fil
 shared object travels with the source tree to the GPU box. The HIP runtime is resolved to the
 one torch already loaded (same soname ``libamdhip64.so.7``).
 
+Provenance: the build embeds ``source_hash()`` (sha256 over every ``csrc`` file's bytes plus the
+compile flags) into the binding as the string ``DV_SOURCE_HASH:<hex>`` (``_C.source_hash()``).
+``ops/native.py`` recomputes it from the tree before importing and refuses a binary built from
+other sources (``DV_AUTOBUILD=1``: rebuilds instead), so a GPU run can not silently use a stale
+``_C`` pushed with a newer tree.
+
 Usage: ``python -m deconv_api_amd._build [--force] [-j N] [--debug]``.
 """
 from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -25,6 +33,34 @@ BUILD = PKG.parent / "build" / "native"
 ARCH = os.environ.get("DV_OFFLOAD_ARCH", "gfx950")
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 TARGET = PKG / f"_C{EXT}"
+
+
+def _flags(debug: bool) -> list:
+    return (["-O1", "-g"] if debug else ["-O3"]), (["-DDV_DEBUG=1"] if debug else [])
+
+
+def source_hash(debug: bool = False) -> str:
+    """sha256 of the native sources (file names + bytes, sorted) and the flags they compile with."""
+    h = hashlib.sha256()
+    opt, defs = _flags(debug)
+    h.update(" ".join([ARCH, *opt, *defs]).encode())
+    for p in sorted(CSRC.iterdir()):
+        if p.suffix in (".hip", ".h", ".cpp"):
+            h.update(p.name.encode() + b"\0")
+            h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+_HASH_RE = re.compile(rb"DV_SOURCE_HASH:([0-9a-f]{64})")
+
+
+def embedded_hash(so: Path = TARGET):
+    """The hash a built ``_C`` carries (read from the file, without loading it); None if absent."""
+    try:
+        m = _HASH_RE.search(Path(so).read_bytes())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
 
 
 def _torch_paths():
@@ -64,8 +100,10 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     inc, libdirs = _torch_paths()
     headers = sorted(CSRC.glob("*.h"))
     hip_srcs = sorted(CSRC.glob("*.hip"))
-    opt = ["-O1", "-g"] if debug else ["-O3"]
-    defs = ["-DDV_DEBUG=1"] if debug else []
+    opt, defs = _flags(debug)
+    shash = source_hash(debug)
+    stamp = bdir / "source_hash.txt"
+    stale_hash = not stamp.exists() or stamp.read_text().strip() != shash
     hipcc = _hipcc()
     objs = []
     tasks = []
@@ -86,9 +124,10 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     bsrc = CSRC / "bindings.cpp"
     bobj = bdir / "bindings.o"
     objs.append(bobj)
-    if force or _newer([bsrc, *headers], bobj):
+    if force or stale_hash or _newer([bsrc, *headers], bobj):
         py_inc = sysconfig.get_paths()["include"]
-        tasks.append(["g++", *opt, *defs, "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+        tasks.append(["g++", *opt, *defs, f"-DDV_SOURCE_HASH=\"{shash}\"", "-fPIC", "-std=c++17",
+                      "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                       "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C", "-D_GLIBCXX_USE_CXX11_ABI=1",
                       *[f"-I{p}" for p in inc], f"-I{py_inc}", f"-I{CSRC}", "-c", str(bsrc), "-o", str(bobj)])
     if tasks:
@@ -105,6 +144,7 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
         link += [f"-Wl,-rpath,{torch_lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
                  "-ltorch_hip", "-lamdhip64", "-pthread"]
         _run(link)
+    stamp.write_text(shash + "\n")
     return TARGET
 
 

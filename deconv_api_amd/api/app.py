@@ -111,6 +111,11 @@ def create_app(service=None, cfg: Optional[Config] = None, dream_service=None) -
             except Exception as e:  # noqa: BLE001
                 from ..serve.service import ServiceOverloaded
 
+                code = getattr(e, "status", None)  # serve/frontend.py RemoteError: the GPU owner's answer
+                if isinstance(code, int) and code != 500:
+                    status = str(code)
+                    return JSONResponse(status_code=code, content={"detail": str(e)})
+
                 if isinstance(e, ServiceOverloaded):
                     status = "503"
                     return JSONResponse(status_code=503, content={"detail": str(e)})
@@ -135,12 +140,14 @@ def create_app(service=None, cfg: Optional[Config] = None, dream_service=None) -
 
     @app.get("/metrics")
     def metrics():
-        return PlainTextResponse(M.REGISTRY.render(), media_type="text/plain; version=0.0.4")
+        svc = state["service"]
+        # a front-end process (serve/frontend.py) adds its GPU owner's batch / GPU-stage series
+        txt = svc.metrics_text() if hasattr(svc, "metrics_text") else M.REGISTRY.render()
+        return PlainTextResponse(txt, media_type="text/plain; version=0.0.4")
 
     @app.get("/layers")
     def layers():
-        svc = get_service()
-        return {"layers": [s.name for s in svc.engine.specs[1:]]}
+        return {"layers": get_service().layer_names()}
 
     @app.post("/deepdream", openapi_extra=_FORM_SCHEMA)
     async def deepdream(request: Request):
@@ -169,7 +176,11 @@ def create_app(service=None, cfg: Optional[Config] = None, dream_service=None) -
             except (ImageDecodeError, ValueError) as e:
                 status = "400"
                 return JSONResponse(status_code=400, content={"detail": str(e)})
-            except Exception:  # noqa: BLE001
+            except Exception as e:  # noqa: BLE001
+                code = getattr(e, "status", None)  # RemoteError from the GPU owner (front-end mode)
+                if isinstance(code, int) and code != 500:
+                    status = str(code)
+                    return JSONResponse(status_code=code, content={"detail": str(e)})
                 status = "500"
                 log.exception("deepdream request failed")
                 return JSONResponse(status_code=500, content={"detail": "internal error"})

@@ -21,17 +21,21 @@ def _env(name: str, default, cast):
     return cast(v)
 
 
+DTYPES = ("bf16", "fp16", "fp32")
+
+
 @dataclass(frozen=True)
 class Config:
-    model: str = "vgg16"                  # reference: vgg16.VGG16 (app/main.py:17)
-    weights: str = ""                     # path to .safetensors/.pt/.h5; empty = seeded random init
+    weights: str = ""                     # VGG16 (app/main.py:17) .safetensors/.pt/.h5; empty = seeded random init
     seed: int = 0
-    dtype: str = "bf16"
+    dtype: str = "bf16"                   # GPU engine storage dtype: bf16 | fp16 (MFMA, fp32 accumulate);
+                                          #   fp32 is the CPU engine's (the oracle); fp32 on a GPU is refused
     device: str = "auto"                  # auto | cuda | cpu
     image_size: int = 224                 # app/main.py:53
     filters: int = 4                      # tiles in the mosaic (app/main.py:67-69)
-    top: int = 8                          # find_top_filters default (app/deepdream.py:369)
     mode: str = "all"                     # visualize_mode (app/main.py:64)
+    frontends: int = 4                    # serve/launch.py: HTTP front-end processes per rank (serve/ingest.py);
+                                          #   0 = uvicorn inside the GPU process (multi-rank: rank 0 shards batches)
     jpeg_quality: int = 95                # OpenCV imencode default (app/main.py:73)
     # request batcher. Sweep at 128 in-process clients (profiles/latency_r3_batch_sweep.txt):
     # 16 / 2 ms 2858 req/s (p50 41 ms) vs 64 / 2 ms 1989 (p50 59 ms) - small batches keep more of
@@ -72,6 +76,28 @@ class Config:
             kw[f.name] = _env("DV_" + f.name.upper(), f.default, cast)
         kw.update(overrides)
         return cls(**kw)
+
+    def __post_init__(self):
+        if self.dtype not in DTYPES:
+            raise ValueError(f"DV_DTYPE must be one of {DTYPES}, got {self.dtype!r}")
+        if self.mode not in ("all", "max"):
+            raise ValueError(f"DV_MODE must be 'all' or 'max', got {self.mode!r}")
+        if not 1 <= self.filters <= 4:
+            raise ValueError("DV_FILTERS must be 1..4 (tiles of the 2x2 mosaic)")
+        if self.frontends < 0:
+            raise ValueError("DV_FRONTENDS must be >= 0")
+
+    def torch_dtype(self, device):
+        """Engine dtype on ``device``: the MFMA kernels run bf16 or fp16 storage; the CPU engine is
+        the fp32 PyTorch oracle whatever ``dtype`` says."""
+        import torch
+
+        if torch.device(device).type != "cuda":
+            return torch.float32
+        if self.dtype == "fp32":
+            raise ValueError("DV_DTYPE=fp32 is not served on the GPU: the deconvnet kernels are bf16 / fp16 "
+                             "MFMA with fp32 accumulation (the fp32 path is the CPU engine, DV_DEVICE=cpu)")
+        return torch.float16 if self.dtype == "fp16" else torch.bfloat16
 
     def resolve_device(self) -> str:
         if self.device != "auto":

@@ -35,6 +35,9 @@ void need(const Tensor& t, int64_t bytes, const char* name) {
               avail_bytes(t), " are available");
 }
 
+static bool is16(const Tensor& t) { return t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf; }
+static int f16(const Tensor& t) { return t.scalar_type() == at::kHalf ? 1 : 0; }
+
 void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " launch failed with code ", rc);
 }
@@ -100,6 +103,30 @@ int64_t conv_group_end() {
   return launches;
 }
 
+// KW3P stream-K hand-off timeouts (conv_dma_impl.h): one process-wide counter in host-coherent pinned
+// memory, written by the kernel with a system-scope atomic, read by the host without any copy or sync
+static unsigned* sk_error_host() {
+  static unsigned* p = [] {
+    void* h = nullptr;
+    check_rc((int)hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc(sk errors)");
+    std::memset(h, 0, 64);
+    return reinterpret_cast<unsigned*>(h);
+  }();
+  return p;
+}
+static unsigned* sk_error_counter() {
+  unsigned* h = sk_error_host();
+  void* d = nullptr;
+  check_rc((int)hipHostGetDevicePointer(&d, h, 0), "hipHostGetDevicePointer(sk errors)");
+  return reinterpret_cast<unsigned*>(d);
+}
+int64_t sk_errors(bool reset) {
+  volatile unsigned* h = sk_error_host();
+  const unsigned v = *h;
+  if (reset) *h = 0u;
+  return (int64_t)v;
+}
+
 // compute units of the current device (cached per device)
 int64_t device_cus() {
   static std::mutex mu;
@@ -143,8 +170,9 @@ int64_t conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::op
   const auto dt = x.scalar_type();
   TORCH_CHECK((dt == at::kBFloat16 || dt == at::kHalf) && w.scalar_type() == dt, "conv: x, w must both be bf16 or fp16");
   a.dtype = dt == at::kHalf ? dv::DT_F16 : dv::DT_BF16;
-  TORCH_CHECK(a.dtype == dv::DT_BF16 || (epi == dv::CONV_E_BF16 && amode != dv::CONV_A_UNPOOL),
-              "conv: fp16 supports forward / transpose with a 16-bit output");
+  // fp16 (DeepDream, Config.dtype = fp16): the bf16-only kernels (weight-resident halo, pool v3, c8 stream,
+  // stem, tail) decline it and the launch lands on the dtype-generic DMA / halo-stream / pw kernels; an
+  // unpool input is materialized by the (16-bit move) unpool2x2 first. A combination no kernel has raises.
   TORCH_CHECK(w.is_contiguous() && w.numel() == (int64_t)a.OCpad * a.Kpad, "conv: w must be [OCpad, Kpad]");
   TORCH_CHECK(a.K == a.KH * a.KW * a.C && a.Kpad >= a.K && a.Kpad % 64 == 0, "conv: bad K/Kpad");
   TORCH_CHECK(a.C % 8 == 0 && a.x_ld % 8 == 0 && a.x_ld >= a.C, "conv: C and x_ld must be multiples of 8");
@@ -486,6 +514,8 @@ int64_t conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::op
       skws = at::empty({cus * dv::kSkSlotFloats + cus}, x.options().dtype(at::kFloat));
       a.skw = skws.data_ptr<float>();
       a.skflag = reinterpret_cast<unsigned*>(a.skw + cus * dv::kSkSlotFloats);
+      a.skslots = (int)cus;
+      a.skerr = sk_error_counter();
     }
     check_rc(dv::conv_dma_launch(a, (int)amode, (int)epi, cur_stream()), "conv_dma");
     if (ks > 1) check_rc(dv::splitk_reduce_launch(a, (int)epi, cur_stream()), "splitk_reduce");
@@ -973,6 +1003,39 @@ py::bytes data_url_b64decode(py::str uri) {
   return py::bytes(out);
 }
 
+// urllib.parse.unquote_plus of an ASCII str up to the final UTF-8 decode (the caller's): '+' -> ' ', %XX ->
+// byte XX, anything else (a '%' without two hex digits too) verbatim. GIL released: a percent-encoded
+// ~180 KB data URL has thousands of escapes, which urllib walks in a Python loop (api/forms.py).
+py::bytes url_unquote_plus(py::str s) {
+  PyObject* o = s.ptr();
+  if (!PyUnicode_IS_ASCII(o)) throw py::type_error("url_unquote_plus: ASCII text only");
+  Py_ssize_t n = 0;
+  const char* p = PyUnicode_AsUTF8AndSize(o, &n);
+  if (p == nullptr) throw py::error_already_set();
+  std::string out;
+  {
+    py::gil_scoped_release nogil;
+    out.resize((size_t)n);
+    auto hex = [](char c) -> int {
+      return c >= '0' && c <= '9' ? c - '0' : (c >= 'a' && c <= 'f' ? c - 'a' + 10 : (c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1));
+    };
+    size_t j = 0;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      const char c = p[i];
+      if (c == '+') {
+        out[j++] = ' ';
+      } else if (c == '%' && i + 2 < n && hex(p[i + 1]) >= 0 && hex(p[i + 2]) >= 0) {
+        out[j++] = (char)(hex(p[i + 1]) * 16 + hex(p[i + 2]));
+        i += 2;
+      } else {
+        out[j++] = c;
+      }
+    }
+    out.resize(j);
+  }
+  return py::bytes(out);
+}
+
 py::bytes jpeg_gpu_header(int64_t H, int64_t W, int64_t quality) {
   return py::bytes(dvjpeg::jpeg_header((int)H, (int)W, (int)quality, 1));
 }
@@ -1036,12 +1099,12 @@ void softmax_rows(Tensor x, Tensor y) {
 void channel_sum(Tensor x, Tensor sums, int64_t N, int64_t HW, int64_t C) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "channel_sum: x bf16 contiguous");
+  TORCH_CHECK(is16(x) && x.is_contiguous(), "channel_sum: x bf16 / fp16 contiguous");
   TORCH_CHECK(sums.scalar_type() == at::kFloat && sums.is_contiguous(), "channel_sum: sums fp32");
   need(x, N * HW * C * 2, "x");
   need(sums, N * C * 4, "sums");
   check_rc(dv::channel_sum_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()), sums.data_ptr<float>(), (int)N,
-                                  (int)HW, (int)C, cur_stream()),
+                                  (int)HW, (int)C, f16(x), cur_stream()),
            "channel_sum");
 }
 
@@ -1062,7 +1125,7 @@ void topk_pos(Tensor v, Tensor idx, Tensor val, int64_t k) {
 void seed_map(Tensor out4, Tensor idx, c10::optional<Tensor> code, Tensor S, int64_t mode) {
   check_cuda(out4, "out4");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(out4.device());
-  TORCH_CHECK(out4.dim() == 4 && out4.is_contiguous() && out4.scalar_type() == at::kBFloat16, "seed_map: out4 bf16 NHWC");
+  TORCH_CHECK(out4.dim() == 4 && out4.is_contiguous() && is16(out4), "seed_map: out4 bf16 / fp16 NHWC");
   TORCH_CHECK(idx.dim() == 2 && idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.size(0) == out4.size(0),
               "seed_map: idx int32 [B, K]");
   const int64_t B = out4.size(0), H = out4.size(1), W = out4.size(2), C = out4.size(3), K = idx.size(1);
@@ -1079,7 +1142,7 @@ void seed_map(Tensor out4, Tensor idx, c10::optional<Tensor> code, Tensor S, int
   }
   check_rc(dv::seed_map_launch(reinterpret_cast<const uint16_t*>(out4.data_ptr()), idx.data_ptr<int>(), cp,
                                S.data_ptr<float>(), (int)(B * K), (int)K, (int)H, (int)W, (int)C, (int)mode,
-                               cur_stream()),
+                               f16(out4), cur_stream()),
            "seed_map");
 }
 
@@ -1089,17 +1152,16 @@ void seed_deconv3x3(Tensor S, Tensor f, Tensor wt, Tensor out) {
   TORCH_CHECK(S.dim() == 3 && S.scalar_type() == at::kFloat && S.is_contiguous(), "seed: S [B,H,W] fp32");
   const int64_t B = S.size(0), H = S.size(1), W = S.size(2);
   TORCH_CHECK(f.scalar_type() == at::kInt && f.numel() == B && f.is_contiguous(), "seed: f [B] int32");
-  TORCH_CHECK(wt.dim() == 4 && wt.size(1) == 3 && wt.size(2) == 3 && wt.scalar_type() == at::kBFloat16 &&
-                  wt.is_contiguous(),
-              "seed: wt [F,3,3,Cin] bf16");
+  TORCH_CHECK(wt.dim() == 4 && wt.size(1) == 3 && wt.size(2) == 3 && is16(wt) && wt.is_contiguous(),
+              "seed: wt [F,3,3,Cin] bf16 / fp16");
   const int64_t Cin = wt.size(3);
-  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == B * H * W * Cin,
-              "seed: out [B,H,W,Cin] bf16");
+  TORCH_CHECK(out.scalar_type() == wt.scalar_type() && out.is_contiguous() && out.numel() == B * H * W * Cin,
+              "seed: out [B,H,W,Cin] of wt's dtype");
   // f values >= F are clamped to F - 1 in the kernel; < 0 gives a zero map
   check_rc(dv::seed_deconv3x3_launch(S.data_ptr<float>(), f.data_ptr<int>(),
                                      reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                                      reinterpret_cast<uint16_t*>(out.data_ptr()), (int)B, (int)H, (int)W, (int)Cin,
-                                     (int)wt.size(0), cur_stream()),
+                                     (int)wt.size(0), f16(wt), cur_stream()),
            "seed_deconv3x3");
 }
 
@@ -1151,11 +1213,12 @@ void resize_batch(Tensor blob, Tensor table, Tensor out, int64_t max_end) {
               "resize_batch: table int64 [B, 4]");
   TORCH_CHECK(out.dim() == 4 && out.is_contiguous() && out.size(0) == table.size(0), "resize_batch: out [B, OH, OW, C]");
   const bool u8 = out.scalar_type() == at::kByte;
-  TORCH_CHECK(u8 ? out.size(3) == 3 : (out.scalar_type() == at::kBFloat16 && out.size(3) >= 3 &&
+  const bool f16 = out.scalar_type() == at::kHalf;
+  TORCH_CHECK(u8 ? out.size(3) == 3 : ((out.scalar_type() == at::kBFloat16 || f16) && out.size(3) >= 3 &&
                                        reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0),
-              "resize_batch: out u8 [..., 3] or bf16 [..., Cpad]");
+              "resize_batch: out u8 [..., 3] or bf16 / fp16 [..., Cpad]");
   check_rc(dv::resize_batch_launch(blob.data_ptr<uint8_t>(), reinterpret_cast<const long long*>(table.data_ptr<int64_t>()), (int)table.size(0), out.data_ptr(),
-                                   (int)out.size(1), (int)out.size(2), (int)out.size(3), u8 ? 1 : 0, cur_stream()),
+                                   (int)out.size(1), (int)out.size(2), (int)out.size(3), u8 ? 1 : (f16 ? 2 : 0), cur_stream()),
            "resize_batch");
 }
 
@@ -1164,12 +1227,13 @@ void preprocess_u8(Tensor in, Tensor out) {
   c10::hip::HIPGuardMasqueradingAsCUDA guard(in.device());
   TORCH_CHECK(in.scalar_type() == at::kByte && in.is_contiguous() && in.dim() == 4 && in.size(3) == 3,
               "preprocess_u8: in u8 [B, H, W, 3]");
-  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.dim() == 4 && out.size(0) == in.size(0) &&
-                  out.size(1) == in.size(1) && out.size(2) == in.size(2) && out.size(3) >= 3 &&
-                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
-              "preprocess_u8: out bf16 [B, H, W, Cpad]");
+  const bool f16 = out.scalar_type() == at::kHalf;
+  TORCH_CHECK((out.scalar_type() == at::kBFloat16 || f16) && out.is_contiguous() && out.dim() == 4 &&
+                  out.size(0) == in.size(0) && out.size(1) == in.size(1) && out.size(2) == in.size(2) &&
+                  out.size(3) >= 3 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "preprocess_u8: out bf16 / fp16 [B, H, W, Cpad]");
   check_rc(dv::preprocess_u8_launch(in.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(out.data_ptr()),
-                                    in.numel() / 3, (int)out.size(3), cur_stream()),
+                                    in.numel() / 3, (int)out.size(3), f16 ? 1 : 0, cur_stream()),
            "preprocess_u8");
 }
 
@@ -1178,8 +1242,10 @@ void resize_preprocess(Tensor img, Tensor out, int64_t mode) {
   c10::hip::HIPGuardMasqueradingAsCUDA guard(img.device());
   TORCH_CHECK(img.dim() == 4 && img.size(3) == 3 && img.scalar_type() == at::kByte && img.is_contiguous(),
               "resize_preprocess: img [B, H, W, 3] u8");
-  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.size(0) == img.size(0),
-              "resize_preprocess: out [B, OH, OW, Cpad] bf16");
+  const bool f16 = out.scalar_type() == at::kHalf;
+  TORCH_CHECK(out.dim() == 4 && (out.scalar_type() == at::kBFloat16 || f16) && out.is_contiguous() &&
+                  out.size(0) == img.size(0),
+              "resize_preprocess: out [B, OH, OW, Cpad] bf16 / fp16");
   const int64_t B = img.size(0), Hs = img.size(1), Ws = img.size(2), OH = out.size(1), OW = out.size(2),
                 Cp = out.size(3);
   if (mode == 1) TORCH_CHECK(Hs == 2 * OH && Ws == 2 * OW, "area mode needs exact 2x");
@@ -1187,7 +1253,7 @@ void resize_preprocess(Tensor img, Tensor out, int64_t mode) {
   TORCH_CHECK(Cp >= 3 && (Cp != 8 || reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0), "resize_preprocess: Cpad");
   check_rc(dv::resize_preprocess_launch(img.data_ptr<uint8_t>(), (int)B, (int)Hs, (int)Ws,
                                         reinterpret_cast<uint16_t*>(out.data_ptr()), (int)OH, (int)OW, (int)Cp,
-                                        (int)mode, cur_stream()),
+                                        (int)mode, f16 ? 1 : 0, cur_stream()),
            "resize_preprocess");
 }
 
@@ -1310,23 +1376,24 @@ void zsum3x3(Tensor z, Tensor out, c10::optional<Tensor> stats, int64_t stats_di
 void maxpool2x2(Tensor x, Tensor out, Tensor code) {
   check_cuda(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "maxpool: x NHWC bf16");
+  TORCH_CHECK(x.dim() == 4 && is16(x) && x.is_contiguous(), "maxpool: x NHWC bf16 / fp16");
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == N * (H / 2) * (W / 2) * C,
+  TORCH_CHECK(out.scalar_type() == x.scalar_type() && out.is_contiguous() && out.numel() == N * (H / 2) * (W / 2) * C,
               "maxpool: out");
   TORCH_CHECK(code.scalar_type() == at::kByte && code.is_contiguous() && code.numel() == out.numel(), "maxpool: code");
   check_rc(dv::maxpool2x2_launch(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                  reinterpret_cast<uint16_t*>(out.data_ptr()), code.data_ptr<uint8_t>(), (int)N, (int)H,
-                                 (int)W, (int)C, cur_stream()),
+                                 (int)W, (int)C, f16(x), cur_stream()),
            "maxpool2x2");
 }
 
 void unpool2x2(Tensor p, Tensor code, Tensor out, int64_t code_div, bool relu) {
   check_cuda(p, "p");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
-  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16 && out.is_contiguous(), "unpool: out NHWC bf16");
+  // 16-bit moves + a sign-bit ReLU: the same kernel for bf16 and fp16
+  TORCH_CHECK(out.dim() == 4 && is16(out) && out.is_contiguous(), "unpool: out NHWC bf16 / fp16");
   const int64_t N = out.size(0), H = out.size(1), W = out.size(2), C = out.size(3);
-  TORCH_CHECK(p.scalar_type() == at::kBFloat16 && p.is_contiguous() && p.numel() == N * (H / 2) * (W / 2) * C,
+  TORCH_CHECK(p.scalar_type() == out.scalar_type() && p.is_contiguous() && p.numel() == N * (H / 2) * (W / 2) * C,
               "unpool: p");
   TORCH_CHECK(code_div >= 1 && N % code_div == 0, "unpool: code_div");
   TORCH_CHECK(code.scalar_type() == at::kByte && code.is_contiguous() && code.numel() == p.numel() / code_div,
@@ -1340,7 +1407,17 @@ void unpool2x2(Tensor p, Tensor code, Tensor out, int64_t code_div, bool relu) {
 
 }  // namespace
 
+// build provenance (_build.py): sha256 of the csrc tree + compile flags, found in the file by
+// ops/native.py before it loads this module
+#ifndef DV_SOURCE_HASH
+#define DV_SOURCE_HASH "unknown"
+#endif
+static const char kSourceHash[] = "DV_SOURCE_HASH:" DV_SOURCE_HASH;
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("source_hash", [] { return std::string(kSourceHash + 15); }, "sha256 of the sources this binary was built from");
+  m.def("sk_errors", &sk_errors, py::arg("reset") = false,
+        "KW3P stream-K hand-offs that timed out since the last reset (their tiles are wrong)");
   m.doc() = "deconv_api_amd gfx950 (MI355X) HIP kernels";
   m.def("conv", &conv, "MFMA implicit-GEMM conv (fwd / unpool-gather / transposed; bf16/pool/f32 epilogues)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("out_code"), py::arg("code"),
@@ -1380,6 +1457,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("paced_copy", &paced_copy, "bench: CU-occupying copy paced to a link bandwidth (all-gather interference model)");
   m.def("jpeg_gpu", &jpeg_gpu, "GPU baseline JPEG scans of uint8 [B,H,W,3] (restart per MCU row)");
   m.def("data_url_b64decode", &data_url_b64decode, "data URL payload -> bytes (lenient base64, GIL released)");
+  m.def("url_unquote_plus", &url_unquote_plus, "unquote_plus of an ASCII str -> bytes (GIL released)");
   m.def("jpeg_gpu_header", &jpeg_gpu_header, "SOI..SOS of the GPU encoder's streams");
   m.def("jpeg_gpu_max_width", &dv::jpeg_gpu_max_width, "widest image the GPU encoder takes");
   m.def("jpeg_gpu_data_urls", &jpeg_gpu_data_urls, "GPU scans -> data URLs (host base64, GIL released)");

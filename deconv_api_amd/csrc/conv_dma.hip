@@ -100,8 +100,10 @@ int conv_dma_launch(const ConvArgs& a, int amode, int epi, hipStream_t s) {
                                : dma_mask_bn<DT_BF16, CONV_A_TRANSPOSE>(a, s);
     return -1;
   }
-  if (a.dtype == DT_F16) {  // DeepDream fp16 path (BASELINE config 5): forward + dgrad
+  if (a.dtype == DT_F16) {  // DeepDream fp16 (BASELINE config 5) + the fp16 deconvnet (Config.dtype)
     if (amode == CONV_A_FWD && epi == CONV_E_BF16) return dma_run_f16_fwd(a, s);
+    if (amode == CONV_A_FWD && epi == CONV_E_POOL) return dma_run_f16_fwd_pool(a, s);
+    if (amode == CONV_A_FWD && epi == CONV_E_F32) return dma_run_f16_fwd_f32(a, s);
     if (amode == CONV_A_TRANSPOSE && epi == CONV_E_BF16) return dma_run_f16_tr(a, s);
     return -1;
   }

@@ -1451,11 +1451,19 @@ __global__ void __launch_bounds__(512) conv_dma_kw3p_kernel(const ConvArgs a, in
       if (ck1 < nsteps) {  // head piece (this range's last segment): add the tail's partial, then the epilogue
         const int src = (slot + tiles_n) % (int)gridDim.x;  // the next workgroup of this column group
         if (tid == 0) {
-          // bounded poll (~seconds): a lost hand-off must not hang the GPU (it would corrupt this tile)
+          // bounded poll (~1 s): a lost hand-off must not hang the GPU. A timeout (the producer never
+          // became resident, e.g. every other CU held by kernels of other streams that spin on peers)
+          // leaves this tile wrong, so it is COUNTED in host-coherent memory and the host raises
+          // (bindings.cpp sk_errors(), checked after each serving batch / bench / test)
+          bool ok = false;
           for (int it = 0; it < (1 << 22); ++it) {
-            if (__hip_atomic_load(a.skflag + src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) break;
+            if (__hip_atomic_load(a.skflag + src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+              ok = true;
+              break;
+            }
             __builtin_amdgcn_s_sleep(8);
           }
+          if (!ok && a.skerr != nullptr) __hip_atomic_fetch_add(a.skerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load moves above the poll
         __syncthreads();
@@ -1684,7 +1692,7 @@ static bool kw3_sk_ok(const ConvArgs& a, int BM, int BN) {
   // (DV_KW3_SK=all: every eligible grid, A/B; read per launch)
   const char* ska = std::getenv("DV_KW3_SK");
   const long long max_tiles = ska && std::strcmp(ska, "all") == 0 ? (1LL << 40) : 4LL * G;
-  return G <= kSkMaxWg && (long long)BM * BN <= kSkSlotFloats && tiles_n >= 1 && G % tiles_n == 0 &&
+  return G <= kSkMaxWg && G <= a.skslots && (long long)BM * BN <= kSkSlotFloats && tiles_n >= 1 && G % tiles_n == 0 &&
          tiles_m * tiles_n > G && tiles_m * tiles_n < max_tiles && tiles_m >= G / tiles_n &&
          tiles_m * (3LL * a.C / 32) < (1LL << 31);
 }
@@ -1989,6 +1997,8 @@ int dma_run_bf16_fwd_pool(const ConvArgs& a, hipStream_t s);
 int dma_run_bf16_fwd_f32(const ConvArgs& a, hipStream_t s);
 int dma_run_bf16_tr(const ConvArgs& a, hipStream_t s);
 int dma_run_f16_fwd(const ConvArgs& a, hipStream_t s);
+int dma_run_f16_fwd_pool(const ConvArgs& a, hipStream_t s);
+int dma_run_f16_fwd_f32(const ConvArgs& a, hipStream_t s);
 int dma_run_f16_tr(const ConvArgs& a, hipStream_t s);
 
 }  // namespace dv

@@ -70,6 +70,8 @@ struct ConvArgs {
                           //   the transposed pooled-max epilogue (conv_dma_impl.h:epilogue_pool_t)
   float* skw;             // optional: KW3P stream-K workspace, kSkSlotFloats fp32 per workgroup (partial tiles)
   unsigned* skflag;       //   + one ready flag per workgroup; zeroed by the launcher before each launch
+  int skslots;            //   workspace slots (workgroups) allocated: the launch needs G <= skslots
+  unsigned* skerr;        //   host-coherent counter of hand-offs that timed out (bindings.cpp sk_errors())
   // 1-bit ReLU masks (LDS-staged epilogue only; host: OC % 8 == 0): bit c % 8 of byte c / 8 of row m.
   // obits: written with the output, bit = (stored 16-bit value > 0); ebits: replaces emask (read 1/16
   // of its bytes). The launcher sets them only on kernels whose epilogue is epilogue_lds (conv_pw).
@@ -120,13 +122,13 @@ int stem_conv_dgrad_launch(const uint16_t* gy, const float* w, uint16_t* gx, int
 int conv_pw_launch(const ConvArgs& a, hipStream_t stream);
 
 // ---- misc kernels (misc.hip) ----
-// per-(image, channel) sums of a NHWC bf16 tensor: sums[n][c] = sum_{hw} x[n][hw][c]
-int channel_sum_launch(const uint16_t* x, float* sums, int N, int HW, int C, hipStream_t s);
+// per-(image, channel) sums of a NHWC bf16 / fp16 (f16 = 1) tensor: sums[n][c] = sum_{hw} x[n][hw][c]
+int channel_sum_launch(const uint16_t* x, float* sums, int N, int HW, int C, int f16, hipStream_t s);
 // per-row stable top-k of positive values: idx[n][k] (-1 when fewer than k positives)
 int topk_pos_launch(const float* v, int* idx, float* val, int N, int C, int k, hipStream_t s);
 // one-channel seeded deconv: out[b][h][w][ci] = relu(sum_taps S[b][h+kh-1][w+kw-1] * wt[f_b][kh][kw][ci])
 int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint16_t* out,
-                          int B, int H, int W, int Cin, int F, hipStream_t s);
+                          int B, int H, int W, int Cin, int F, int f16, hipStream_t s);
 // fp32 recon [B*4][224][224][3] -> u8 mosaic [B][448][448][3] (channel-reversed), Keras deprocess
 int deprocess_mosaic_launch(const float* recon, uint8_t* out, int B, int H, int W, int tiles,
                             int reverse_channels, hipStream_t s);
@@ -135,18 +137,20 @@ int recon_stats_launch(const float* x, double* stats, long long per_group, int g
 // deprocess with precomputed per-image stats (single pass, 4 px per thread); W % 4 == 0
 int deprocess_apply_launch(const float* recon, const double* stats, uint8_t* out, int B, int H, int W, int tiles,
                            int reverse_channels, hipStream_t s);
-// uint8 [B][Hs][Ws][3] RGB -> bf16 NHWC [B][OH][OW][Cpad]: cv2 INTER_LINEAR resize + caffe mean subtract
+// uint8 [B][Hs][Ws][3] RGB -> bf16 / fp16 (f16 = 1) NHWC [B][OH][OW][Cpad]: cv2 INTER_LINEAR resize +
+// caffe mean subtract
 int resize_preprocess_launch(const uint8_t* img, int B, int Hs, int Ws, uint16_t* out, int OH, int OW,
-                             int Cpad, int mode, hipStream_t s);
+                             int Cpad, int mode, int f16, hipStream_t s);
+// fmt: 0 bf16 preprocessed, 1 u8 resized RGB, 2 fp16 preprocessed
 int resize_batch_launch(const uint8_t* blob, const long long* table, int B, void* out, int OH, int OW, int Cpad,
-                        int out_u8, hipStream_t s);
-int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad, hipStream_t s);
+                        int fmt, hipStream_t s);
+int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad, int f16, hipStream_t s);
 // standalone 2x2/s2 max pool with switch codes, and its inverse (unpool scatter to full res)
 int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C,
-                      hipStream_t s);
+                      int f16, hipStream_t s);
 // seed maps of the deconvnet's B*K chains (all / max mode, optional max-unpool for pool targets)
 int seed_map_launch(const uint16_t* out4, const int* idx, const uint8_t* code, float* S, int BK, int K, int H, int W,
-                    int C, int mode, hipStream_t s);
+                    int C, int mode, int f16, hipStream_t s);
 int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int N, int H, int W,
                      int C, int code_div, int relu, hipStream_t s);
 

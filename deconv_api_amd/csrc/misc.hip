@@ -13,6 +13,7 @@ namespace dv {
 // each filter's activation map; here per image, fp32 accumulate of the stored bf16 map).
 // One block per image; each thread owns 8 channels (one 16-B chunk) of a pixel group.
 // ---------------------------------------------------------------------------------------
+template <int DT>
 __global__ void __launch_bounds__(256) channel_sum_kernel(const uint16_t* __restrict__ x,
                                                           float* __restrict__ sums, int HW, int C) {
   __shared__ float red[256 * 8];
@@ -26,10 +27,10 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const uint16_t* __rest
     const uint16_t* base = x + (long long)n * HW * C + chunk * 8;
     for (int p = grp; p < HW; p += groups) {
       const uint4 v = *reinterpret_cast<const uint4*>(base + (long long)p * C);
-      acc[0] += bf2f(v.x & 0xFFFF); acc[1] += bf2f(v.x >> 16);
-      acc[2] += bf2f(v.y & 0xFFFF); acc[3] += bf2f(v.y >> 16);
-      acc[4] += bf2f(v.z & 0xFFFF); acc[5] += bf2f(v.z >> 16);
-      acc[6] += bf2f(v.w & 0xFFFF); acc[7] += bf2f(v.w >> 16);
+      acc[0] += to_f<DT>(v.x & 0xFFFF); acc[1] += to_f<DT>(v.x >> 16);
+      acc[2] += to_f<DT>(v.y & 0xFFFF); acc[3] += to_f<DT>(v.y >> 16);
+      acc[4] += to_f<DT>(v.z & 0xFFFF); acc[5] += to_f<DT>(v.z >> 16);
+      acc[6] += to_f<DT>(v.w & 0xFFFF); acc[7] += to_f<DT>(v.w >> 16);
     }
   }
 #pragma unroll
@@ -44,9 +45,10 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const uint16_t* __rest
   }
 }
 
-int channel_sum_launch(const uint16_t* x, float* sums, int N, int HW, int C, hipStream_t s) {
+int channel_sum_launch(const uint16_t* x, float* sums, int N, int HW, int C, int f16, hipStream_t s) {
   if (C % 8 != 0 || C > 2048 || N <= 0) return -1;
-  hipLaunchKernelGGL(channel_sum_kernel, dim3(N), dim3(256), 0, s, x, sums, HW, C);
+  if (f16) hipLaunchKernelGGL(channel_sum_kernel<DT_F16>, dim3(N), dim3(256), 0, s, x, sums, HW, C);
+  else hipLaunchKernelGGL(channel_sum_kernel<DT_BF16>, dim3(N), dim3(256), 0, s, x, sums, HW, C);
   return (int)hipGetLastError();
 }
 
@@ -114,6 +116,7 @@ int topk_pos_launch(const float* v, int* idx, float* val, int N, int C, int k, h
 // f_b is clamped to [-1, F) here (one ALU op; the host no longer runs a clamp launch). Index math is
 // 32-bit (the launcher checks B*H*W*Cin/8 < 2^31): the 64-bit div/mod chain per 16-B chunk made this
 // memory-bound kernel ALU-bound (141 us for 205 MB at block5, profiles/kseq_c2_r5.txt).
+template <int DT>
 __global__ void __launch_bounds__(256) seed_deconv3x3_kernel(const float* __restrict__ S,
                                                              const int* __restrict__ f,
                                                              const uint16_t* __restrict__ wt,
@@ -147,17 +150,17 @@ __global__ void __launch_bounds__(256) seed_deconv3x3_kernel(const float* __rest
       }
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        acc[0] += sv[t] * bf2f(wv[t].x & 0xFFFF); acc[1] += sv[t] * bf2f(wv[t].x >> 16);
-        acc[2] += sv[t] * bf2f(wv[t].y & 0xFFFF); acc[3] += sv[t] * bf2f(wv[t].y >> 16);
-        acc[4] += sv[t] * bf2f(wv[t].z & 0xFFFF); acc[5] += sv[t] * bf2f(wv[t].z >> 16);
-        acc[6] += sv[t] * bf2f(wv[t].w & 0xFFFF); acc[7] += sv[t] * bf2f(wv[t].w >> 16);
+        acc[0] += sv[t] * to_f<DT>(wv[t].x & 0xFFFF); acc[1] += sv[t] * to_f<DT>(wv[t].x >> 16);
+        acc[2] += sv[t] * to_f<DT>(wv[t].y & 0xFFFF); acc[3] += sv[t] * to_f<DT>(wv[t].y >> 16);
+        acc[4] += sv[t] * to_f<DT>(wv[t].z & 0xFFFF); acc[5] += sv[t] * to_f<DT>(wv[t].z >> 16);
+        acc[6] += sv[t] * to_f<DT>(wv[t].w & 0xFFFF); acc[7] += sv[t] * to_f<DT>(wv[t].w >> 16);
       }
     }
     uint4 o;
-    o.x = pack_bf2(fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f));
-    o.y = pack_bf2(fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
-    o.z = pack_bf2(fmaxf(acc[4], 0.f), fmaxf(acc[5], 0.f));
-    o.w = pack_bf2(fmaxf(acc[6], 0.f), fmaxf(acc[7], 0.f));
+    o.x = pack2<DT>(fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f));
+    o.y = pack2<DT>(fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
+    o.z = pack2<DT>(fmaxf(acc[4], 0.f), fmaxf(acc[5], 0.f));
+    o.w = pack2<DT>(fmaxf(acc[6], 0.f), fmaxf(acc[7], 0.f));
     *reinterpret_cast<uint4*>(out + (size_t)g * 8) = o;
   }
 }
@@ -167,6 +170,7 @@ __global__ void __launch_bounds__(256) seed_deconv3x3_kernel(const float* __rest
 // Cin/8 lanes per pixel: 1 KiB coalesced stores at Cin = 512), so the per-pixel traffic is one LDS
 // broadcast per tap instead of 9 weight rows from L1. Same taps in the same order as the kernel above.
 constexpr int kSeedMaxHW = 4096;
+template <int DT>
 __global__ void __launch_bounds__(256) seed_deconv3x3_smallmap_kernel(const float* __restrict__ S,
                                                                       const int* __restrict__ f,
                                                                       const uint16_t* __restrict__ wt,
@@ -194,33 +198,42 @@ __global__ void __launch_bounds__(256) seed_deconv3x3_smallmap_kernel(const floa
       for (int k = 0; k < 9; ++k) {
         const int ih = h + k / 3 - 1, iw = w + k % 3 - 1;
         const float sv = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? Ss[ih * W + iw] : 0.f;
-        acc[0] += sv * bf2f(wv[k].x & 0xFFFF); acc[1] += sv * bf2f(wv[k].x >> 16);
-        acc[2] += sv * bf2f(wv[k].y & 0xFFFF); acc[3] += sv * bf2f(wv[k].y >> 16);
-        acc[4] += sv * bf2f(wv[k].z & 0xFFFF); acc[5] += sv * bf2f(wv[k].z >> 16);
-        acc[6] += sv * bf2f(wv[k].w & 0xFFFF); acc[7] += sv * bf2f(wv[k].w >> 16);
+        acc[0] += sv * to_f<DT>(wv[k].x & 0xFFFF); acc[1] += sv * to_f<DT>(wv[k].x >> 16);
+        acc[2] += sv * to_f<DT>(wv[k].y & 0xFFFF); acc[3] += sv * to_f<DT>(wv[k].y >> 16);
+        acc[4] += sv * to_f<DT>(wv[k].z & 0xFFFF); acc[5] += sv * to_f<DT>(wv[k].z >> 16);
+        acc[6] += sv * to_f<DT>(wv[k].w & 0xFFFF); acc[7] += sv * to_f<DT>(wv[k].w >> 16);
       }
     }
     uint4 o;
-    o.x = pack_bf2(fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f));
-    o.y = pack_bf2(fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
-    o.z = pack_bf2(fmaxf(acc[4], 0.f), fmaxf(acc[5], 0.f));
-    o.w = pack_bf2(fmaxf(acc[6], 0.f), fmaxf(acc[7], 0.f));
+    o.x = pack2<DT>(fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f));
+    o.y = pack2<DT>(fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f));
+    o.z = pack2<DT>(fmaxf(acc[4], 0.f), fmaxf(acc[5], 0.f));
+    o.w = pack2<DT>(fmaxf(acc[6], 0.f), fmaxf(acc[7], 0.f));
     *reinterpret_cast<uint4*>(ob + (size_t)pix * Cin) = o;
   }
 }
 
 int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint16_t* out, int B, int H,
-                          int W, int Cin, int F, hipStream_t s) {
+                          int W, int Cin, int F, int f16, hipStream_t s) {
   if (Cin % 8 != 0 || B <= 0 || F <= 0) return -1;
   const long long total = (long long)B * H * W * (Cin / 8);
   if (total >= (1LL << 31) || (long long)F * 9 * Cin >= (1LL << 31)) return -2;
   if ((long long)H * W <= kSeedMaxHW && Cin / 8 <= 256 && std::getenv("DV_SEED_V1") == nullptr) {
-    hipLaunchKernelGGL(seed_deconv3x3_smallmap_kernel, dim3((unsigned)B), dim3(256), 0, s, S, f, wt, out, H, W, Cin, F);
+    if (f16)
+      hipLaunchKernelGGL(seed_deconv3x3_smallmap_kernel<DT_F16>, dim3((unsigned)B), dim3(256), 0, s, S, f, wt, out, H, W,
+                         Cin, F);
+    else
+      hipLaunchKernelGGL(seed_deconv3x3_smallmap_kernel<DT_BF16>, dim3((unsigned)B), dim3(256), 0, s, S, f, wt, out, H,
+                         W, Cin, F);
     return (int)hipGetLastError();
   }
   const long long blocks = std::min<long long>((total + 255) / 256, 256LL * 16);
-  hipLaunchKernelGGL(seed_deconv3x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, S, f, wt, out, B, H,
-                     W, Cin, F);
+  if (f16)
+    hipLaunchKernelGGL(seed_deconv3x3_kernel<DT_F16>, dim3((unsigned)blocks), dim3(256), 0, s, S, f, wt, out, B, H, W,
+                       Cin, F);
+  else
+    hipLaunchKernelGGL(seed_deconv3x3_kernel<DT_BF16>, dim3((unsigned)blocks), dim3(256), 0, s, S, f, wt, out, B, H, W,
+                       Cin, F);
   return (int)hipGetLastError();
 }
 
@@ -230,6 +243,7 @@ int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint
 // top-k where all images share the filter); idx >= C reads as -1. With `code` (a max-pool target) the map is
 // max-unpooled to [2H, 2W] with that pool's switch codes and clamped at 0 (the seed of the conv
 // below the pool). One workgroup per chain: the 'max' reduction stays in the block.
+template <int DT>
 __global__ void __launch_bounds__(256) seed_map_kernel(const uint16_t* __restrict__ out4, const int* __restrict__ idx,
                                                        const uint8_t* __restrict__ code, float* __restrict__ S, int K,
                                                        int H, int W, int C, int mode) {
@@ -244,7 +258,7 @@ __global__ void __launch_bounds__(256) seed_map_kernel(const uint16_t* __restric
     const int b0 = mode == 2 ? 0 : b, b1 = mode == 2 ? (int)gridDim.x / K : b + 1;
     for (int bb = b0; bb < b1; ++bb) {
       const uint16_t* o2 = out4 + (long long)bb * HW * C;
-      for (int p = threadIdx.x; p < HW; p += 256) m = fmaxf(m, bf2f(o2[(long long)p * C + f]));
+      for (int p = threadIdx.x; p < HW; p += 256) m = fmaxf(m, to_f<DT>(o2[(long long)p * C + f]));
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
@@ -255,7 +269,7 @@ __global__ void __launch_bounds__(256) seed_map_kernel(const uint16_t* __restric
   if (code == nullptr) {
     float* Sb = S + (long long)bk * HW;
     for (int p = threadIdx.x; p < HW; p += 256) {
-      float v = f >= 0 ? bf2f(ob[(long long)p * C + f]) : 0.f;
+      float v = f >= 0 ? to_f<DT>(ob[(long long)p * C + f]) : 0.f;
       if (mode != 0 && v != m) v = 0.f;
       Sb[p] = v;
     }
@@ -269,7 +283,7 @@ __global__ void __launch_bounds__(256) seed_map_kernel(const uint16_t* __restric
     const long long p = (long long)(y >> 1) * W + (x >> 1);
     float v = 0.f;
     if (f >= 0 && cb[p * C + f] == (uint8_t)(((y & 1) << 1) | (x & 1))) {
-      v = bf2f(ob[p * C + f]);
+      v = to_f<DT>(ob[p * C + f]);
       if (mode != 0 && v != m) v = 0.f;
       v = fmaxf(v, 0.f);
     }
@@ -278,9 +292,12 @@ __global__ void __launch_bounds__(256) seed_map_kernel(const uint16_t* __restric
 }
 
 int seed_map_launch(const uint16_t* out4, const int* idx, const uint8_t* code, float* S, int BK, int K, int H, int W,
-                    int C, int mode, hipStream_t s) {
+                    int C, int mode, int f16, hipStream_t s) {
   if (BK <= 0 || K <= 0 || BK % K) return -1;
-  hipLaunchKernelGGL(seed_map_kernel, dim3((unsigned)BK), dim3(256), 0, s, out4, idx, code, S, K, H, W, C, mode);
+  if (f16)
+    hipLaunchKernelGGL(seed_map_kernel<DT_F16>, dim3((unsigned)BK), dim3(256), 0, s, out4, idx, code, S, K, H, W, C, mode);
+  else
+    hipLaunchKernelGGL(seed_map_kernel<DT_BF16>, dim3((unsigned)BK), dim3(256), 0, s, out4, idx, code, S, K, H, W, C, mode);
   return (int)hipGetLastError();
 }
 
@@ -532,85 +549,92 @@ __device__ __forceinline__ void resize_px(const uint8_t* __restrict__ img, int H
   }
 }
 
-// caffe preprocess of one pixel into Cpad 16-bit slots (slot c<3 = rgb[c] - mean[c], quirk Q1)
+// caffe preprocess of one pixel into Cpad 16-bit slots (slot c<3 = rgb[c] - mean[c], quirk Q1);
+// DT: the engine's storage dtype (bf16 or fp16, Config.dtype)
+template <int DT>
 __device__ __forceinline__ void store_pre(uint16_t* __restrict__ o, const int (&px)[3], int Cpad) {
   const float mean[3] = {103.939f, 116.779f, 123.68f};
   if (Cpad == 8) {  // one 16-B store per pixel
     uint4 v;
-    v.x = pack_bf2((float)px[0] - mean[0], (float)px[1] - mean[1]);
-    v.y = (uint32_t)f2bf((float)px[2] - mean[2]);
+    v.x = pack2<DT>((float)px[0] - mean[0], (float)px[1] - mean[1]);
+    v.y = (uint32_t)from_f<DT>((float)px[2] - mean[2]);
     v.z = 0u;
     v.w = 0u;
     *reinterpret_cast<uint4*>(o) = v;
   } else {
-    for (int c = 0; c < Cpad; ++c) o[c] = c < 3 ? f2bf((float)px[c] - mean[c]) : (uint16_t)0;
+    for (int c = 0; c < Cpad; ++c) o[c] = c < 3 ? from_f<DT>((float)px[c] - mean[c]) : (uint16_t)0;
   }
+}
+
+__device__ __forceinline__ void store_pre_dt(uint16_t* __restrict__ o, const int (&px)[3], int Cpad, int f16) {
+  if (f16) store_pre<DT_F16>(o, px, Cpad);
+  else store_pre<DT_BF16>(o, px, Cpad);
 }
 
 __global__ void __launch_bounds__(256) resize_preprocess_kernel(const uint8_t* __restrict__ img_b, int Hs, int Ws,
                                                                 uint16_t* __restrict__ out_b, int OH, int OW,
-                                                                int Cpad, int mode) {
+                                                                int Cpad, int mode, int f16) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= OH * OW) return;
   const uint8_t* img = img_b + (long long)blockIdx.y * Hs * Ws * 3;
   uint16_t* out = out_b + (long long)blockIdx.y * OH * OW * Cpad;
   int px[3];
   resize_px(img, Hs, Ws, OH, OW, p % OW, p / OW, mode, px);
-  store_pre(out + (long long)p * Cpad, px, Cpad);
+  store_pre_dt(out + (long long)p * Cpad, px, Cpad, f16);
 }
 
 int resize_preprocess_launch(const uint8_t* img, int B, int Hs, int Ws, uint16_t* out, int OH, int OW, int Cpad,
-                             int mode, hipStream_t s) {
+                             int mode, int f16, hipStream_t s) {
   if (Cpad < 3 || mode < 0 || mode > 2 || B <= 0) return -1;
   hipLaunchKernelGGL(resize_preprocess_kernel, dim3((OH * OW + 255) / 256, B), dim3(256), 0, s, img, Hs, Ws, out,
-                     OH, OW, Cpad, mode);
+                     OH, OW, Cpad, mode, f16);
   return (int)hipGetLastError();
 }
 
 // Whole request batch in ONE launch: images of any sizes packed back to back in one u8 blob (one
 // pinned staging slot, one H2D copy; runtime/staging.py), table[b] = {byte offset, Hs, Ws, mode}.
-// out_u8 == 0: preprocessed 16-bit [B, OH, OW, Cpad]; out_u8 == 1: resized RGB u8 [B, OH, OW, 3]
+// fmt 0 / 2: preprocessed bf16 / fp16 [B, OH, OW, Cpad]; fmt 1: resized RGB u8 [B, OH, OW, 3]
 // (the 150 KB/image form rank 0 scatters to the other GPUs; preprocess_u8 finishes it there).
 __global__ void __launch_bounds__(256) resize_batch_kernel(const uint8_t* __restrict__ blob,
                                                            const long long* __restrict__ table, void* __restrict__ out,
-                                                           int OH, int OW, int Cpad, int out_u8) {
+                                                           int OH, int OW, int Cpad, int fmt) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= OH * OW) return;
   const long long* t = table + (long long)blockIdx.y * 4;
   int px[3];
   resize_px(blob + t[0], (int)t[1], (int)t[2], OH, OW, p % OW, p / OW, (int)t[3], px);
   const long long pix = (long long)blockIdx.y * OH * OW + p;
-  if (out_u8) {
+  if (fmt == 1) {
     uint8_t* o = reinterpret_cast<uint8_t*>(out) + pix * 3;
     o[0] = (uint8_t)px[0];
     o[1] = (uint8_t)px[1];
     o[2] = (uint8_t)px[2];
   } else {
-    store_pre(reinterpret_cast<uint16_t*>(out) + pix * Cpad, px, Cpad);
+    store_pre_dt(reinterpret_cast<uint16_t*>(out) + pix * Cpad, px, Cpad, fmt == 2);
   }
 }
 
 int resize_batch_launch(const uint8_t* blob, const long long* table, int B, void* out, int OH, int OW, int Cpad,
-                        int out_u8, hipStream_t s) {
-  if (B <= 0 || B > 65535 || (!out_u8 && Cpad < 3)) return -1;
+                        int fmt, hipStream_t s) {
+  if (B <= 0 || B > 65535 || fmt < 0 || fmt > 2 || (fmt != 1 && Cpad < 3)) return -1;
   hipLaunchKernelGGL(resize_batch_kernel, dim3((OH * OW + 255) / 256, B), dim3(256), 0, s, blob, table, out, OH, OW,
-                     Cpad, out_u8);
+                     Cpad, fmt);
   return (int)hipGetLastError();
 }
 
 // resized RGB u8 [P pixels, 3] -> preprocessed 16-bit [P, Cpad] (the scattered shard on a rank)
 __global__ void __launch_bounds__(256) preprocess_u8_kernel(const uint8_t* __restrict__ in, uint16_t* __restrict__ out,
-                                                            long long P, int Cpad) {
+                                                            long long P, int Cpad, int f16) {
   for (long long p = blockIdx.x * 256LL + threadIdx.x; p < P; p += (long long)gridDim.x * 256) {
     const int px[3] = {in[p * 3], in[p * 3 + 1], in[p * 3 + 2]};
-    store_pre(out + p * Cpad, px, Cpad);
+    store_pre_dt(out + p * Cpad, px, Cpad, f16);
   }
 }
 
-int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad, hipStream_t s) {
+int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad, int f16, hipStream_t s) {
   if (P <= 0 || Cpad < 3) return -1;
   const unsigned grid = (unsigned)std::min<long long>((P + 255) / 256, 256LL * 32);
-  hipLaunchKernelGGL(preprocess_u8_kernel, dim3(grid), dim3(256), 0, s, in, out, P, Cpad);
+  hipLaunchKernelGGL(preprocess_u8_kernel, dim3(grid), dim3(256), 0, s, in, out, P, Cpad, f16);
   return (int)hipGetLastError();
 }
 
@@ -619,6 +643,7 @@ int preprocess_u8_launch(const uint8_t* in, uint16_t* out, long long P, int Cpad
 // and max-unpool to full resolution (reference: app/deepdream.py:191-209). The hot paths fuse
 // both into the conv kernel; these serve pool-layer targets and tests.
 // ---------------------------------------------------------------------------------------
+template <int DT>
 __global__ void __launch_bounds__(256) maxpool2x2_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out,
                                                          uint8_t* __restrict__ code, int N, int H, int W, int C) {
   const int PH = H >> 1, PW = W >> 1;
@@ -633,13 +658,13 @@ __global__ void __launch_bounds__(256) maxpool2x2_kernel(const uint16_t* __restr
     int bc = 0;
     for (int r = 0; r < 4; ++r) {
       const int ih = 2 * ph + (r >> 1), iw = 2 * pw + (r & 1);
-      const float v = bf2f(x[((n * H + ih) * W + iw) * C + c]);
+      const float v = to_f<DT>(x[((n * H + ih) * W + iw) * C + c]);
       if (v > best) {
         best = v;
         bc = r;
       }
     }
-    out[g] = f2bf(best);
+    out[g] = from_f<DT>(best);
     code[g] = (uint8_t)bc;
   }
 }
@@ -647,6 +672,7 @@ __global__ void __launch_bounds__(256) maxpool2x2_kernel(const uint16_t* __restr
 // Vectorized form (C % 8 == 0, 16-B aligned rows): one thread per (pooled pixel, 8-channel chunk), four
 // 16-B window loads, one 16-B value store and one 8-B code store; 32-bit index math. The same first-max
 // rule per channel as the scalar kernel (strict > over the window in (0,0), (0,1), (1,0), (1,1) order).
+template <int DT>
 __global__ void __launch_bounds__(256) maxpool2x2_vec_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out,
                                                              uint8_t* __restrict__ code, int N, int H, int W, int C) {
   const unsigned PH = H >> 1, PW = W >> 1, cpp = (unsigned)C >> 3;
@@ -670,14 +696,14 @@ __global__ void __launch_bounds__(256) maxpool2x2_vec_kernel(const uint16_t* __r
       for (int r = 0; r < 4; ++r) {
         const uint32_t wd = (&v[r].x)[e >> 1];
         const uint32_t h16 = (e & 1) ? (wd >> 16) : (wd & 0xFFFFu);
-        const float f = bf2f(h16);
+        const float f = to_f<DT>(h16);
         if (f > best) {
           best = f;
           bc = r;
           bits = h16;
         }
       }
-      if (bc == 0 && !(best > -INFINITY)) bits = f2bf(best);  // nothing beat -inf: the scalar kernel's f2bf(-inf)
+      if (bc == 0 && !(best > -INFINITY)) bits = from_f<DT>(best);  // nothing beat -inf: the scalar kernel's from_f<DT>(-inf)
       if (e & 1) ob[e >> 1] |= bits << 16;
       else ob[e >> 1] = bits;
       cb[e >> 2] |= bc << (8 * (e & 3));
@@ -687,18 +713,23 @@ __global__ void __launch_bounds__(256) maxpool2x2_vec_kernel(const uint16_t* __r
   }
 }
 
-int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C, hipStream_t s) {
+int maxpool2x2_launch(const uint16_t* x, uint16_t* out, uint8_t* code, int N, int H, int W, int C, int f16,
+                      hipStream_t s) {
   if ((H | W) & 1) return -1;
   const long long total = (long long)N * (H / 2) * (W / 2) * C;
   if (C % 8 == 0 && total / 8 < (1LL << 31) && (long long)N * H * W * C < (1LL << 32) &&
       !(reinterpret_cast<uintptr_t>(x) & 15) && !(reinterpret_cast<uintptr_t>(out) & 15) &&
       !(reinterpret_cast<uintptr_t>(code) & 7)) {
     const long long blocks = std::min<long long>((total / 8 + 255) / 256, 256LL * 32);
-    hipLaunchKernelGGL(maxpool2x2_vec_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
+    if (f16)
+      hipLaunchKernelGGL(maxpool2x2_vec_kernel<DT_F16>, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
+    else
+      hipLaunchKernelGGL(maxpool2x2_vec_kernel<DT_BF16>, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
     return (int)hipGetLastError();
   }
   const long long blocks = std::min<long long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(maxpool2x2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
+  if (f16) hipLaunchKernelGGL(maxpool2x2_kernel<DT_F16>, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
+  else hipLaunchKernelGGL(maxpool2x2_kernel<DT_BF16>, dim3((unsigned)blocks), dim3(256), 0, s, x, out, code, N, H, W, C);
   return (int)hipGetLastError();
 }
 

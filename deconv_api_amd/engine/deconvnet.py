@@ -183,6 +183,7 @@ class DeconvNet:
         out = st.outputs.get(layer, st.out) if layer != st.target else st.out
         f = idx.reshape(B * K).to(torch.int32)
         d: Optional[torch.Tensor] = None
+        seed_scale: Optional[torch.Tensor] = None  # fp16 dense seeds: per-chain scale of the reconstruction
         pending_code: Optional[torch.Tensor] = None
         j = li  # index of the layer whose down is applied next
         if spec.kind == "conv":
@@ -204,6 +205,12 @@ class DeconvNet:
                 # the reference's max runs over the batch axis of output[:, f] (:454-457)
                 v = v * (v == v.amax(dim=0, keepdim=True))
             v = v * (idx >= 0)
+            if dev.type == "cuda" and self.rt.dtype == torch.float16:
+                # fp16 (smallest subnormal 6e-8) cannot carry a softmax probability through the dense
+                # downs; the deconv chain is positively homogeneous (bias-free convs, ReLU, max-unpool),
+                # so it runs from a unit seed and the reconstruction is scaled by |v| at the end
+                seed_scale = v.abs().reshape(B * K)
+                v = torch.sign(v)
             seed = torch.zeros(B * K, units, device=dev, dtype=torch.float32)
             seed.scatter_(1, idx.reshape(B * K, 1).long().clamp_min(0), v.reshape(B * K, 1))
             d = seed
@@ -227,6 +234,8 @@ class DeconvNet:
             j -= 2  # skip flatten and block5_pool (its unpool is fused into block5_conv3's down)
         # ---- conv / pool downs to the input ----
         recon = None
+        if seed_scale is not None:  # the final conv's epilogue statistics would be of the unit-seed chains
+            stats_out, stats = stats, None
         while j >= 1:
             s = self.specs[j]
             if s.kind == "pool":
@@ -274,6 +283,11 @@ class DeconvNet:
             if stats is not None:  # no fp32 conv epilogue on this path: sums over each image's K maps
                 r = recon.reshape(B, -1).double()
                 stats.copy_(torch.stack([r.sum(1), (r * r).sum(1)], 1))
+        if seed_scale is not None:
+            recon = recon * seed_scale.view(-1, *([1] * (recon.dim() - 1)))
+            if stats_out is not None:
+                r = recon.reshape(B, -1).double()
+                stats_out.copy_(torch.stack([r.sum(1), (r * r).sum(1)], 1))
         return recon.reshape(B, K, *recon.shape[1:])
 
     # ------------------------------------------------------------------ one call

@@ -29,7 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from ..ops import native
-from ..runtime.capture import capture, drain_collective
+from ..runtime.capture import capture
 from ..utils.logging import get_logger
 from ..ops.autograd import loss_tap, premasked_grads, sumsq_core
 
@@ -442,6 +442,7 @@ class TiledDeepDream(DeepDream):
         # one hipGraph per octave shape for the whole tile forward/backward/stitch
         self.tile_graphs = use_graphs and self.device.type == "cuda"
         self._tgraphs: "OrderedDict[tuple, object]" = OrderedDict()
+        self._cgroup = None  # (default group id, process group of the captured all-gathers)
         self.tile_fused = FUSED_STEP and self.device.type == "cuda"
         # coll_wait(work): how an EAGER collective of the tiled step is waited for. None: a blocking
         # call. The multi-rank service sets a poll under its heartbeat / re-form deadlines
@@ -640,11 +641,27 @@ class TiledDeepDream(DeepDream):
         else:
             self.coll_wait(fn(*args, async_op=True))
 
-    def _gather_chunk(self, st, c: int):
+    def _gather_chunk(self, st, c: int, group=None):
         """Async all-gather of chunk c's packs (every rank's slot) -> the work object."""
         import torch.distributed as dist
 
-        return dist.all_gather_into_tensor(st.packs[c].view(-1), st.packs[c, st.rank], async_op=True)
+        return dist.all_gather_into_tensor(st.packs[c].view(-1), st.packs[c, st.rank], group=group, async_op=True)
+
+    def _capture_group(self):
+        """The process group the CAPTURED all-gathers run on: a second communicator over the same
+        ranks, connected eagerly at creation (bound device) and never used by an eager collective.
+        Its watchdog therefore never tracks a work, so it can not query an event of the stream an
+        octave capture has pulled in (the hipErrorCapturedEvent abort of round 3; the eager
+        collectives of the default group - weight broadcast, dream broadcast, deconv scatter /
+        gather - live on another stream). Created collectively: every rank reaches the first
+        captured octave of a world at the same command. Keyed on the default group, so a group
+        re-formed over the survivors gets a new one."""
+        import torch.distributed as dist
+
+        key = id(dist.distributed_c10d._get_default_group())
+        if self._cgroup is None or self._cgroup[0] != key:
+            self._cgroup = (key, dist.new_group(ranks=list(range(dist.get_world_size()))))
+        return self._cgroup[1]
 
     def _finish(self, work) -> None:
         if self.coll_wait is None:
@@ -657,6 +674,7 @@ class TiledDeepDream(DeepDream):
         and runs on the collective's stream while chunk c+1's network runs on this one; the update
         waits for every chunk's gather (captured as graph edges when ``capturing``)."""
         coll = self._collective(st)
+        group = self._capture_group() if coll and capturing else None
         ns = min(TILE_CHUNK_STREAMS, st.C)
         if ns > 1 and len(getattr(self, "_cstreams", ())) < ns:
             self._cstreams = [torch.cuda.Stream(self.device) for _ in range(ns)]
@@ -667,7 +685,7 @@ class TiledDeepDream(DeepDream):
                 for c, cs in enumerate(st.chunks):
                     self._tile_compute_chunk(st, cs, it, st.rank)
                     if coll:
-                        works.append(self._gather_chunk(st, c))
+                        works.append(self._gather_chunk(st, c, group))
             else:
                 # fork: chunk c on stream c % ns. Its all-gather is issued from THIS stream behind an event
                 # of the chunk (a collective issued from a forked capture stream is not seen as captured
@@ -684,7 +702,7 @@ class TiledDeepDream(DeepDream):
                 for c, ev in enumerate(done):
                     cur.wait_event(ev)
                     if coll:
-                        works.append(self._gather_chunk(st, c))
+                        works.append(self._gather_chunk(st, c, group))
             for w in works:
                 if capturing:
                     w.wait()  # recorded into the octave graph: nothing to poll here
@@ -775,14 +793,15 @@ class TiledDeepDream(DeepDream):
             # warm up on a side stream (autograd / allocator), restore the image, capture the octave
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
-            works = []
             with torch.cuda.stream(s):
                 self._tile_compute(st, 0)
-                if coll:  # the collective's communicator is set up outside the capture
-                    works = [self._gather_chunk(st, c) for c in range(st.C)]
             torch.cuda.current_stream(self.device).wait_stream(s)
-            for i, work in enumerate(works):  # retire the eager warm-up collectives before the capture opens
-                drain_collective(work, self.device, self.coll_wait, settle=i + 1 == len(works))
+            if coll and CAPTURE_COLLECTIVE:
+                # the captured all-gathers' communicator exists (eagerly connected) before the capture
+                # opens, and no eager collective ever runs on it (_capture_group): no warm-up
+                # collective, nothing for a watchdog to poll during the capture
+                self._capture_group()
+                torch.cuda.synchronize(self.device)
             if not coll or CAPTURE_COLLECTIVE:
                 # the whole octave, all-gathers included (RCCL collectives are graph-capturable):
                 # one replay per octave instead of `iterations` replays + eager collectives

@@ -33,7 +33,7 @@ class GraphedDeconv:
         self._lock = threading.Lock()
 
     def _capture(self, layer: str, B: int):
-        x = torch.zeros(B, self.S, self.S, 8, dtype=torch.bfloat16, device=self.device)
+        x = torch.zeros(B, self.S, self.S, 8, dtype=self.engine.rt.dtype, device=self.device)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

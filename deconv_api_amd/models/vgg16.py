@@ -159,12 +159,13 @@ class VGG16:
 
 class VGG16Runtime:
     """Weights packed for one device: per conv the forward GEMM matrix, the deconv GEMM matrix
-    and the seeded-first-step weights; per dense layer bf16 (device) kernels."""
+    and the seeded-first-step weights; per dense layer 16-bit (device) kernels. ``dtype``: the
+    device storage dtype, bf16 or fp16 (Config.dtype); CPU weights stay fp32."""
 
     def __init__(self, model: VGG16, device: torch.device, dtype: torch.dtype):
         self.model = model
         self.device = device
-        self.dtype = dtype if device.type == "cuda" else dtype
+        self.dtype = dtype
         self.specs = model.specs
         self.convs: Dict[str, ConvLayer] = {}
         self.dense: Dict[str, DenseLayer] = {}
@@ -177,7 +178,7 @@ class VGG16Runtime:
                 cin8 = w_oihw.shape[1]
                 seed = torch.zeros(s.cout, 3, 3, cin8)
                 seed[..., : s.cin] = k.flip(0, 1).permute(3, 0, 1, 2)  # [f, kh, kw, ci] = W[2-kh, 2-kw, ci, f]
-                self.convs[s.name] = ConvLayer(s, fwd.to_device(device), dec.to_device(device),
+                self.convs[s.name] = ConvLayer(s, fwd.to_device(device, dtype), dec.to_device(device, dtype),
                                                seed.to(device=device, dtype=dtype).contiguous())
             elif s.kind == "dense" and s.name in model.params:
                 k, b = model.params[s.name]

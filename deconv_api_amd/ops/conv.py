@@ -379,6 +379,16 @@ def conv_group_paused():
         lib.conv_group_pause(False)
 
 
+def check_stream_k() -> None:
+    """Raise if a KW3P stream-K hand-off timed out since the last check: its tile was finished
+    without the other half of its K range (conv_dma_impl.h; the counter lives in host-coherent
+    memory, so this costs one host load, no sync). Called after every serving batch and bench."""
+    n = native.lib().sk_errors(True)
+    if n:
+        raise RuntimeError(f"{n} KW3P stream-K hand-off(s) timed out: those conv output tiles are wrong "
+                           "(set DV_NO_KW3_SK=1 when other kernels hold the CUs for seconds)")
+
+
 _tls = threading.local()
 
 

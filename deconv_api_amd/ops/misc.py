@@ -76,7 +76,7 @@ def seed_map(out4: torch.Tensor, idx: torch.Tensor, mode: str = "all", batch_top
     B, H, W, C = out4.shape
     K = idx.shape[1]
     m = {"all": 0, "max": 2 if batch_topk == "global" else 1}[mode]
-    if out4.is_cuda and out4.dtype == torch.bfloat16:
+    if out4.is_cuda and out4.dtype in (torch.bfloat16, torch.float16):
         up = 1 if code is None else 2
         S = torch.empty(B * K, H * up, W * up, device=out4.device, dtype=torch.float32)
         native.lib().seed_map(out4.contiguous(), idx.to(torch.int32).contiguous(),

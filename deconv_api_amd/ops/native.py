@@ -15,16 +15,48 @@ _mod = None
 _err: Exception | None = None
 
 
+class StaleBinaryError(RuntimeError):
+    pass
+
+
+def check_provenance() -> str:
+    """The tree's source hash if the built ``_C`` carries the same one; raises StaleBinaryError
+    when it was built from other sources / flags (``_build.py``: provenance). A missing binary
+    passes here (the import reports it). ``DV_SKIP_PROVENANCE=1`` skips the check (tools that
+    load a scratch build on purpose)."""
+    from .. import _build
+
+    want = _build.source_hash()
+    if os.environ.get("DV_SKIP_PROVENANCE") == "1" or not _build.TARGET.exists():
+        return want
+    got = _build.embedded_hash(_build.TARGET)
+    if got != want:
+        raise StaleBinaryError(
+            f"deconv_api_amd/_C was built from other sources (embedded hash {got}, tree {want}); rebuild with "
+            "`python -m deconv_api_amd._build` (or set DV_AUTOBUILD=1)")
+    return want
+
+
 def load(build_if_missing: bool = False):
-    """Import ``deconv_api_amd._C``; optionally build it in-tree first."""
+    """Import ``deconv_api_amd._C`` after checking that it was built from this tree's sources;
+    optionally (re)build it in-tree first."""
     global _mod, _err
     with _lock:
         if _mod is not None:
             return _mod
+        autobuild = build_if_missing or os.environ.get("DV_AUTOBUILD", "0") == "1"
+        try:
+            check_provenance()
+        except StaleBinaryError:
+            if not autobuild:
+                raise
+            from .. import _build
+
+            _build.build()
         try:
             _mod = importlib.import_module("deconv_api_amd._C")
         except ImportError as e:  # pragma: no cover - depends on build state
-            if build_if_missing or os.environ.get("DV_AUTOBUILD", "0") == "1":
+            if autobuild:
                 from .. import _build
 
                 _build.build()

@@ -218,7 +218,8 @@ class ShardedRunner:
 
     def _preprocess(self, u8: torch.Tensor) -> torch.Tensor:
         if u8.is_cuda:
-            x = torch.empty(*u8.shape[:3], 8, dtype=torch.bfloat16, device=u8.device)
+            rt = getattr(self.engine, "rt", None)  # (test doubles have no runtime: bf16)
+            x = torch.empty(*u8.shape[:3], 8, dtype=rt.dtype if rt is not None else torch.bfloat16, device=u8.device)
             ops.native.lib().preprocess_u8(u8, x)
             return x
         return torch.stack([ops.preprocess_ref(u8[b].numpy(), 8, torch.float32) for b in range(u8.shape[0])]) \

@@ -1,16 +1,29 @@
-"""Server launcher: one process per GPU (reference: a single uvicorn worker, Dockerfile:15).
+"""Server launcher: one GPU-owner process per GPU (reference: a single uvicorn worker, Dockerfile:15).
 
     python -m torch.distributed.run --standalone --nproc-per-node 8 -m deconv_api_amd.serve.launch
     python -m deconv_api_amd.serve.launch            # single GPU / CPU
 
-Rank 0 creates (or loads) the VGG16 weights and broadcasts them over RCCL, then runs uvicorn
-with the batching service; every other rank builds the same engine on its GPU and serves rank
-0's shards (parallel/sharded.py) until shutdown.
+Rank 0 creates (or loads) the VGG16 weights and broadcasts them over RCCL; every rank builds the
+same engine on its GPU. Two serving layouts:
+
+  * ``DV_FRONTENDS=N`` (default 4): each rank starts N HTTP front-end processes (serve/frontend.py)
+    BEFORE touching its GPU, all bound to the port with SO_REUSEPORT, and serves what they decode
+    through an ``IngestServer`` (serve/ingest.py). Ranks are independent on the request path:
+    every rank parses, decodes, batches and encodes only its own front ends' requests, so HTTP
+    throughput scales with the ranks (no rank-0 decode / resize / scatter). ``/deepdream`` runs on
+    the receiving rank's GPU (tiled on that GPU above ``dream_tile``).
+  * ``DV_FRONTENDS=0``: rank 0 runs uvicorn in-process and shards every batch across the ranks
+    (parallel/sharded.py: scatter / gather, failover re-forming the group over the survivors,
+    ``/deepdream`` tiled across every rank); the followers serve rank 0's command stream.
 """
 from __future__ import annotations
 
 import argparse
 import os
+import signal
+import subprocess
+import sys
+import threading
 
 import torch
 
@@ -25,24 +38,80 @@ log = get_logger("deconv_api_amd.launch")
 
 
 def build_engine(cfg: Config, info: pdist.DistInfo) -> DeconvNet:
-    model = load_model(cfg) if info.is_main else load_model(Config(**{**cfg.__dict__, "seed": cfg.seed}))
+    model = load_model(cfg)
     if info.world > 1:
         sd = pdist.broadcast_state(model.state_dict(), info)
         model = type(model).from_state_dict(sd)
-    dtype = torch.bfloat16 if info.device.type == "cuda" else torch.float32
-    return DeconvNet(model.build(info.device, dtype))
+    return DeconvNet(model.build(info.device, cfg.torch_dtype(info.device)))
+
+
+def spawn_frontends(cfg: Config, path: str, n: int) -> list:
+    """Start ``n`` front-end processes for the ingest socket ``path``. Called before this process
+    initialises the GPU: the children are fresh interpreters that never open it."""
+    env = dict(os.environ, DV_HOST=cfg.host, DV_PORT=str(cfg.port))
+    return [subprocess.Popen([sys.executable, "-m", "deconv_api_amd.serve.frontend", "--sock", path,
+                              "--index", str(i)], env=env) for i in range(n)]
+
+
+def serve_frontends(cfg: Config, info: pdist.DistInfo, eng: DeconvNet, path: str, fes: list,
+                    stop: threading.Event) -> None:
+    """This rank's GPU owner: the batching service + /deepdream behind the ingest socket, until
+    ``stop`` is set or every front end has exited."""
+    from .dream_service import DreamService
+    from .ingest import IngestServer
+
+    svc = DeconvService(cfg, engine=eng)
+    dream = DreamService(cfg)
+    srv = IngestServer(path, svc, dream, rank=info.rank)
+    log.info("serving through front ends", extra={"fields": {"rank": info.rank, "world": info.world,
+                                                             "frontends": len(fes), "port": cfg.port}})
+    try:
+        while not stop.wait(0.5):
+            if fes and all(p.poll() is not None for p in fes):
+                log.error("every front end exited", extra={"fields": {"codes": [p.returncode for p in fes]}})
+                break
+    finally:
+        srv.close()
+        for p in fes:
+            if p.poll() is None:
+                p.terminate()
+        for p in fes:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        svc.close()
+        dream.close()
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--host", default=None)
     ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--frontends", type=int, default=None, help="HTTP front-end processes per rank (0: in-process)")
     a = ap.parse_args(argv)
-    overrides = {k: v for k, v in (("host", a.host), ("port", a.port)) if v is not None}
+    overrides = {k: v for k, v in (("host", a.host), ("port", a.port), ("frontends", a.frontends)) if v is not None}
     cfg = Config.from_env(**overrides)
     setup(cfg.log_json)
+    stop = threading.Event()
+    fes, path = [], None
+    if cfg.frontends > 0:
+        from .ingest import socket_path
+
+        # before pdist.init(): nothing that touches the GPU has run in this process yet
+        path = socket_path(cfg.port, int(os.environ.get("RANK", "0")))
+        fes = spawn_frontends(cfg, path, cfg.frontends)
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            signal.signal(sig, lambda *_: stop.set())
     info = pdist.init()
     eng = build_engine(cfg, info)
+    if cfg.frontends > 0:
+        try:
+            serve_frontends(cfg, info, eng, path, fes, stop)
+        finally:
+            if torch.distributed.is_initialized():  # ranks are independent here: no exit barrier
+                torch.distributed.destroy_process_group()
+        return
     runner = ShardedRunner(eng, info, cfg.image_size, cfg.filters, cfg.mode, cfg=cfg) if info.world > 1 else None
     if not info.is_main:
         n = runner.follow()

@@ -22,7 +22,7 @@ import queue
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Callable, List, Optional
 
 import numpy as np
 import torch
@@ -47,10 +47,12 @@ class ServiceOverloaded(RuntimeError):
 
 @dataclass
 class _Job:
+    """One request in the batcher. ``deliver(value, exc)`` hands the result back: for an HTTP
+    request of this process it completes an asyncio future on the request's loop, for a request
+    from a front-end process (serve/ingest.py) it writes the response to that front-end's socket."""
     layer: str
     image: np.ndarray
-    loop: asyncio.AbstractEventLoop
-    future: asyncio.Future
+    deliver: Callable[[object, Optional[BaseException]], None]
     t_enq: float = field(default_factory=time.perf_counter)
     t_launch: float = 0.0
     t_gpu: float = 0.0
@@ -85,8 +87,7 @@ class DeconvService:
             self.device = torch.device("cuda", torch.cuda.current_device())
         if engine is None:
             model = load_model(self.cfg)
-            dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
-            engine = DeconvNet(model.build(self.device, dtype))
+            engine = DeconvNet(model.build(self.device, self.cfg.torch_dtype(self.device)))
         self.engine = engine
         self.graphs = None
         self.ring = None
@@ -136,6 +137,21 @@ class DeconvService:
     def validate_layer(self, layer: str) -> None:
         self.engine._check_layer(layer)  # raises UnknownLayerError
 
+    def layer_names(self) -> List[str]:
+        return [s.name for s in self.engine.specs[1:]]
+
+    def submit(self, layer: str, img: np.ndarray, deliver) -> _Job:
+        """Enqueue an already decoded HxWx3 uint8 image; ``deliver(value, exc)`` is called from a
+        service thread with the response string (or the error). Raises at once for an unknown
+        layer or a full queue."""
+        self.validate_layer(layer)
+        if self.q.qsize() >= self.cfg.max_queue:
+            raise ServiceOverloaded("request queue is full")
+        job = _Job(layer, img, deliver)
+        self.q.put(job)
+        M.QUEUE_DEPTH.set(self.q.qsize())
+        return job
+
     async def deconv(self, uri: str, layer: str) -> str:
         """The reference's POST / pipeline for one request -> data URL string."""
         self.validate_layer(layer)
@@ -144,10 +160,10 @@ class DeconvService:
         loop = asyncio.get_running_loop()
         t0 = time.perf_counter()
         img = await loop.run_in_executor(self.codec.ex, read_data_url, uri)
+        M.HOST_STAGE.observe(time.perf_counter() - t0, stage="decode")
         fut = loop.create_future()
-        job = _Job(layer, img, loop, fut)
-        self.q.put(job)
-        M.QUEUE_DEPTH.set(self.q.qsize())
+        job = self.submit(layer, img, lambda v, e: _deliver(loop, _set_exc if e is not None else _set_result,
+                                                            fut, e if e is not None else v))
         res = await asyncio.wait_for(fut, timeout=self.cfg.request_timeout_s)
         if self.trace is not None:  # per-request stage timestamps (tools/latency.py --trace)
             self.trace.append((t0, job.t_enq, job.t_launch, job.t_gpu, job.t_enc, time.perf_counter()))
@@ -268,6 +284,8 @@ class DeconvService:
             handle, group, layer, t0 = item
             try:
                 mos = self.finish_batch(handle)
+                if self.device.type == "cuda":
+                    ops.conv.check_stream_k()
                 tg = time.perf_counter()
                 for j in group:
                     j.t_gpu = tg
@@ -285,7 +303,7 @@ class DeconvService:
                 te = time.perf_counter()
                 for j, m in zip(group, urls):
                     j.t_enc = te
-                    _deliver(j.loop, _set_result, j.future, m)
+                    j.deliver(m, None)
             elif self.native_codec:
                 # GIL-free native JPEG + base64 + quote, in chunks of ``encode_chunk`` images over
                 # the native threads (a lone request is split into restart segments); each chunk
@@ -296,10 +314,15 @@ class DeconvService:
                     te = time.perf_counter()
                     for j, m in zip(group[c0:c0 + step], urls):
                         j.t_enc = te
-                        _deliver(j.loop, _set_result, j.future, m)
+                        j.deliver(m, None)
             else:
                 for j, m in zip(group, mos):
-                    _deliver(j.loop, _set_result, j.future, m)
+                    j.deliver(m, None)
+            for j in group:
+                if j.t_enc:
+                    M.HOST_STAGE.observe(j.t_launch - j.t_enq, stage="queue")
+                    M.HOST_STAGE.observe(j.t_gpu - j.t_launch, stage="gpu")
+                    M.HOST_STAGE.observe(j.t_enc - j.t_gpu, stage="encode")
             self.batches += 1
             self.images += len(group)
             M.BATCH_SIZE.observe(len(group))
@@ -312,7 +335,7 @@ class DeconvService:
         self.last_error = repr(e)
         log.exception("batch failed", exc_info=e)
         for j in group:
-            _deliver(j.loop, _set_exc, j.future, e)
+            j.deliver(None, e)
 
     # ------------------------------------------------------------------ batch execution
     def preprocess(self, images: List[np.ndarray]) -> torch.Tensor:
@@ -322,7 +345,7 @@ class DeconvService:
         if self.device.type == "cuda":
             from ..runtime.staging import resize_batch
 
-            return resize_batch(images, torch.empty(B, S, S, 8, dtype=torch.bfloat16, device=self.device))
+            return resize_batch(images, torch.empty(B, S, S, 8, dtype=self.engine.rt.dtype, device=self.device))
         x = torch.empty(B, S, S, 8, dtype=torch.float32)
         for b, img in enumerate(images):
             x[b] = ops.preprocess_ref(ops.resize_u8_ref(img, S, S), 8, torch.float32)
@@ -343,7 +366,7 @@ class DeconvService:
             st = self.ring.stage(images, x)
             res = self.graphs.replay(layer, n)
         else:
-            x = torch.empty(n, S, S, 8, dtype=torch.bfloat16, device=self.device)
+            x = torch.empty(n, S, S, 8, dtype=self.engine.rt.dtype, device=self.device)
             st = self.ring.stage(images, x)
             res = self.engine.run(x, layer, k=self.cfg.filters, mode=self.cfg.mode)
         if self.cfg.gpu_jpeg and gpu_jpeg_fits(res.mosaic.shape[2]):  # JPEG on the device: only scans cross PCIe

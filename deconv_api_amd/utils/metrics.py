@@ -113,6 +113,35 @@ class Registry:
         return "\n".join(lines) + "\n"
 
 
+def merge_text(local: str, remote: str) -> str:
+    """Union of two Prometheus text renders (a front-end process and its GPU owner, serve/ingest.py):
+    one HELP/TYPE header per metric, the local sample when both processes have the same series.
+    Each process only populates its own metrics (HTTP counters in the front end, batch / GPU
+    stage histograms in the owner), so the union is the whole picture of one front end."""
+    def blocks(txt):
+        out, cur = {}, None
+        for line in txt.splitlines():
+            if line.startswith("# HELP "):
+                cur = line.split()[2]
+                out.setdefault(cur, ([], {}))[0].append(line)
+            elif line.startswith("# TYPE ") and cur is not None:
+                out[cur][0].append(line)
+            elif line and cur is not None:
+                out[cur][1].setdefault(line.rsplit(" ", 1)[0], line)
+        return out
+
+    a, b = blocks(local), blocks(remote)
+    lines = []
+    for name in list(a) + [n for n in b if n not in a]:
+        head, samples = a.get(name) or b[name]
+        merged = dict(samples)
+        for k, v in (b.get(name, ([], {}))[1]).items():
+            merged.setdefault(k, v)
+        lines.extend(head)
+        lines.extend(merged.values())
+    return "\n".join(lines) + "\n"
+
+
 REGISTRY = Registry()
 REQUESTS = REGISTRY.counter("dv_requests_total", "HTTP requests by route and status")
 LATENCY = REGISTRY.histogram("dv_request_latency_seconds", "request latency by route and layer")
@@ -122,4 +151,8 @@ ENGINE_TIME = REGISTRY.histogram("dv_engine_seconds", "engine time per batch by 
 QUEUE_DEPTH = REGISTRY.gauge("dv_queue_depth", "pending requests in the batcher")
 IMAGES = REGISTRY.counter("dv_images_total", "images processed by the engine")
 STAGE_TIME = REGISTRY.histogram("dv_stage_seconds", "per-batch GPU stage time from hipEvents (h2d, compute, d2h)",
+                                (0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 1.0))
+HOST_STAGE = REGISTRY.histogram("dv_host_stage_seconds",
+                                "per-request host stage time: parse, decode (front end / codec pool), ipc, "
+                                "queue (batcher wait), gpu (launch -> results on the host), encode (-> data URL)",
                                 (0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 1.0))

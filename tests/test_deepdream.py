@@ -742,7 +742,8 @@ def test_gpu_tiled_collective_octave_captured(native_lib):
     assert out["backend"] == "nccl" and out["collective"] is True, out
     assert out["octave_graph"] is True and out["step_graphs"] is False, out
     assert out["equal"] is True, out
-    # chunked (2 chunks on 2 streams, each chunk's all-gather issued from its stream; captured)
+    # chunked (2 chunks on 2 streams; each chunk's all-gather is issued from the capture-origin stream
+    # behind that chunk's event, not from the chunk's stream, so the process group sees it as captured)
     assert out["chunks"] == 2 and out["chunk_streams"] == 2 and out["chunked_octave_graph"] is True, out
     assert out["chunked_cos"] > 0.995 and out["chunked_maxdiff"] < 5e-2, out
 

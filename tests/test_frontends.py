@@ -1,0 +1,166 @@
+"""Multi-process serving: HTTP front ends (serve/frontend.py) feeding their rank's GPU owner over the
+ingest socket (serve/ingest.py), launched by serve/launch.py; CPU engine here (the same processes run
+the HIP engine on a GPU box). Reference surface: app/main.py:19-78."""
+from __future__ import annotations
+
+import base64
+import io
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.error
+import urllib.request
+from urllib.parse import quote_plus
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _png_url(h=40, w=56, seed=0) -> str:
+    from PIL import Image
+
+    rng = np.random.default_rng(seed)
+    buf = io.BytesIO()
+    Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)).save(buf, format="PNG")
+    return "data:image/png;base64," + base64.b64encode(buf.getvalue()).decode()
+
+
+def _post(base, fields, multipart=False, timeout=120):
+    """Fresh connection per call (urllib): SO_REUSEPORT hashes each one to some front end."""
+    if multipart:
+        from deconv_api_amd.api.forms import encode_multipart
+
+        body, ct = encode_multipart(fields)
+    else:
+        body = "&".join(f"{k}={quote_plus(v)}" for k, v in fields.items()).encode()
+        ct = "application/x-www-form-urlencoded"
+    req = urllib.request.Request(base + "/", data=body, headers={"Content-Type": ct})
+    try:
+        with urllib.request.urlopen(req, timeout=timeout) as r:
+            return r.status, json.loads(r.read())
+    except urllib.error.HTTPError as e:
+        return e.code, json.loads(e.read())
+
+
+def _get(base, path, timeout=30):
+    with urllib.request.urlopen(base + path, timeout=timeout) as r:
+        return r.status, r.read()
+
+
+def _wait_ready(base, proc, timeout=240):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        assert proc.poll() is None, f"server exited with {proc.returncode}"
+        try:
+            if _get(base, "/ready", 5)[0] == 200:
+                return
+        except OSError:
+            pass
+        time.sleep(0.3)
+    raise TimeoutError("server not ready")
+
+
+def _start(cmd, port, frontends, extra_env=None):
+    env = dict(os.environ, DV_DEVICE="cpu", DV_PORT=str(port), DV_HOST="127.0.0.1", DV_FRONTENDS=str(frontends),
+               DV_HIP_GRAPHS="0", DV_CODEC_WORKERS="2", DV_LOG_JSON="1", OMP_NUM_THREADS="1",
+               DV_INGEST_DIR="/tmp", PYTHONPATH=ROOT)
+    env.update(extra_env or {})
+    return subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                            start_new_session=True)
+
+
+def _stop(p):
+    if p.poll() is None:
+        os.killpg(p.pid, signal.SIGTERM)
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+
+
+@pytest.mark.timeout(300)
+def test_frontends_serve_reference_surface():
+    """Two front ends + one CPU owner: the reference's routes behave as in single-process mode."""
+    port = _free_port()
+    base = f"http://127.0.0.1:{port}"
+    p = _start([sys.executable, "-m", "deconv_api_amd.serve.launch"], port, 2)
+    try:
+        _wait_ready(base, p)
+        assert json.loads(_get(base, "/health-check")[1]) == {"healthy": "true"}
+        layers = json.loads(_get(base, "/layers")[1])["layers"]
+        assert layers[0] == "block1_conv1" and "block5_conv3" in layers
+        url = _png_url()
+        outs = []
+        for mp in (False, True):
+            st, out = _post(base, {"file": url, "layer": "block1_conv1"}, multipart=mp)
+            assert st == 200 and out.startswith("data:image/webp;base64,")
+            outs.append(out)
+        assert outs[0] == outs[1]  # same image, same layer: same bytes through either body encoding
+        from deconv_api_amd.codec.image import parse_result_data_url
+
+        assert parse_result_data_url(outs[0]).shape == (448, 448, 3)
+        st, out = _post(base, {"file": url, "layer": "nope"})
+        assert st == 400 and "unknown layer" in out["detail"]
+        st, out = _post(base, {"file": "data:image/png;base64,AAAA", "layer": "block1_conv1"})
+        assert st == 400
+        st, out = _post(base, {"layer": "block1_conv1"})
+        assert st == 422
+        st, out = _post(base, {"file": url, "layer": "input_1"})  # the owner's check, relayed
+        assert st == 400 and "no filters" in out["detail"]
+        st, body = _get(base, "/ready")
+        rd = json.loads(body)
+        assert rd["ready"] and rd["ingest"]["connections"] == 2 and rd["frontend"]["pid"] != rd["ingest"]["pid"]
+        m = _get(base, "/metrics")[1].decode()
+        assert "dv_requests_total" in m and "dv_batch_size_count" in m and 'stage="decode"' in m
+        assert m.count("# TYPE dv_uptime_seconds") == 1
+    finally:
+        _stop(p)
+    assert p.returncode is not None
+
+
+@pytest.mark.timeout(420)
+def test_frontends_per_rank_ingest_world3():
+    """torchrun world 3 (Gloo, CPU): every rank runs its own front end on the shared port
+    (SO_REUSEPORT) and decodes / computes only what its own front end accepted. Requests are spread
+    over the ranks by the kernel; each rank's owner counts exactly the requests its front end
+    shipped (no rank-0 decode, resize or scatter on the POST path)."""
+    port = _free_port()
+    mport = _free_port()
+    base = f"http://127.0.0.1:{port}"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={mport}", "-m", "deconv_api_amd.serve.launch"]
+    p = _start(cmd, port, 1)
+    try:
+        _wait_ready(base, p, 300)
+        url = _png_url(seed=3)
+        n = 36
+        for i in range(n):
+            st, out = _post(base, {"file": url, "layer": "block1_conv1"}, multipart=bool(i % 2))
+            assert st == 200 and out.startswith("data:image/webp;base64,")
+        seen = {}
+        for _ in range(200):  # fresh connections land on every rank's front end sooner or later
+            rd = json.loads(_get(base, "/ready")[1])
+            seen[rd["ingest"]["rank"]] = (rd["ingest"]["requests"], rd["frontend"]["pid"], rd["ingest"]["pid"])
+            if len(seen) == 3:
+                break
+        assert sorted(seen) == [0, 1, 2], seen
+        assert sum(v[0] for v in seen.values()) == n  # every request was decoded and run by exactly one rank
+        assert all(v[0] > 0 for v in seen.values()), seen  # ... and every rank took a share
+        assert len({v[2] for v in seen.values()}) == 3 and len({v[1] for v in seen.values()}) == 3
+    finally:
+        _stop(p)
