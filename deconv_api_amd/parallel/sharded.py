@@ -188,10 +188,16 @@ class ShardedRunner:
         # the next replay, so each batch's mosaics are copied into its own slot on the compute
         # stream; the gather runs on ``comm_stream`` behind that batch's event only
         self.slots: List[Optional[torch.Tensor]] = [None, None]
-        self.comm_stream = torch.cuda.Stream(info.device) if cuda else None
         # a batch's input path (upload + resize + scatter) runs on its own stream, never behind the
-        # previous batch's engine work on the compute stream nor behind a gather on comm_stream
-        self.in_stream = torch.cuda.Stream(info.device) if cuda else None
+        # previous batch's engine work on the compute stream nor behind a gather on comm_stream; both
+        # side streams are probed onto hardware queues of their own (runtime/streams.py)
+        self.comm_stream = self.in_stream = None
+        if cuda:
+            from ..runtime.streams import independent_stream
+
+            cur = torch.cuda.current_stream(info.device)
+            self.comm_stream = independent_stream(info.device, [cur])
+            self.in_stream = independent_stream(info.device, [cur, self.comm_stream])
         self._bid = 0
 
     @property

@@ -81,9 +81,12 @@ class StagingRing:
         self.device = device
         self.slots = slots
         self.max_images = max_images
-        self.copy_stream = torch.cuda.Stream(device)
-        self.back_stream = torch.cuda.Stream(device)
+        from .streams import independent_stream
+
+        # upload / copy-back streams on hardware queues apart from the compute stream's (streams.py)
         self.compute_stream = torch.cuda.Stream(device)
+        self.copy_stream = independent_stream(device, [self.compute_stream])
+        self.back_stream = independent_stream(device, [self.compute_stream, self.copy_stream])
         self._bytes = [0] * slots
         self.host: List[Optional[torch.Tensor]] = [None] * slots
         self.dev: List[Optional[torch.Tensor]] = [None] * slots

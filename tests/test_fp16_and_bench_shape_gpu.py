@@ -124,6 +124,11 @@ def test_fp16_service_serves_post(native_lib):
         assert _psnr(torch.from_numpy(got), ref) >= 35.0, _psnr(torch.from_numpy(got), ref)
     finally:
         svc.close()
+        del svc
+        import gc
+
+        gc.collect()  # its hipGraphs go now, not in some later test's timed region
+        torch.cuda.synchronize()
 
 
 def test_fp32_on_gpu_is_refused():
@@ -146,7 +151,13 @@ def b256(native_lib):
     x = _pre(img, torch.bfloat16)
     res = gpu.run(x, "block5_conv3", k=4)
     torch.cuda.synchronize()
-    return gpu, m, img, x, res
+    yield gpu, m, img, x, res
+    # ~10 GB of B = 256 activations: hand the cached blocks back, so later modules' small allocations
+    # do not carve (and hipMalloc around) this module's pool (tests/test_sharded_streams_gpu.py times
+    # host launch latency)
+    del res, x, gpu
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
 
 
 def test_b256_equals_b4_on_sampled_images(b256):
@@ -165,9 +176,12 @@ def test_b256_equals_b4_on_sampled_images(b256):
             psnr = _psnr(res.mosaic[b].cpu(), sub.mosaic[i].cpu())
             # (measured: mean 0.8-1.0 level, PSNR 43-44 dB)
             assert psnr >= 38.0 and float(diff.mean()) <= 1.5, (b, float(diff.mean()), psnr)
+            # two bf16 forwards whose near-tied pool switches may resolve differently (measured 0.9979 -
+            # 0.9999); the arithmetic itself is held to >= 0.999 against fp32 by the strict test below
             for k in range(4):
                 if float(sub.recon[i, k].abs().max()) > 0:
-                    assert _cos(res.recon[b, k].cpu(), sub.recon[i, k].cpu()) >= 0.999, (b, k)
+                    c = _cos(res.recon[b, k].cpu(), sub.recon[i, k].cpu())
+                    assert c >= 0.995, (b, k, c)
         else:  # only a near-tie may differ (accumulation order of the batch-size-dependent kernels)
             assert sums is not None
             st = gpu.forward(x[b:b + 1].contiguous(), "block5_conv3")

@@ -104,19 +104,39 @@ def _images(seed):
 @pytest.mark.parametrize("side", [True, False])
 def test_next_batch_enqueued_while_previous_runs(monkeypatch, side):
     r = _runner(monkeypatch, side)
-    # warm-up in the measured pattern (two in flight): stream pools, pinned host blocks, native library
-    w = [r.launch("block5_conv3", _images(0)) for _ in range(2)]
-    for b in w:
-        r.finish(b)
+    # warm-up in the measured pattern (two in flight), every staging slot twice: stream pools, pinned
+    # host blocks (a fresh pinned block is a device-synchronizing hipHostMalloc), native library
+    for _ in range(3):
+        w = [r.launch("block5_conv3", _images(0)) for _ in range(2)]
+        for b in w:
+            r.finish(b)
     torch.cuda.synchronize()
+    # no cyclic-GC pass inside the timed launches: collecting an earlier test's hipGraphs destroys
+    # them, and hipGraphExecDestroy waits for the device (it did, behind batch 1's engine spin)
+    import gc
+
+    gc.collect()
+    gc.disable()
+    import sys
+    import threading
+    import traceback
+
+    main, where = threading.get_ident(), []
+    # if the launches block, record where (the host stack 60 ms in, while the spin still runs)
+    timer = threading.Timer(0.06, lambda: where.append("".join(traceback.format_stack(sys._current_frames()[main]))))
     t0 = time.perf_counter()
+    timer.start()
     b1 = r.launch("block5_conv3", _images(1))
+    t1 = time.perf_counter()
     b2 = r.launch("block5_conv3", _images(2))
+    timer.cancel()
     host_ms = (time.perf_counter() - t0) * 1e3
+    host_ms = f"{host_ms:.1f} (batch 1 {1e3 * (t1 - t0):.1f}) {where[-1][-1500:] if where else ''}"
     b1_running = not b1.ev.query()  # batch 2's engine is enqueued: was batch 1's still running?
+    gc.enable()
     out1, out2 = r.finish(b1), r.finish(b2)
     if side:
-        assert b1_running, f"batch 2's scatter waited for batch 1's engine work ({host_ms:.1f} ms to launch both)"
+        assert b1_running, f"batch 2's scatter waited for batch 1's engine work ({host_ms} ms to launch both)"
     else:
         assert not b1_running  # the gap this change removes (guards the stand-ins' semantics)
     # rank 0's half of each batch went through scatter -> engine -> gather -> copy-back intact

@@ -50,15 +50,15 @@ def _image(rng, w, h):
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
-def corpus(n: int, seed: int = 0):
-    """n (data URL, kind) pairs: mixed sizes, JPEG (q90) and PNG."""
+def corpus(n: int, seed: int = 0, png_every: int = 4):
+    """n (data URL, kind) pairs: mixed sizes, JPEG (q90) and every ``png_every``-th one PNG."""
     from PIL import Image
 
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
         w, h = SIZES[rng.choice(len(SIZES), p=WEIGHTS)]
-        fmt = "PNG" if i % 4 == 3 else "JPEG"
+        fmt = "PNG" if png_every and i % png_every == png_every - 1 else "JPEG"
         buf = io.BytesIO()
         kw = {"quality": 90} if fmt == "JPEG" else {"compress_level": 1}
         Image.fromarray(_image(rng, w, h)).save(buf, format=fmt, **kw)
@@ -125,8 +125,11 @@ def _client(addr, conns, reqs, t_warm, t_end, seed, q):
         c = connect()
         cs.append(c)
         send_next(c)
+    cpu0 = None
     while True:
         now = time.perf_counter()
+        if cpu0 is None and now >= t_warm:
+            cpu0 = time.process_time()
         if now > t_end:
             break
         for key, ev in sel.select(timeout=0.05):
@@ -185,7 +188,7 @@ def _client(addr, conns, reqs, t_warm, t_end, seed, q):
             c.sock.close()
         except OSError:
             pass
-    q.put((lat, errs, bad, n_out))
+    q.put((lat, errs, bad, n_out, time.process_time() - (cpu0 or 0.0)))
 
 
 def scrape(base: str) -> dict:
@@ -221,7 +224,28 @@ def breakdown(m0: dict, m1: dict) -> dict:
     return out
 
 
-def run_load(base, reqs, clients, procs, seconds, warmup):
+def _tree_cpu(pid):
+    """{"frontend"|"owner"|"other": CPU seconds} of a process tree (psutil), by command line."""
+    import psutil
+
+    out = {}
+    try:
+        root = psutil.Process(pid)
+        procs = [root] + root.children(recursive=True)
+    except psutil.Error:
+        return out
+    for p in procs:
+        try:
+            t = p.cpu_times()
+            cmd = " ".join(p.cmdline())
+        except psutil.Error:
+            continue
+        kind = "frontend" if "serve.frontend" in cmd else ("owner" if "serve.launch" in cmd else "other")
+        out[kind] = out.get(kind, 0.0) + t.user + t.system
+    return out
+
+
+def run_load(base, reqs, clients, procs, seconds, warmup, server_pid=None):
     host, port = base.split("://")[1].split(":")
     addr = (host, int(port))
     procs = max(1, min(procs, clients))
@@ -236,7 +260,10 @@ def run_load(base, reqs, clients, procs, seconds, warmup):
     for p in ps:
         p.start()
     time.sleep(max(0.0, t_warm - time.perf_counter()))
+    c0 = _tree_cpu(server_pid) if server_pid else {}
     m0 = scrape(base)
+    time.sleep(max(0.0, t_end - time.perf_counter()))
+    c1 = _tree_cpu(server_pid) if server_pid else {}
     res = [q.get(timeout=seconds + warmup + 120) for _ in ps]
     m1 = scrape(base)
     for p in ps:
@@ -247,10 +274,16 @@ def run_load(base, reqs, clients, procs, seconds, warmup):
     def pct(f):
         return round(lat[min(n - 1, int(f * n))], 2) if n else None
 
-    return {"clients": clients, "client_procs": procs, "seconds": seconds, "responses": n,
-            "req_per_s": round(n / seconds, 1), "p50_ms": pct(0.5), "p90_ms": pct(0.9), "p99_ms": pct(0.99),
-            "errors": sum(r[1] for r in res), "bad_bodies": sum(r[2] for r in res),
-            "server_stages": breakdown(m0, m1)}
+    out = {"clients": clients, "client_procs": procs, "seconds": seconds, "responses": n,
+           "req_per_s": round(n / seconds, 1), "p50_ms": pct(0.5), "p90_ms": pct(0.9), "p99_ms": pct(0.99),
+           "errors": sum(r[1] for r in res), "bad_bodies": sum(r[2] for r in res),
+           "client_cpu_s": round(sum(r[4] for r in res), 2), "server_stages": breakdown(m0, m1)}
+    if c1:  # CPU-seconds the server spent in the window, per process kind, and per response
+        out["server_cpu_s"] = {k: round(c1.get(k, 0.0) - c0.get(k, 0.0), 2) for k in c1}
+        tot = sum(out["server_cpu_s"].values())
+        out["server_cpu_ms_per_req"] = round(1e3 * tot / max(n, 1), 3)
+        out["cpus_busy"] = round((tot + out["client_cpu_s"]) / seconds, 2)
+    return out
 
 
 def wait_ready(base: str, timeout: float, proc=None) -> None:
@@ -286,12 +319,13 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--warmup", type=float, default=3.0)
     ap.add_argument("--corpus", type=int, default=64)
+    ap.add_argument("--png-every", type=int, default=4, help="every n-th corpus image is a PNG (0: JPEG only)")
     ap.add_argument("--spawn", action="store_true", help="start `python -m deconv_api_amd.serve.launch` as a child")
     ap.add_argument("--frontends", type=int, default=None, help="DV_FRONTENDS for the spawned server")
     ap.add_argument("--env", action="append", default=[], help="extra KEY=VALUE for the spawned server")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    urls = corpus(a.corpus)
+    urls = corpus(a.corpus, png_every=a.png_every)
     host = a.url.split("://")[1]
     reqs = build_requests(urls, a.layer, host)
     srv = None
@@ -318,7 +352,7 @@ def main():
         except OSError:
             pass
         for c in [int(x) for x in a.clients.split(",")]:
-            r = run_load(a.url, reqs, c, a.procs, a.seconds, a.warmup)
+            r = run_load(a.url, reqs, c, a.procs, a.seconds, a.warmup, srv.pid if srv is not None else None)
             print(json.dumps(r), flush=True)
             res["runs"].append(r)
     finally:
