@@ -169,6 +169,11 @@ def main(argv=None):
     eng = DeconvNet(model.build(dev, dtype))
     log(f"[rank {info.rank}] weights ready in {time.time() - t0:.1f}s ({model.num_params() / 1e6:.1f}M params)")
 
+    # with RCCL: every step's work on a stream whose hardware queue is not the all-gather's, so step i's
+    # async gather overlaps step i+1's compute instead of queueing with it (parallel/dist.py)
+    comp, overlap = pdist.pick_compute_stream(info) if dev.type == "cuda" else (None, None)
+    if comp is not None:
+        torch.cuda.set_stream(comp)
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(1000 + info.rank)
     images = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=dev, generator=g)
@@ -393,6 +398,7 @@ def main(argv=None):
         "gpu_jpeg": bool(JPEG and cuda),
         **({"jpeg_scan_bytes_per_image": round(sum(jpeg_bytes) / len(jpeg_bytes))} if jpeg_bytes else {}),
         "process_group": info.backend,
+        **({"collective_overlaps_compute": overlap} if overlap is not None else {}),
         "data": "synthetic uint8 224x224 images, seeded random-init VGG16 weights",
         "config": {"model": f"vgg16_deconvnet_{args.layer}", "global_batch": B * info.world, "seq_len": S,
                    "image_size": S, "filters_per_image": args.k, "parallelism": f"dp{info.world}"},

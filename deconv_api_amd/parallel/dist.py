@@ -142,3 +142,73 @@ def shard_sizes(total: int, world: int, bucket: int = 1) -> List[int]:
 def shard_counts(total: int, world: int) -> List[int]:
     per = -(-total // world)
     return [max(0, min(per, total - r * per)) for r in range(world)]
+
+
+
+def _spin_vs_gather(info: DistInfo, spinner: Optional[torch.cuda.Stream], x, y, idle, spin_cycles: int,
+                    timeout_s: float) -> bool:
+    """One probe round (collective): ``spinner`` (this rank only, None elsewhere) runs a ~2 ms spin,
+    every rank issues an async all-gather from an idle stream. True when, on the spinning rank, the
+    gather completed while the spin still ran (the two are on different hardware queues)."""
+    dev = info.device
+    torch.cuda.synchronize(dev)
+    end = None
+    if spinner is not None:
+        with torch.cuda.stream(spinner):
+            torch.cuda._sleep(spin_cycles)
+            end = torch.cuda.Event()
+            end.record(spinner)
+    with torch.cuda.stream(idle):
+        work = dist.all_gather_into_tensor(y, x, async_op=True)
+    ok = True
+    if end is not None:
+        import time
+
+        ok, t0 = False, time.perf_counter()
+        while time.perf_counter() - t0 < timeout_s:
+            w, e = work.is_completed(), end.query()
+            if w and not e:
+                ok = True
+                break
+            if e:
+                break
+    torch.cuda.synchronize(dev)
+    return ok
+
+
+def pick_compute_stream(info: DistInfo, tries: int = 6, spin_cycles: int = 4_000_000,
+                        timeout_s: float = 10.0):
+    """This rank's compute stream for steps whose collectives run async beside the next step's compute
+    (bench.py's all-gather). HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues round-robin, and
+    RCCL's internal stream can share one with the compute stream: the gather then waits for, and
+    delays, the compute queued before it. Measured on MI355X (tools/queue_alias_probe.py, 1-rank RCCL
+    group): the NULL stream and 2 of 6 pool streams were serialized with the all-gather; every
+    high-priority stream overlapped it, but a high-priority compute stream cost 3-4 % at N=1
+    (profiles/bench_c2_r6_stream_prio_ab.txt), so a normal-priority stream is probed instead.
+
+    Probed rank by rank (collective; every rank calls it): only the probing rank spins, so the
+    all-gather's completion answers for that rank alone. Returns ``(stream, independent)``; the
+    current stream and None without an RCCL group."""
+    dev = info.device
+    if info.backend != "nccl":
+        return torch.cuda.current_stream(dev) if dev.type == "cuda" else None, None
+    x = torch.ones(1 << 14, device=dev)
+    y = torch.empty(info.world << 14, device=dev)
+    idle = torch.cuda.Stream(dev)
+    _spin_vs_gather(info, None, x, y, idle, spin_cycles, timeout_s)  # communicator / kernels warm
+    chosen, independent = torch.cuda.current_stream(dev), False
+    for r in range(info.world):
+        cand = chosen
+        for _ in range(max(1, tries)):
+            me = r == info.rank
+            ok = _spin_vs_gather(info, cand if me else None, x, y, idle, spin_cycles, timeout_s)
+            flag = torch.tensor([0.0 if (ok or not me) else 1.0], device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            if float(flag.item()) == 0.0:
+                if me:
+                    chosen, independent = cand, True
+                break
+            if me:
+                cand = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    return chosen, independent

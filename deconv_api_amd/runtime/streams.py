@@ -15,6 +15,7 @@ issues the copy: behind the first MFMA-bound layers of the next step (bench.py:C
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from typing import Dict, Sequence
@@ -26,12 +27,14 @@ _copy_streams: Dict[int, torch.cuda.Stream] = {}
 
 
 def copy_stream(device: torch.device) -> torch.cuda.Stream:
-    """The device's long-lived device -> host copy stream (created once)."""
+    """The device's long-lived device -> host copy stream (created once, on a hardware queue apart
+    from the calling thread's current stream)."""
     idx = torch.device(device).index or 0
     with _lock:
         s = _copy_streams.get(idx)
         if s is None:
-            s = _copy_streams[idx] = torch.cuda.Stream(device=idx)
+            s = _copy_streams[idx] = independent_stream(torch.device("cuda", idx),
+                                                        [torch.cuda.current_stream(idx)])
         return s
 
 
@@ -61,6 +64,8 @@ def independent_stream(device, avoid: Sequence[torch.cuda.Stream], tries: int = 
     outside graph capture (it synchronizes the device). Falls back to a plain new stream when every
     candidate shares a queue (fewer hardware queues than streams in use)."""
     dev = torch.device(device)
+    if os.environ.get("DV_NO_STREAM_PROBE") == "1":  # A/B: plain pool streams
+        return torch.cuda.Stream(dev)
     torch.cuda.synchronize(dev)
     first = None
     for _ in range(max(1, tries)):
@@ -71,3 +76,4 @@ def independent_stream(device, avoid: Sequence[torch.cuda.Stream], tries: int = 
             return s
     torch.cuda.synchronize(dev)
     return first
+

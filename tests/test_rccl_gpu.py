@@ -51,6 +51,9 @@ def test_bench_under_torchrun_uses_rccl():
     out = _torchrun(["bench.py", "--gpus", "1", "--steps", "2", "--warmup", "1", "--batch", "8"])
     assert out["process_group"] == "nccl" and out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1"
     assert out["value"] > 0 and out["p50_req_latency_ms"] >= out["p50_batch_latency_ms"] * 0.5
+    # the step's compute stream was probed onto a hardware queue apart from RCCL's (parallel/dist.py:
+    # pick_compute_stream): the async all-gather of step i overlaps step i+1 instead of queueing behind it
+    assert out["collective_overlaps_compute"] is True, out
 
 
 @pytest.mark.gpu
