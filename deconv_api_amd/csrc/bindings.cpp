@@ -223,14 +223,14 @@ int64_t conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::op
     need(*out_code, out_rows * a.OC, "out_code");
     a.out_code = reinterpret_cast<uint8_t*>(out_code->data_ptr());
     TORCH_CHECK(out.scalar_type() == dt, "pool out must have x's dtype");
-    const bool no_pool_t = std::getenv("DV_NO_POOL_T") != nullptr;  // A/B: the per-element pool stores (per call)
+    const bool no_pool_t = dv_ab_env("DV_NO_POOL_T") != nullptr;  // A/B: the per-element pool stores (per call)
     a.pool_t = !no_pool_t && a.OC % 4 == 0 && a.out_ld % 4 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0 &&
                reinterpret_cast<uintptr_t>(a.out_code) % 4 == 0;
     // 2 (opt-in, DV_POOL_EPI=lds, per call): the LDS-staged pooled epilogue (whole 16-B value / code chunks
     // per lane). Measured equal to slightly slower than the transposed 8-B stores on config 2 (the pooled
     // output is a quarter of the conv's: 7478 / 7506 / 7547 vs 7504 / 7531 / 7549 img/s, same box,
     // alternating; profiles/bench_c2_r5_pool_epi_ab.txt)
-    const char* pe = std::getenv("DV_POOL_EPI");
+    const char* pe = dv_ab_env("DV_POOL_EPI");
     if (a.pool_t && pe && std::strcmp(pe, "lds") == 0 && a.OC % 16 == 0 && a.out_ld % 8 == 0 &&
         reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(a.out_code) % 16 == 0)
       a.pool_t = 2;
@@ -297,9 +297,9 @@ int64_t conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::op
   {  // LDS-staged vector epilogue: 16-bit rows (out / res / emask) 16-B aligned
     auto al = [](const void* p, int64_t ld) { return reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 8 == 0; };
     a.vec_epi = epi == dv::CONV_E_BF16 && al(a.out, a.out_ld) && (!a.res || al(a.res, a.res_ld)) &&
-                (!a.emask || al(a.emask, a.emask_ld)) && (std::getenv("DV_NO_VEC_EPI") == nullptr || a.out2);
+                (!a.emask || al(a.emask, a.emask_ld)) && (dv_ab_env("DV_NO_VEC_EPI") == nullptr || a.out2);
     TORCH_CHECK(!a.out2 || a.vec_epi, "conv out2: 16-B aligned out rows (LDS-staged epilogue)");
-    static const bool no_batch = std::getenv("DV_NO_EPI_BATCH") != nullptr;
+    static const bool no_batch = dv_ab_env("DV_NO_EPI_BATCH") != nullptr;
     a.epi_batch = !no_batch;
   }
   if (ucode.has_value()) {  // max-unpooled output (the consumer of this conv reads the full-res map)
@@ -368,13 +368,13 @@ int64_t conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::op
   // on plain 16-bit-output convs whose sides are multiples of 16 (measured on the pool variant:
   // VGG16 block1_conv2 fwd 1.28 -> 1.04 ms, profiles/layers_r1_ab{0,1}.txt)
   const bool hs16_ok = a.H % 16 == 0 && a.W % 16 == 0 && a.C % 32 == 0 && a.OC % 4 == 0 && !a.relu_in &&
-                       (a.OCpad == 64 || a.OCpad == 128) && std::getenv("DV_NO_HS") == nullptr;
+                       (a.OCpad == 64 || a.OCpad == 128) && dv_ab_env("DV_NO_HS") == nullptr;
   const bool halo_auto = halo_ok && a.H * a.W >= 112 * 112 && a.res == nullptr && a.emask == nullptr &&
                          !(hs16_ok && amode == dv::CONV_A_FWD && epi == dv::CONV_E_BF16);
   // conv 64 -> 64 + fused 2x2 max-pool at large maps (VGG16 block1_conv2 forward): weight-resident
   // halo kernel with LDS-DMA staging and the pool in registers
   if (epi == dv::CONV_E_POOL && amode == dv::CONV_A_FWD && (impl == 0 || impl == 3) && a.H * a.W >= 112 * 112 &&
-      !mask.has_value() && std::getenv("DV_NO_POOL_V3") == nullptr && (impl == 3 || !hs16_ok)) {
+      !mask.has_value() && (impl == 3 || !hs16_ok)) {
     const int rc = dv::conv3x3_pool_v3_launch(a, cur_stream());
     if (rc >= 0) {
       check_rc(rc, "conv_pool_v3");
@@ -385,19 +385,10 @@ int64_t conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::op
   // first layer (8-channel padded RGB image -> 64 channels): row-streaming, output-write bound
   if (epi == dv::CONV_E_BF16 && amode == dv::CONV_A_FWD && (impl == 0 || impl == 3) && a.C == 8 && !a.ucode &&
       !a.res && !a.emask && a.relu_cols <= 0 && a.H * a.W >= 56 * 56 && !mask.has_value() &&
-      std::getenv("DV_NO_C8_STREAM") == nullptr) {
+      dv_ab_env("DV_NO_C8_STREAM") == nullptr) {
     const int rc = dv::conv3x3_c8_stream_launch(a, cur_stream());
     if (rc >= 0) {
       check_rc(rc, "conv_c8_stream");
-      finish_stats();
-      return 0;
-    }
-  }
-  // unpool -> conv (64/128 out, full-res sides % 16): hs16 with the pooled halo expanded in LDS
-  if (impl == 0 && amode == dv::CONV_A_UNPOOL && epi == dv::CONV_E_BF16 && !mask.has_value()) {
-    const int rc = dv::conv3x3_hs_unpool_launch(a, cur_stream());
-    if (rc >= 0) {
-      check_rc(rc, "conv_halo_stream_unpool");
       finish_stats();
       return 0;
     }
@@ -450,10 +441,10 @@ int64_t conv(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor out, c10::op
       a.relu_in = 0;
     }
     // A/B switches: DV_HS_EMASK_OFF (masked dgrads back on the DMA kernel), DV_HS_PAD_OFF (pad != 1)
-    static const bool hs_emask_off = std::getenv("DV_HS_EMASK_OFF") != nullptr;
-    static const bool hs_pad_off = std::getenv("DV_HS_PAD_OFF") != nullptr;
+    static const bool hs_emask_off = dv_ab_env("DV_HS_EMASK_OFF") != nullptr;
+    static const bool hs_pad_off = dv_ab_env("DV_HS_PAD_OFF") != nullptr;
     // smallest map side routed to the halo-stream kernels (DV_HS_MIN_W, default 64)
-    static const int64_t hs_min_w = std::getenv("DV_HS_MIN_W") ? std::atoll(std::getenv("DV_HS_MIN_W")) : 64;
+    static const int64_t hs_min_w = dv_ab_env("DV_HS_MIN_W") ? std::atoll(dv_ab_env("DV_HS_MIN_W")) : 64;
     // 3x3 s1 convs (pad 0..2) with 64/128 padded output channels at large maps: halo-stream kernel
     // (every input pixel fetched once per 32-channel chunk instead of once per tap); also the ReLU-
     // masked (emask) input gradients of such convs (InceptionV3 stem / ResNet 3x3 dgrads)
@@ -1176,7 +1167,7 @@ void deprocess_mosaic(Tensor recon, Tensor out, int64_t tiles, bool reverse, c10
   const int64_t rows = (tiles + 1) / 2;
   TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.numel() == B * rows * H * 2 * W * 3,
               "deprocess: out [B, rows*H, 2*W, 3] u8");
-  if (W % 4 != 0 || std::getenv("DV_DEPROCESS_V1")) {  // one block per image, two-pass statistics
+  if (W % 4 != 0) {  // one block per image, two-pass statistics
     check_rc(dv::deprocess_mosaic_launch(recon.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)B, (int)H, (int)W,
                                          (int)tiles, reverse ? 1 : 0, cur_stream()),
              "deprocess_mosaic");

@@ -11,6 +11,7 @@
 
 #include "kernels.h"  // DT_BF16 / DT_F16
 
+
 // ---- DV_DEBUG device bounds checks (python -m deconv_api_amd._build --debug) ----
 // DV_BOUNDS(off, n, extent, what): in a debug build, an access of n elements at element offset
 // `off` outside [0, extent) prints the kernel site and the offending numbers and evaluates to

@@ -21,15 +21,15 @@ void conv_dma_tune(int cfg, int ks) {
 // 14.8 -> 11.4 us, M 4096 x N 96 x K 2592 23.3 -> 15.2 us; K <= 768 gains nothing).
 int conv_dma_splitk(const ConvArgs& a) {
   if (g_ks > 0) return std::min(g_ks, a.Kpad / 64);
-  static const bool off = std::getenv("DV_NO_SPLITK") != nullptr;
-  static const bool small_off = std::getenv("DV_NO_SMALL_SPLITK") != nullptr;
+  static const bool off = dv_ab_env("DV_NO_SPLITK") != nullptr;
+  static const bool small_off = dv_ab_env("DV_NO_SMALL_SPLITK") != nullptr;
   if (off) return 1;
   const int nk = a.Kpad / 64;
   if (g_cfg == 0 && auto_cfg(a) == 8) {
     // only the smallest problems: the reduce pass re-reads ks x M x OCpad fp32 partials, which
     // outweighs the shorter K loop once M x OCpad grows (full-model A/B, docs/KERNELS.md)
     static const long long mn_max =
-        std::getenv("DV_SMALL_SPLITK_MN") ? std::atoll(std::getenv("DV_SMALL_SPLITK_MN")) : 300000LL;
+        dv_ab_env("DV_SMALL_SPLITK_MN") ? std::atoll(dv_ab_env("DV_SMALL_SPLITK_MN")) : 300000LL;
     if (small_off || (long long)a.M * a.OCpad > mn_max) return 1;
     return nk >= 20 ? 4 : (nk >= 16 ? 2 : 1);
   }

@@ -1648,7 +1648,7 @@ static int num_cus() {
 // DV_KW3: 0 disables the shared-kw-tap kernel (A/B), 2 forces it for every eligible launch regardless
 // of the grid size (tests: small shapes with many image borders per tile). Read per launch.
 static int kw3_mode() {
-  const char* e = std::getenv("DV_KW3");
+  const char* e = dv_ab_env("DV_KW3");
   return e ? std::atoi(e) : 1;
 }
 // DV_KW3_VAR: the KW3 main-loop variant (conv_dma_kw3_kernel VAR; 8 / 9 and 10 (KW3P without stores) are
@@ -1656,11 +1656,11 @@ static int kw3_mode() {
 // DV_KW3_VAR in a serving process cannot corrupt convs; without it they fall back to the default).
 // Read per launch.
 static int kw3_var() {
-  const char* e = std::getenv("DV_KW3_VAR");
+  const char* e = dv_ab_env("DV_KW3_VAR");
   const int v = e ? std::atoi(e) : kKw3DefaultVar;
   if (v == 8 || v == 9 || v == 10 || v == 20 || v == 21) {
     static bool warned = false;
-    if (std::getenv("DV_ALLOW_WRONG_ABLATION") == nullptr) {
+    if (dv_ab_env("DV_ALLOW_WRONG_ABLATION") == nullptr) {
       if (!warned) fprintf(stderr, "deconv_api_amd: DV_KW3_VAR=%d ignored (needs DV_ALLOW_WRONG_ABLATION=1)\n", v);
       warned = true;
       return kKw3DefaultVar;
@@ -1672,7 +1672,7 @@ static int kw3_var() {
 }
 
 // DV_KW3P_NO_PRE=1: KW3P without the step-1 DMA issued ahead of the epilogue stores (A/B; read per launch)
-static int kw3p_pre() { return std::getenv("DV_KW3P_NO_PRE") == nullptr ? 1 : 0; }
+static int kw3p_pre() { return dv_ab_env("DV_KW3P_NO_PRE") == nullptr ? 1 : 0; }
 
 // KW3P stream-K applies (conv_dma_kw3p_kernel SK): a workspace was passed (bindings.cpp), not switched off
 // (DV_NO_KW3_SK=1, read per launch), one workgroup per CU with the column groups dividing the grid, more
@@ -1690,7 +1690,7 @@ static bool kw3_sk_ok(const ConvArgs& a, int BM, int BN) {
   // 0.26 -> 0.22 ms; on many-round grids its split-tile traffic and lost A sharing cost 1-3 %,
   // profiles/kw3_sk_ab_r5.txt)
   // (DV_KW3_SK=all: every eligible grid, A/B; read per launch)
-  const char* ska = std::getenv("DV_KW3_SK");
+  const char* ska = dv_ab_env("DV_KW3_SK");
   const long long max_tiles = ska && std::strcmp(ska, "all") == 0 ? (1LL << 40) : 4LL * G;
   return G <= kSkMaxWg && G <= a.skslots && (long long)BM * BN <= kSkSlotFloats && tiles_n >= 1 && G % tiles_n == 0 &&
          tiles_m * tiles_n > G && tiles_m * tiles_n < max_tiles && tiles_m >= G / tiles_n &&
@@ -1745,7 +1745,7 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
         // caches): config 2 +0.3 % (3 / 3 pairs, profiles/bench_c2_r5_unp_nt_ab.txt). DV_KW3P_UNP_NT=0: plain
         // stores (A/B; read per launch)
         if constexpr (U == 1) {
-          const char* unt = std::getenv("DV_KW3P_UNP_NT");
+          const char* unt = dv_ab_env("DV_KW3P_UNP_NT");
           if (!(unt && std::strcmp(unt, "0") == 0) && !(tiles_m_limit == 0 && kw3_sk_ok(a, BM, BN))) {
             hipLaunchKernelGGL((conv_dma_kw3p_kernel<DT, BN, BM, U, 2>), dim3(g), dim3(512), 0, s, a, tiles_n, (int)nwg,
                                kw3p_pre());
@@ -1770,7 +1770,7 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
         // the LDS-sliced 16-B store epilogue unless DV_KW3P_EPI=reg (A/B) or the rows are not 16-B aligned:
         // config-2 KW3P launches 9-13 % faster than with the register-transposed 8-B stores
         // (profiles/kw3_epi_ab_r5.txt), config 2 +6.6 % (7418 / 7457 vs 6966 / 6985 img/s, same box)
-        return (std::getenv("DV_KW3P_EPI") == nullptr || std::strcmp(std::getenv("DV_KW3P_EPI"), "reg") != 0) &&
+        return (dv_ab_env("DV_KW3P_EPI") == nullptr || std::strcmp(dv_ab_env("DV_KW3P_EPI"), "reg") != 0) &&
                        a.OC % 8 == 0 && a.out_ld % 8 == 0
                    ? launch_p(std::integral_constant<int, 2>{})
                    : launch_p(std::integral_constant<int, 0>{});
@@ -1778,7 +1778,7 @@ static int kw3_try(const ConvArgs& a, hipStream_t s, int tiles_m_limit = 0) {
       // non-persistent KW3 kernel's workgroup-staged one, A/B; read per launch)
       if (pvar && a.ucode != nullptr && a.res == nullptr && a.emask == nullptr && !a.accumulate &&
           a.out2 == nullptr && a.OC == a.OCpad && a.OC % 8 == 0 && a.out_ld % 8 == 0 && a.W >= 8 && a.ucode_div >= 1 &&
-          a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19) && std::getenv("DV_NO_KW3P_UNPOOL") == nullptr)
+          a.H < 4096 && 2LL * a.H * a.W + BM < (1LL << 19) && dv_ab_env("DV_NO_KW3P_UNPOOL") == nullptr)
         return launch_p(std::integral_constant<int, 1>{});
     }
     if constexpr (DT == DT_BF16 && EPI == CONV_E_BF16) {
@@ -1884,12 +1884,12 @@ static int dma_forced(const ConvArgs& a, hipStream_t s, int cfg) {
 // 4-wave tile with a 3-stage ring and no split-K; mid-size / short-K ones by the epilogue and DMA
 // issue of one big tile per CU: 128x128. The big-K VGG16 layers keep the large tiles.
 static int auto_cfg(const ConvArgs& a) {
-  static const bool off = std::getenv("DV_NO_AUTO_CFG") != nullptr;  // A/B: the size-based choice only
+  static const bool off = dv_ab_env("DV_NO_AUTO_CFG") != nullptr;  // A/B: the size-based choice only
   if (a.mask != nullptr || off) return 0;
   const long long mn = (long long)a.M * a.OCpad;
   // (short K too: M 1600 x N 64 x K 64 4.2 vs 6.0 us for the size-based 256 x 64 tile in a graph,
   // tools/small_conv_latency.py; DV_SMALL_TILE_KMIN=256 restores the round-1 rule)
-  static const int kmin = std::getenv("DV_SMALL_TILE_KMIN") ? std::atoi(std::getenv("DV_SMALL_TILE_KMIN")) : 0;
+  static const int kmin = dv_ab_env("DV_SMALL_TILE_KMIN") ? std::atoi(dv_ab_env("DV_SMALL_TILE_KMIN")) : 0;
   // (an 8-wave 64x64 tile with a 4-deep ring, config 17, was -8 % per launch in isolation but
   // neutral end to end, 417 vs 418 img/s: it stays a tuner-only config)
   if (a.OCpad % 64 == 0 && a.OC > 16 && mn <= 3000000LL && a.Kpad >= kmin) return 8;
@@ -1909,7 +1909,7 @@ static int dma_bn(const ConvArgs& a, hipStream_t s) {
   auto nwg = [&](int BM, int BN) { return (long long)((a.M + BM - 1) / BM) * (a.OCpad / BN); };
   if (a.OCpad % 256 == 0 && a.OC > 128) {
     {  // DV_KW3_TILE=512x128 (per launch): the 512 x 128 KW3P tile for these shapes too (A/B)
-      const char* kt = std::getenv("DV_KW3_TILE");
+      const char* kt = dv_ab_env("DV_KW3_TILE");
       if (kt && std::strcmp(kt, "512x128") == 0) {
         const int rc = kw3_try<DT, AMODE, EPI, 128, 512>(a, s);
         if (rc != -4) return rc;

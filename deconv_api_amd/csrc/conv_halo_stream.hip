@@ -852,7 +852,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_hs16_kernel(const ConvArgs a, 
 // weight ring depth (slots; B(k + ring - 1) is prefetched at step k). DV_HS_RING = 3 / 4 / 5 (A/B)
 static int hs_ring() {
   static int v = [] {
-    const char* e = std::getenv("DV_HS_RING");
+    const char* e = dv_ab_env("DV_HS_RING");
     const int r = e ? std::atoi(e) : 3;
     return r == 4 || r == 5 ? r : 3;
   }();
@@ -871,10 +871,10 @@ static int hs_ring() {
 
 int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used) {
   if (lepi_used) *lepi_used = false;  // set when the LDS-staged epilogue (the only one with 1-bit masks) runs
-  if (std::getenv("DV_NO_HS") != nullptr) return -4;
+  if (dv_ab_env("DV_NO_HS") != nullptr) return -4;
   // 192 / 256 padded output channels (InceptionV3 conv2d_5: 96 -> 192): two launches over the
   // channel halves [0, 128) and [128, OCpad), each re-reading the (small) input halo
-  if ((a.OCpad == 192 || a.OCpad == 256) && a.OC > 128 && epi == CONV_E_BF16 && std::getenv("DV_NO_HS_SPLIT") == nullptr) {
+  if ((a.OCpad == 192 || a.OCpad == 256) && a.OC > 128 && epi == CONV_E_BF16 && dv_ab_env("DV_NO_HS_SPLIT") == nullptr) {
     ConvArgs a1 = a, a2 = a;
     a1.OC = 128;
     a1.OCpad = 128;
@@ -912,7 +912,7 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used
                a.dtype != DT_BF16 || (reinterpret_cast<uintptr_t>(a.out_code) & 3)))
     return -4;
   // exact 16 x 16 tiling of the output (OC % 4 == 0: whole 8-B channel quads) -> hs16
-  if (a.OH % 16 == 0 && a.OW % 16 == 0 && a.OC % 4 == 0 && std::getenv("DV_NO_HS16") == nullptr) {
+  if (a.OH % 16 == 0 && a.OW % 16 == 0 && a.OC % 4 == 0 && dv_ab_env("DV_NO_HS16") == nullptr) {
     const int t16x = a.OW / 16, t16y = a.OH / 16;
     const long long n16 = (long long)a.N * t16x * t16y;
     if (n16 <= 0 || n16 > 0x7fffffffLL) return -2;
@@ -921,7 +921,7 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used
   hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_, OCT_, POOL_, false, OCT_ == 64 ? 3 : 1, LEPI_>), g16, b16, 0, s, a, t16x, \
                      t16y)
     // the LDS-staged 16-B store epilogue (DV_HS16_EPI=reg: the register layout's 8-B stores, A/B; read per launch)
-    const char* he = std::getenv("DV_HS16_EPI");
+    const char* he = dv_ab_env("DV_HS16_EPI");
     const bool lepi = !pool && !(he && std::strcmp(he, "reg") == 0) && a.OC % 8 == 0 && a.out_ld % 8 == 0 &&
                       !(reinterpret_cast<uintptr_t>(a.out) & 15) &&
                       (!a.emask || (a.emask_ld % 8 == 0 && !(reinterpret_cast<uintptr_t>(a.emask) & 15)));
@@ -955,7 +955,7 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used
   const dim3 grid((unsigned)nwg), block(512);
   const int ring = hs_ring();
   // the LDS-staged 16-B store epilogue (DV_HS16_EPI=reg: the register layout's 8-B stores, A/B; per launch)
-  const char* he = std::getenv("DV_HS16_EPI");
+  const char* he = dv_ab_env("DV_HS16_EPI");
   const bool lepi = !pool && ring == 3 && !(he && std::strcmp(he, "reg") == 0) && a.OC % 8 == 0 && a.out_ld % 8 == 0 &&
                     !(reinterpret_cast<uintptr_t>(a.out) & 15) &&
                     (!a.emask || (a.emask_ld % 8 == 0 && !(reinterpret_cast<uintptr_t>(a.emask) & 15)));
@@ -991,38 +991,6 @@ int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used
 #undef HS_LEPI
   return (int)hipGetLastError();
 }
-
-// unpool (pooled map + switch codes, ReLU) -> 3x3 conv on the hs16 kernel: the deconvnet's conv-down
-// of a pooled signal at maps whose full-resolution sides are multiples of 16 (< 0: unsupported).
-// Opt-in (DV_HSU=1): on VGG16 block1_conv2.down (224^2, 64 -> 64, only 2 channel chunks per tile, so the
-// synchronous first expansion is not amortized) it measured 5.23 ms vs 4.57 ms for the weight-resident
-// halo kernel (profiles/layers_r1_hsu_{off,on}.txt); the 128-channel unpools are fused into the
-// producing conv-down's epilogue instead (ucode).
-int conv3x3_hs_unpool_launch(const ConvArgs& a, hipStream_t s) {
-  const char* on = std::getenv("DV_HSU");
-  if (on == nullptr || std::atoi(on) == 0 || std::getenv("DV_NO_HSU") != nullptr) return -4;
-  if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.OH || a.W != a.OW ||
-      a.H % 16 || a.W % 16 || a.C % 32 || a.x_ld % 8 || (a.OCpad != 64 && a.OCpad != 128) || a.OC % 4 ||
-      !a.relu_in || a.code == nullptr || a.code_div < 1 || a.N % a.code_div || a.accumulate || a.mask || a.res ||
-      a.emask || a.ws || a.stats || a.ucode || a.out_ld % 4 || (reinterpret_cast<uintptr_t>(a.out) & 7) ||
-      (reinterpret_cast<uintptr_t>(a.x) & 15) || (reinterpret_cast<uintptr_t>(a.bias) & 15) ||
-      (reinterpret_cast<uintptr_t>(a.code) & 15) || (long long)a.Kpad < 9LL * a.C ||
-      (long long)(a.H / 2) * (a.W / 2) * a.x_ld * 2 > 0x7FFFFFF0LL)
-    return -4;
-  const int t16x = a.W / 16, t16y = a.H / 16;
-  const long long n16 = (long long)a.N * t16x * t16y;
-  if (n16 <= 0 || n16 > 0x7fffffffLL) return -2;
-  const dim3 g16((unsigned)n16), b16(256);
-  if (a.dtype == DT_F16) {
-    if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_F16, 128, false, true>), g16, b16, 0, s, a, t16x, t16y);
-    else hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_F16, 64, false, true>), g16, b16, 0, s, a, t16x, t16y);
-  } else {
-    if (a.OCpad == 128) hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_BF16, 128, false, true>), g16, b16, 0, s, a, t16x, t16y);
-    else hipLaunchKernelGGL((conv3x3_hs16_kernel<DT_BF16, 64, false, true>), g16, b16, 0, s, a, t16x, t16y);
-  }
-  return (int)hipGetLastError();
-}
-
 
 // fused VGG16 stem (block1_conv1 -> block1_conv2 -> 2x2 max-pool + switch): the hs16 pool kernel with the
 // halo computed from the RGB image (STEM above). a: the SECOND conv's geometry (C = OC = 64, pad 1)

@@ -123,8 +123,8 @@ __global__ void __launch_bounds__(WM * WN * 64, 4) conv_pw_kernel(const ConvArgs
 
 // < 0: not a persistent-pointwise problem (the caller falls back to the LDS-DMA kernel)
 int conv_pw_launch(const ConvArgs& a, hipStream_t s) {
-  static const bool off = std::getenv("DV_NO_PW") != nullptr;
-  static const long long min_tiles = std::getenv("DV_PW_MIN_TILES") ? std::atoll(std::getenv("DV_PW_MIN_TILES")) : 0;
+  static const bool off = dv_ab_env("DV_NO_PW") != nullptr;
+  static const long long min_tiles = dv_ab_env("DV_PW_MIN_TILES") ? std::atoll(dv_ab_env("DV_PW_MIN_TILES")) : 0;
   if (off || g_cfg > 0) return -4;
   if (a.KH != 1 || a.KW != 1 || a.stride != 1 || a.pad_h != 0 || a.pad_w != 0 || a.H != a.OH || a.W != a.OW ||
       a.C % 64 != 0 || a.Kpad != a.C || a.K != a.C || a.mask || a.code || a.ucode || a.ws || a.stats ||
@@ -147,7 +147,7 @@ int conv_pw_launch(const ConvArgs& a, hipStream_t s) {
   // per CU (config 5 +0.7 %, config 3 unchanged, profiles/dream_r4_pw_min_tiles.txt)
   if (tiles_total < (min_tiles > 0 ? min_tiles : cus) || tiles_total > 0x7fffffffLL) return -4;
   // DV_PW_WG_PER_CU: persistent workgroups per CU (2 by default: each holds 64 KiB of LDS ring)
-  static const long long wpc = std::getenv("DV_PW_WG_PER_CU") ? std::max(1LL, std::atoll(std::getenv("DV_PW_WG_PER_CU"))) : 2;
+  static const long long wpc = dv_ab_env("DV_PW_WG_PER_CU") ? std::max(1LL, std::atoll(dv_ab_env("DV_PW_WG_PER_CU"))) : 2;
   const unsigned G = (unsigned)std::min<long long>(tiles_total, wpc * cus);
   if (BN == 128) {
     if (a.dtype == DT_F16)

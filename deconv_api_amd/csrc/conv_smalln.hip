@@ -1053,7 +1053,7 @@ int conv3x3_c8_stream_launch(const ConvArgs& a, hipStream_t s) {
 
 static int stream_variant() {
   static int v = [] {
-    const char* e = std::getenv("DV_STREAM_P");  // measured: P=1 (3 WG/CU) 1.57 ms, P=2 1.60, P=3 1.94
+    const char* e = dv_ab_env("DV_STREAM_P");  // measured: P=1 (3 WG/CU) 1.57 ms, P=2 1.60, P=3 1.94
     return e ? std::atoi(e) : 1;
   }();
   return v;
@@ -1100,7 +1100,7 @@ int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, b
   if (!narrow && a.OCpad != 64) return -5;
   // v2: unpool + 64 -> 64 with a 16-B aligned bf16 output of 64-channel rows (block1_conv2.down)
   if (unpool && !narrow && epi == CONV_E_BF16 && a.OC == 64 && a.out_ld % 8 == 0 && a.x_ld % 8 == 0 &&
-      (a.H % 2) == 0 && (a.W % 2) == 0 && std::getenv("DV_HALO_V1") == nullptr) {
+      (a.H % 2) == 0 && (a.W % 2) == 0) {
     static const int cus = [] {
       int dev = 0, n = 256;
       if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1113,7 +1113,7 @@ int conv3x3_halo_launch(const ConvArgs& a, int unpool, int epi, hipStream_t s, b
                        a);
     return (int)hipGetLastError();
   }
-  if (!unpool && narrow && std::getenv("DV_HALO_V1") == nullptr) {  // row-streaming strips
+  if (!unpool && narrow) {  // row-streaming strips
     const long long nwg = (long long)a.N * ((a.W + ST_W - 1) / ST_W);
     if (nwg <= 0 || nwg > 0x7fffffffLL) return -2;
     const int P = stream_variant();
@@ -1168,9 +1168,9 @@ int conv3x3_unpool_z_launch(const ConvArgs& a, hipStream_t s) {
   const long long ntiles = (long long)a.N * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   if (ntiles <= 0 || ntiles > 0x7fffffffLL) return -2;
   // DV_TAIL_V: variant bits (see the kernel); 3 by default, 0 = the round-4 schedule (A/B)
-  const char* tve = std::getenv("DV_TAIL_V");  // per launch: tests switch it in one process
+  const char* tve = dv_ab_env("DV_TAIL_V");  // per launch: tests switch it in one process
   int tv = tve ? std::atoi(tve) : 3;
-  if ((tv & ~3) && std::getenv("DV_ALLOW_WRONG_ABLATION") == nullptr) tv &= 3;  // ablation bits: tools only
+  if ((tv & ~3) && dv_ab_env("DV_ALLOW_WRONG_ABLATION") == nullptr) tv &= 3;  // ablation bits: tools only
   const dim3 g((unsigned)std::min<long long>(ntiles, cus));
   if (tv == 0) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 0>), g, dim3(512), 0, s, a);
   else if (tv == 1) hipLaunchKernelGGL((conv3x3_unpool_c64_v2_kernel<true, 1>), g, dim3(512), 0, s, a);

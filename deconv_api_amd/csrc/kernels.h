@@ -4,6 +4,16 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
+// Runtime A/B switch of a measured alternative (deconv_api_amd/knobs.py ABLATION): the variable is read
+// only when DV_ABLATIONS=1, so a serving / benchmark process takes one dispatch per shape whatever its
+// environment holds; tools/*_ab.py and the variant tests set DV_ABLATIONS=1. (Host code only.)
+static inline const char* dv_ab_env(const char* name) {
+  const char* on = std::getenv("DV_ABLATIONS");
+  return (on != nullptr && on[0] == '1' && on[1] == 0) ? std::getenv(name) : nullptr;
+}
+
 namespace dv {
 
 // A-operand (implicit-GEMM gather) modes of the conv kernel.
@@ -243,6 +253,4 @@ int conv3x3_stem_pool_launch(const ConvArgs& a, hipStream_t s);
 // halo-stream 3x3 s1 p1 conv, C % 32 == 0 -> OCpad 64 / 128, 16-bit out or fused 2x2 max-pool +
 // switch (epi CONV_E_BF16 / CONV_E_POOL; < 0: unsupported)
 int conv3x3_hs_launch(const ConvArgs& a, int epi, hipStream_t s, bool* lepi_used = nullptr);
-// unpool (pooled map + switch codes, input ReLU) -> 3x3 conv, 16-bit out, on the hs16 kernel (< 0: unsupported)
-int conv3x3_hs_unpool_launch(const ConvArgs& a, hipStream_t s);
 }  // namespace dv

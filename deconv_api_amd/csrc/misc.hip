@@ -218,7 +218,7 @@ int seed_deconv3x3_launch(const float* S, const int* f, const uint16_t* wt, uint
   if (Cin % 8 != 0 || B <= 0 || F <= 0) return -1;
   const long long total = (long long)B * H * W * (Cin / 8);
   if (total >= (1LL << 31) || (long long)F * 9 * Cin >= (1LL << 31)) return -2;
-  if ((long long)H * W <= kSeedMaxHW && Cin / 8 <= 256 && std::getenv("DV_SEED_V1") == nullptr) {
+  if ((long long)H * W <= kSeedMaxHW && Cin / 8 <= 256) {
     if (f16)
       hipLaunchKernelGGL(seed_deconv3x3_smallmap_kernel<DT_F16>, dim3((unsigned)B), dim3(256), 0, s, S, f, wt, out, H, W,
                          Cin, F);

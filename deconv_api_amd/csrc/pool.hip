@@ -389,7 +389,7 @@ int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* i
   if (x_ld % 8 || y_ld % 8 || x_ld < C || y_ld < C) return -1;
   if (acc && dir != 1) return -1;
   // DV_NO_POOL_UNROLL=1 (read per call): backward passes on the generic window loop (A/B, bit-identity tests)
-  const int generic = std::getenv("DV_NO_POOL_UNROLL") != nullptr;
+  const int generic = dv_ab_env("DV_NO_POOL_UNROLL") != nullptr;
   const PoolGeom g{N, H, W, C, OH, OW, k, s, pad, x_ld, y_ld, bias, relu, acc, generic};
   return dtype == DT_F16 ? pool_dt<DT_F16>(kind, dir, in, out, idx, g, st)
                          : pool_dt<DT_BF16>(kind, dir, in, out, idx, g, st);

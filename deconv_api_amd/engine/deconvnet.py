@@ -32,15 +32,15 @@ from ..models.vgg16 import VGG16Runtime, LayerSpec
 from ..utils import tracing
 
 VALID_MODES = ("all", "max")
-# DV_DECONV_STREAMS=S: a GPU batch of >= DV_DECONV_SPLIT_MIN images runs as S sub-batches on S streams
-# forked from and joined back into the caller's stream (graph branches when captured); per-image top-k
-# makes the halves independent
-DECONV_STREAMS = max(1, int(os.environ.get("DV_DECONV_STREAMS", "1")))
-DECONV_SPLIT_MIN = int(os.environ.get("DV_DECONV_SPLIT_MIN", "64"))
-# DV_UNPOOL_CONSUMER_MAXC: conv-downs consuming an unpooled map with at most this many input channels
-# expand the unpool themselves (64: block1_conv2.down's fused tail; 128 adds block2_conv2.down on the
-# hs16 unpool path, which also needs DV_HSU=1); wider consumers get the map from the producer's epilogue
-UNPOOL_CONSUMER_MAXC = int(os.environ.get("DV_UNPOOL_CONSUMER_MAXC", "64"))
+# a GPU batch of >= DECONV_SPLIT_MIN images runs as DECONV_STREAMS sub-batches on that many streams forked
+# from and joined back into the caller's stream (graph branches when captured; per-image top-k makes the
+# parts independent). 1 = off: measured no gain on config 2 (docs/KERNELS.md); kept for tests / tools that
+# set the attributes
+DECONV_STREAMS = 1
+DECONV_SPLIT_MIN = 64
+# conv-downs consuming an unpooled map with at most this many input channels expand the unpool themselves
+# (64: block1_conv2.down's fused tail); wider consumers get the map from the producer's epilogue
+UNPOOL_CONSUMER_MAXC = 64
 # DV_POOL_SPLIT=name,...: these convs run WITHOUT the fused pool epilogue (plain conv, which may take the
 # persistent KW3P kernel, then the standalone 2x2 max-pool/switch kernel) on the GPU
 POOL_SPLIT = frozenset(n for n in os.environ.get("DV_POOL_SPLIT", "").split(",") if n)

@@ -28,6 +28,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from .. import knobs
 from ..ops import native
 from ..runtime.capture import capture
 from ..utils.logging import get_logger
@@ -36,7 +37,7 @@ from ..ops.autograd import loss_tap, premasked_grads, sumsq_core
 # DV_DREAM_FUSED=0: the step tail (loss, normalization, update) as torch ops instead of the fused
 # HIP kernels (A/B); DV_DREAM_GRAPHS: hipGraph cache entries (octave shapes) kept, LRU-evicted
 log = get_logger("deconv_api_amd.deepdream")
-FUSED_STEP = os.environ.get("DV_DREAM_FUSED", "1") != "0"
+FUSED_STEP = knobs.ablation("DV_DREAM_FUSED", "1") != "0"
 GRAPH_CACHE = int(os.environ.get("DV_DREAM_GRAPHS", "8"))
 # DV_DREAM_OCTAVE_GRAPH=0: one graph per step, replayed `iterations` times (A/B). Default: the
 # whole octave (every step) is ONE captured graph - each separate replay costs a ~140 us launch
@@ -47,10 +48,10 @@ OCTAVE_GRAPH = os.environ.get("DV_DREAM_OCTAVE_GRAPH", "1") != "0"
 # (images are independent: per-image loss, normalisation and max-loss flag). Measured config 3
 # (B=64, 299^2): 1 -> 327, 2 -> 356, 4 -> 232 img/s (4 side streams + the default stream exceed the
 # 4 hardware queues per process).
-SPLIT = int(os.environ.get("DV_DREAM_SPLIT", "2"))
+SPLIT = int(knobs.ablation("DV_DREAM_SPLIT", "2"))
 # DV_DREAM_TAPS=0: intermediate loss layers get their loss gradient through autograd's sum (A/B);
 # default: a loss tap adds it into the gradient from above in the loss-gradient kernel itself
-TAPS = os.environ.get("DV_DREAM_TAPS", "1") != "0"
+TAPS = knobs.ablation("DV_DREAM_TAPS", "1") != "0"
 # tiled multi-rank octaves: capture the per-step all-gathers inside the octave's hipGraph
 # (DV_TILE_CAPTURE_COLL=0: per-step graphs + eager collectives); DV_TILE_COLLECTIVE=1 takes the
 # collective path even on a 1-rank process group (torchrun rehearsal of the multi-rank octave)
@@ -58,11 +59,11 @@ CAPTURE_COLLECTIVE = os.environ.get("DV_TILE_CAPTURE_COLL", "1") != "0"
 TILE_COLLECTIVE = os.environ.get("DV_TILE_COLLECTIVE", "0") == "1"
 # DV_DREAM_FUSED_LOSS=0: separate forward loss-partial launches (A/B); default: every loss layer's
 # partial sums of squares come out of its loss-gradient kernel (one launch per loss layer, not two)
-FUSED_LOSS = os.environ.get("DV_DREAM_FUSED_LOSS", "1") != "0"
+FUSED_LOSS = knobs.ablation("DV_DREAM_FUSED_LOSS", "1") != "0"
 LOSS_PARTS = 32
 # DV_DREAM_OCTAVE_RESIZE=0: octave transitions as F.interpolate + ATen adds (A/B); default: one
 # octave_resize HIP launch per transition writing the next octave's static inputs directly
-OCTAVE_RESIZE = os.environ.get("DV_DREAM_OCTAVE_RESIZE", "1") != "0"
+OCTAVE_RESIZE = knobs.ablation("DV_DREAM_OCTAVE_RESIZE", "1") != "0"
 # DV_TILE_CHUNKS: a rank's units per tiled step run as this many chunks when the step all-gathers
 # (several ranks): chunk c's pack all-gather is issued (async, captured into the octave graph) right
 # behind chunk c's network, tile_update waits for all of them. 1: one all-gather after the whole

@@ -15,6 +15,7 @@ from typing import Dict, Iterable, List, Optional
 
 import torch
 
+from .. import knobs
 from ..ops.autograd import ConvUnit, avg_pool, cat_channels, max_pool
 from ..ops.inception import InceptionBlock
 
@@ -22,7 +23,7 @@ from ..ops.inception import InceptionBlock
 # ops/inception.py (the oracle-shaped path; GPU tests compare the two). Removed after measuring:
 # branches on side streams (no gain in a graph, profiles/kstats_c3_r2_branch_streams.txt) and
 # conv2d_4/5 padded to 96 channels (neutral, profiles/dream_c3_r2_padstem.txt).
-FUSED_BLOCKS = os.environ.get("DV_INCEPTION_FUSED", "1") != "0"
+FUSED_BLOCKS = knobs.ablation("DV_INCEPTION_FUSED", "1") != "0"
 
 MIXED = [f"mixed{i}" for i in range(11)]
 

@@ -18,23 +18,24 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from .. import knobs
 from . import native
 from .conv import ConvWeights, bits_flags, conv2d, pad_channels_oihw, transpose_subpixel
 
 # DV_RELU_BITS=0: bottleneck outputs keep no 1-bit ReLU masks (the next block's input-gradient epilogue
 # reads the 16-bit activation as its mask again; A/B)
-RELU_BITS = os.environ.get("DV_RELU_BITS", "1") != "0"
+RELU_BITS = knobs.ablation("DV_RELU_BITS", "1") != "0"
 # DV_SUBPIXEL=0 falls back to the direct transposed gather for strided dgrads (A/B testing)
-SUBPIXEL = os.environ.get("DV_SUBPIXEL", "1") != "0"
+SUBPIXEL = knobs.ablation("DV_SUBPIXEL", "1") != "0"
 # DV_COL2IM=0 disables the GEMM + col2im input gradient of few-channel strided convs (A/B testing)
-COL2IM = os.environ.get("DV_COL2IM", "1") != "0"
+COL2IM = knobs.ablation("DV_COL2IM", "1") != "0"
 # DV_STEM_DIRECT=0: InceptionV3's conv2d_1 (3 -> 32, 3x3 / 2) on the GEMM (+ col2im) path (A/B)
-STEM_DIRECT = os.environ.get("DV_STEM_DIRECT", "1") != "0"
+STEM_DIRECT = knobs.ablation("DV_STEM_DIRECT", "1") != "0"
 # DV_STEM_FUSED=0: ResNet-50 conv1's input gradient as GEMM (cols to HBM) + col2im (A/B)
-STEM_FUSED = os.environ.get("DV_STEM_FUSED", "1") != "0"
+STEM_FUSED = knobs.ablation("DV_STEM_FUSED", "1") != "0"
 # DV_STEM7=0: ResNet-50 conv1's forward on the generic implicit GEMM instead of the tap-paired MFMA
 # kernel (csrc/conv_stem7.hip) (A/B)
-STEM7 = os.environ.get("DV_STEM7", "1") != "0"
+STEM7 = knobs.ablation("DV_STEM7", "1") != "0"
 
 
 _PREMASKED = [False]
@@ -216,7 +217,7 @@ def _dgrad(unit: ConvUnit, gy, mask, in_hw, emask=None, ebits=None):
 # strided-conv input gradients below this many (full transposed-GEMM) FLOPs run as ONE transposed
 # conv written straight into its destination (accumulate / x-mask epilogue) instead of s^2
 # sub-pixel GEMMs + copies: small maps are launch-latency bound, not MFMA bound
-STRIDED_DIRECT_FLOPS = float(os.environ.get("DV_STRIDED_DIRECT_GFLOP", "60")) * 1e9
+STRIDED_DIRECT_FLOPS = float(knobs.ablation("DV_STRIDED_DIRECT_GFLOP", "60")) * 1e9
 
 
 def strided_direct(unit: ConvUnit, gy, in_hw) -> bool:

@@ -35,12 +35,13 @@ from typing import Dict, List, Sequence
 import torch
 import torch.nn.functional as F
 
+from .. import knobs
 from . import native
 from .autograd import _PREMASKED, ConvUnit, _is_relu_out, _tag, dgrad_strided_into
 from .conv import conv2d, conv_group, conv_group_paused
 
 # DV_MERGE_B1=0: the b1 branch as its own GEMM (A/B); default: it joins the merged head GEMM forward
-MERGE_B1 = os.environ.get("DV_MERGE_B1", "1") != "0"
+MERGE_B1 = knobs.ablation("DV_MERGE_B1", "1") != "0"
 
 
 def _pool_out(L: int, k: int, s: int, p: int) -> int:

@@ -22,6 +22,8 @@ from typing import Dict, Sequence
 
 import torch
 
+from .. import knobs
+
 _lock = threading.Lock()
 _copy_streams: Dict[int, torch.cuda.Stream] = {}
 
@@ -64,7 +66,7 @@ def independent_stream(device, avoid: Sequence[torch.cuda.Stream], tries: int = 
     outside graph capture (it synchronizes the device). Falls back to a plain new stream when every
     candidate shares a queue (fewer hardware queues than streams in use)."""
     dev = torch.device(device)
-    if os.environ.get("DV_NO_STREAM_PROBE") == "1":  # A/B: plain pool streams
+    if knobs.ablation("DV_NO_STREAM_PROBE") == "1":  # A/B: plain pool streams
         return torch.cuda.Stream(dev)
     torch.cuda.synchronize(dev)
     first = None

@@ -4,6 +4,10 @@ import sys
 import pytest
 import torch
 
+# variant tests switch measured alternatives with their DV_* A/B variables, which the package honours
+# only in ablation mode (deconv_api_amd/knobs.py); set before any package module reads its switches
+os.environ.setdefault("DV_ABLATIONS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

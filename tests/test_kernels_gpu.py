@@ -302,11 +302,11 @@ def test_conv_unpool_out_epilogue(native_lib, N, H, C, OC, div):
 
 
 @pytest.mark.parametrize("N,H,W,C,OC,div", [(4, 224, 224, 64, 64, 4), (2, 64, 96, 128, 128, 2), (3, 48, 32, 64, 120, 1)])
-def test_conv_hs_unpool(native_lib, N, H, W, C, OC, div):
-    """unpool (pooled map + switch codes, input ReLU) -> conv on the hs16 kernel (pooled halo staged by
-    LDS-DMA, expanded in LDS) vs the fp32 reference and vs the other kernels (DV_NO_HSU)."""
-    import os
-
+def test_conv_unpool_input(native_lib, N, H, W, C, OC, div):
+    """unpool (pooled map + switch codes, input ReLU) -> conv, on whichever kernel the router picks for
+    the shape (weight-resident halo kernel, or the materialized unpool + DMA conv), vs the fp32
+    reference. (Round 6 removed the opt-in hs16 unpool kernel, DV_HSU: 5.23 vs 4.57 ms on its one
+    candidate layer, profiles/layers_r1_hsu_{off,on}.txt.)"""
     g = torch.Generator().manual_seed(53)
     p = torch.randn(N, H // 2, W // 2, C, generator=g)  # signed: the input ReLU matters
     code = torch.randint(0, 4, (N // div, H // 2, W // 2, C), generator=g, dtype=torch.uint8)
@@ -314,14 +314,8 @@ def test_conv_hs_unpool(native_lib, N, H, W, C, OC, div):
     kw = dict(relu=True, relu_in=True, in_mode="unpool", code_div=div, use_bias=False)
     ref = ops.conv2d(_bf(p), cw, code=code, **kw)
     pd, cd, cwd = p.to(torch.bfloat16).to(DEV), code.to(DEV), cw.to_device(DEV)
-    os.environ["DV_HSU"] = "1"  # opt-in kernel (read per launch)
-    try:
-        got = ops.conv2d(pd, cwd, code=cd, **kw)
-    finally:
-        del os.environ["DV_HSU"]
+    got = ops.conv2d(pd, cwd, code=cd, **kw)
     assert got.shape == (N, H, W, OC) and _rel(got, ref) < 1e-2
-    alt = ops.conv2d(pd, cwd, code=cd, **kw)
-    assert _rel(got, alt) < 1e-2
 
 
 @pytest.mark.parametrize("N,H,W,C,OC,dt", [(200, 28, 28, 32, 256, torch.bfloat16), (90, 14, 13, 96, 512, torch.bfloat16),

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B: stream probing (independent copy stream) vs plain pool streams vs 8 hardware queues, config 2 bench.py
 set -o pipefail
+export DV_ABLATIONS=1  # the A/B switches below are honoured only in ablation mode (knobs.py)
 O=gpurun_out/ab_streams
 mkdir -p $O
 for i in 1 2 3; do

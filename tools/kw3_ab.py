@@ -11,6 +11,8 @@ time over rounds and the conv TF/s.
 import argparse
 import json
 import os
+
+os.environ.setdefault("DV_ABLATIONS", "1")  # this tool A/Bs switches of deconv_api_amd/knobs.py ABLATION
 import statistics
 import sys
 

@@ -7,6 +7,8 @@ the two launches it replaces, at the config-2 shape (256 x 224^2), and check the
 import argparse
 import json
 import os
+
+os.environ.setdefault("DV_ABLATIONS", "1")  # this tool A/Bs switches of deconv_api_amd/knobs.py ABLATION
 import sys
 
 import torch

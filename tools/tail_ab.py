@@ -8,6 +8,8 @@ stores, 8 = no halo expansion (csrc/conv_smalln.hip). Times include the zsum3x3 
 import argparse
 import json
 import os
+
+os.environ.setdefault("DV_ABLATIONS", "1")  # this tool A/Bs switches of deconv_api_amd/knobs.py ABLATION
 import statistics
 import sys
 
