@@ -42,8 +42,10 @@ DECONV_SPLIT_MIN = 64
 # (64: block1_conv2.down's fused tail); wider consumers get the map from the producer's epilogue
 UNPOOL_CONSUMER_MAXC = 64
 # DV_POOL_SPLIT=name,...: these convs run WITHOUT the fused pool epilogue (plain conv, which may take the
-# persistent KW3P kernel, then the standalone 2x2 max-pool/switch kernel) on the GPU
-POOL_SPLIT = frozenset(n for n in os.environ.get("DV_POOL_SPLIT", "").split(",") if n)
+# persistent KW3P kernel, then the standalone 2x2 max-pool/switch kernel) on the GPU. Default: block3/4's
+# last convs (config 2: 7724 vs 7680 img/s mean of 3 interleaved pairs, profiles/final_r6_validation.txt;
+# their fused-pool convs ran on the generic DMA kernel); DV_POOL_SPLIT= (empty) fuses every pool
+POOL_SPLIT = frozenset(n for n in os.environ.get("DV_POOL_SPLIT", "block3_conv3,block4_conv3").split(",") if n)
 
 
 class UnknownLayerError(KeyError):
