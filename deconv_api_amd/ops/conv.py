@@ -1,6 +1,10 @@
 """Convolution op surface: packed weights + NHWC conv with fused prologues/epilogues.
 
-Device tensors run the MFMA implicit-GEMM kernel in ``csrc/conv_igemm.hip``; CPU tensors run a
+Device tensors (bf16 or fp16) go through ``csrc/bindings.cpp:conv``, which routes each shape to one
+gfx950 kernel family: the LDS-DMA implicit GEMM and its KW3P shared-tap / stream-K variants
+(``conv_dma*.hip``, ``conv_dma_impl.h``), the halo-stream 3x3 kernels (``conv_halo_stream.hip``),
+the 64-channel halo / row-streaming kernels (``conv_smalln.hip``), the persistent 1x1 kernel
+(``conv_pw.hip``), with ``conv_igemm.hip`` as the register-staged fallback. CPU tensors run a
 PyTorch reference of exactly the same math (fp32 compute, output rounded to the input dtype),
 which is both the CPU execution path and the oracle the GPU tests compare against.
 
