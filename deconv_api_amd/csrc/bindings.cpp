@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <optional>
 
 namespace {
 
@@ -987,7 +988,8 @@ py::bytes data_url_b64decode(py::str uri) {
   std::string out, err;
   bool ok;
   {
-    py::gil_scoped_release nogil;
+    std::optional<py::gil_scoped_release> nogil;  // (large payloads only: see url_unquote_plus)
+    if (n >= (1 << 15)) nogil.emplace();
     ok = dvjpeg::data_url_b64decode(p, (size_t)n, out, err);
   }
   if (!ok) throw py::value_error(err);
@@ -1005,7 +1007,10 @@ py::bytes url_unquote_plus(py::str s) {
   if (p == nullptr) throw py::error_already_set();
   std::string out;
   {
-    py::gil_scoped_release nogil;
+    // the GIL goes only for large inputs: a short release hands it to a waiting thread and getting it
+    // back costs up to the switch interval (0.2 ms per call measured on tiny bodies)
+    std::optional<py::gil_scoped_release> nogil;
+    if (n >= (1 << 15)) nogil.emplace();
     out.resize((size_t)n);
     auto hex = [](char c) -> int {
       return c >= '0' && c <= '9' ? c - '0' : (c >= 'a' && c <= 'f' ? c - 'a' + 10 : (c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1));

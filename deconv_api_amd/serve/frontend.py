@@ -48,8 +48,9 @@ class _Remote:
         self.client = client
         self.cfg = cfg
 
-    async def _request(self, send) -> str:
-        """``send(cb)`` queues the request (on a codec thread); -> the owner's 200 payload."""
+    async def _request(self, send, raw: bool = False):
+        """``send(cb)`` queues the request (on a codec thread); -> the owner's 200 payload (bytes when
+        ``raw``: the data URL goes into the HTTP body as is, api/app.py)."""
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
 
@@ -60,7 +61,7 @@ class _Remote:
         st, data = await asyncio.wait_for(fut, timeout=self.cfg.request_timeout_s)
         if st != 200:
             raise RemoteError(st, data.decode("utf-8", errors="replace"))
-        return data.decode("ascii", errors="replace")
+        return data if raw else data.decode("ascii", errors="replace")
 
 
 class RemoteService(_Remote):
@@ -97,7 +98,7 @@ class RemoteService(_Remote):
         async def send(cb):
             await loop.run_in_executor(self.codec.ex, self._decode_send, uri, layer, cb)
 
-        return await self._request(send)
+        return await self._request(send, raw=True)
 
     def status(self) -> dict:
         try:

@@ -319,6 +319,7 @@ class IngestClient:
                 self.on_lost()
 
     def close(self) -> None:
+        self.on_lost = None  # a deliberate close is not a lost owner
         try:
             self.sock.shutdown(socket.SHUT_RDWR)
             self.sock.close()
