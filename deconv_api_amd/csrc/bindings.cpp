@@ -600,6 +600,46 @@ void subpixel_scatter(Tensor E, c10::optional<Tensor> emask, Tensor gx, int64_t 
            "subpixel_scatter");
 }
 
+// gx [N,H,W,C] (=|+=) the strided-conv input gradient assembled from parts[(h%s)*s + w%s] ([N, ceil-class
+// H, W, ld >= C] 16-bit, or None for an empty class), zeroed where emask <= 0 (ops/autograd.py _subpixel_dgrad)
+void subpixel_merge(std::vector<c10::optional<Tensor>> parts, c10::optional<Tensor> emask, Tensor gx, int64_t s,
+                    bool accumulate) {
+  check_cuda(gx, "gx");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gx.device());
+  TORCH_CHECK(gx.dim() == 4 && gx.is_contiguous() && gx.size(3) % 8 == 0 && (s == 1 || s == 2) &&
+                  (int64_t)parts.size() == s * s,
+              "subpixel_merge: gx [N,H,W,C] contiguous, C % 8, s in {1, 2}, s^2 parts");
+  const int64_t N = gx.size(0), H = gx.size(1), W = gx.size(2), C = gx.size(3);
+  const uint16_t* p[4] = {nullptr, nullptr, nullptr, nullptr};
+  int hc[4] = {0, 0, 0, 0}, wc[4] = {0, 0, 0, 0}, ld[4] = {0, 0, 0, 0};
+  for (int k = 0; k < (int)parts.size(); ++k) {
+    if (!parts[k].has_value()) continue;
+    const Tensor& t = *parts[k];
+    check_cuda(t, "part");
+    const int rh = k / (int)s, rw = k % (int)s;
+    const int64_t want_h = (H - rh + s - 1) / s, want_w = (W - rw + s - 1) / s;
+    TORCH_CHECK(t.dim() == 4 && t.scalar_type() == gx.scalar_type() && t.size(0) == N && t.size(1) == want_h &&
+                    t.size(2) == want_w && t.stride(3) == 1 && t.stride(2) >= C && t.stride(2) % 8 == 0 &&
+                    t.stride(1) == t.size(2) * t.stride(2) && t.stride(0) == t.size(1) * t.stride(1) &&
+                    reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+                "subpixel_merge: part k = [N, ceil((H - rh) / s), ceil((W - rw) / s), >= C] dense pixels, 16-B aligned");
+    p[k] = reinterpret_cast<const uint16_t*>(t.data_ptr());
+    hc[k] = (int)t.size(1);
+    wc[k] = (int)t.size(2);
+    ld[k] = (int)t.stride(2);
+  }
+  const uint16_t* mp = nullptr;
+  if (emask.has_value()) {
+    check_cuda(*emask, "emask");
+    TORCH_CHECK(emask->sizes() == gx.sizes() && emask->is_contiguous() && emask->scalar_type() == gx.scalar_type(),
+                "subpixel_merge: emask like gx");
+    mp = reinterpret_cast<const uint16_t*>(emask->data_ptr());
+  }
+  check_rc(dv::subpixel_merge_launch(p, hc, wc, ld, mp, reinterpret_cast<uint16_t*>(gx.data_ptr()), (int)N, (int)H,
+                                     (int)W, (int)C, (int)s, accumulate ? 1 : 0, dt_of(gx), cur_stream()),
+           "subpixel_merge");
+}
+
 static int dt_of(const Tensor& t) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "expected a bf16 or fp16 tensor");
   return t.scalar_type() == at::kHalf ? dv::DT_F16 : dv::DT_BF16;
@@ -1412,6 +1452,7 @@ static const char kSourceHash[] = "DV_SOURCE_HASH:" DV_SOURCE_HASH;
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("source_hash", [] { return std::string(kSourceHash + 15); }, "sha256 of the sources this binary was built from");
+  m.def("subpixel_merge", &subpixel_merge, "strided-conv input gradient from its parity-class parts (+accumulate, emask)");
   m.def("sk_errors", &sk_errors, py::arg("reset") = false,
         "KW3P stream-K hand-offs that timed out since the last reset (their tiles are wrong)");
   m.doc() = "deconv_api_amd gfx950 (MI355X) HIP kernels";

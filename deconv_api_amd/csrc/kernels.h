@@ -169,6 +169,10 @@ int unpool2x2_launch(const uint16_t* p, const uint8_t* code, uint16_t* out, int 
 namespace dv {
 // k x k pooling (pool.hip). kind 0 max (idx = uint8 window position), 1 avg (count_include_pad=0);
 // dir 0 forward (in = x [N,H,W,C], out = y [N,OH,OW,C]), 1 backward (in = gy, out = gx)
+// strided-conv input gradient from its s x s (s <= 2) parity-class parts [N, hc, wc, ld] (nullptr: zero class),
+// optional accumulate into gx and emask (zero where emask <= 0)
+int subpixel_merge_launch(const uint16_t* const* p, const int* hc, const int* wc, const int* ld, const uint16_t* emask,
+                          uint16_t* gx, int N, int H, int W, int C, int s, int acc, int dtype, hipStream_t st);
 int subpixel_scatter_launch(const uint16_t* E, const uint16_t* emask, uint16_t* gx, int N, int H, int W, int C, int OH,
                             int OW, int s, int dtype, hipStream_t st);
 int pool_launch(int kind, int dir, const uint16_t* in, uint16_t* out, uint8_t* idx, int N, int H, int W, int C,

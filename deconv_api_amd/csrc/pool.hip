@@ -336,6 +336,54 @@ __global__ void __launch_bounds__(256) subpixel_scatter_kernel(const uint16_t* _
   }
 }
 
+// Sub-pixel merge (strided-conv input gradient assembled from its s x s parity classes, s <= 2): gx[n][h][w]
+// = part[(h % s) * s + w % s][n][h / s][w / s] (zero for a missing class), optionally += the old gx, then
+// zeroed where emask <= 0 - one pass instead of s^2 strided copies + an add + a threshold pass.
+struct SubpixelParts {
+  const uint16_t* p[4];
+  int hc[4], wc[4], ld[4];
+};
+
+template <int DT>
+__global__ void __launch_bounds__(256) subpixel_merge_kernel(const SubpixelParts parts, const uint16_t* __restrict__ emask,
+                                                             uint16_t* __restrict__ gx, int N, int H, int W, int C, int s,
+                                                             int acc) {
+  const int cpp = C >> 3;
+  const long long total = (long long)N * H * W * cpp;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int ch = (int)(t % cpp);
+    const long long pix = t / cpp;
+    const int w = (int)(pix % W);
+    const int h = (int)((pix / W) % H);
+    const long long n = pix / ((long long)W * H);
+    const int k = (h % s) * s + (w % s);
+    uint4 o = {0u, 0u, 0u, 0u};
+    const uint16_t* src = parts.p[k];
+    if (src != nullptr) {
+      const long long q = ((n * parts.hc[k] + h / s) * parts.wc[k] + w / s) * parts.ld[k] + ch * 8;
+      o = *reinterpret_cast<const uint4*>(src + q);
+    }
+    uint32_t ov[4] = {o.x, o.y, o.z, o.w};
+    if (acc) {
+      const uint4 g = *reinterpret_cast<const uint4*>(gx + pix * C + ch * 8);
+      const uint32_t gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        ov[e] = pack2<DT>(to_f<DT>(ov[e] & 0xFFFFu) + to_f<DT>(gv[e] & 0xFFFFu), to_f<DT>(ov[e] >> 16) + to_f<DT>(gv[e] >> 16));
+    }
+    if (emask) {
+      const uint4 m = *reinterpret_cast<const uint4*>(emask + pix * C + ch * 8);
+      const uint32_t mv[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = to_f<DT>(mv[e] & 0xFFFFu), hi = to_f<DT>(mv[e] >> 16);
+        ov[e] = (lo > 0.f ? (ov[e] & 0xFFFFu) : 0u) | (hi > 0.f ? (ov[e] & 0xFFFF0000u) : 0u);
+      }
+    }
+    *reinterpret_cast<uint4*>(gx + pix * C + ch * 8) = uint4{ov[0], ov[1], ov[2], ov[3]};
+  }
+}
+
 static unsigned grid_for(long long total) {
   return (unsigned)std::min<long long>((total + 255) / 256, 256LL * 32);
 }
@@ -377,6 +425,25 @@ int subpixel_scatter_launch(const uint16_t* E, const uint16_t* emask, uint16_t* 
     hipLaunchKernelGGL(subpixel_scatter_kernel<DT_F16>, dim3(grid), dim3(256), 0, st, E, emask, gx, N, H, W, C, OH, OW, s);
   else
     hipLaunchKernelGGL(subpixel_scatter_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, E, emask, gx, N, H, W, C, OH, OW, s);
+  return (int)hipGetLastError();
+}
+
+int subpixel_merge_launch(const uint16_t* const* p, const int* hc, const int* wc, const int* ld, const uint16_t* emask,
+                          uint16_t* gx, int N, int H, int W, int C, int s, int acc, int dtype, hipStream_t st) {
+  if (C % 8 != 0 || s < 1 || s > 2) return -1;
+  SubpixelParts parts{};
+  for (int k = 0; k < s * s; ++k) {
+    parts.p[k] = p[k];
+    parts.hc[k] = hc[k];
+    parts.wc[k] = wc[k];
+    parts.ld[k] = ld[k];
+    if (p[k] != nullptr && (ld[k] % 8 != 0 || ld[k] < C)) return -1;
+  }
+  const unsigned grid = grid_for((long long)N * H * W * (C / 8));
+  if (dtype == DT_F16)
+    hipLaunchKernelGGL(subpixel_merge_kernel<DT_F16>, dim3(grid), dim3(256), 0, st, parts, emask, gx, N, H, W, C, s, acc);
+  else
+    hipLaunchKernelGGL(subpixel_merge_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, parts, emask, gx, N, H, W, C, s, acc);
   return (int)hipGetLastError();
 }
 

@@ -234,6 +234,9 @@ def dgrad_strided_into(unit: ConvUnit, gy, in_hw, out: torch.Tensor, accumulate:
     if strided_direct(unit, gy, in_hw):
         return conv2d(gy, unit.bwd, stride=unit.stride, pad=unit.pad, relu=False, in_mode="transpose",
                       out_hw=in_hw, use_bias=False, out=out, accumulate=accumulate, emask=emask)
+    if out.is_cuda and SUBPIXEL and _subpixel_ok(unit, out):
+        # parity-class GEMMs merged straight into ``out`` with the accumulate and the mask in the same pass
+        return _subpixel_dgrad(gy, None, unit, in_hw, out=out, accumulate=accumulate, emask=emask)
     r = _dgrad_strided(unit, gy, None, in_hw)
     if emask is not None:
         r = torch.ops.aten.threshold_backward(r, emask, 0)
@@ -278,21 +281,40 @@ def _col2im_dgrad(gy, mask, unit: ConvUnit, in_hw):
     return gx
 
 
-def _subpixel_dgrad(gy, mask, unit: ConvUnit, in_hw):
-    """dx of a strided conv as s^2 stride-1 convs (ops.conv.transpose_subpixel), each written to its
-    parity class of dx."""
+def _subpixel_ok(unit: ConvUnit, out: Optional[torch.Tensor] = None) -> bool:
+    """The native merge takes it: stride <= 2, the classes in (rh, rw) row-major order, 8-channel rows."""
+    C = unit.fwd.cin
+    return (unit.stride <= 2 and C % 8 == 0 and len(unit.bwd_sub) == unit.stride ** 2 and
+            all((rh, rw) == (k // unit.stride, k % unit.stride) for k, (rh, rw, _, _) in enumerate(unit.bwd_sub)) and
+            (out is None or (out.is_contiguous() and out.shape[3] == C)))
+
+
+def _subpixel_dgrad(gy, mask, unit: ConvUnit, in_hw, out=None, accumulate: bool = False, emask=None):
+    """dx of a strided conv as s^2 stride-1 convs (ops.conv.transpose_subpixel), each its parity class
+    of dx. GPU: the class outputs are merged by ONE kernel (csrc/pool.hip subpixel_merge: interleave,
+    optional accumulate into ``out`` and ``emask``) instead of s^2 strided copies (+ add, + mask)."""
     s = unit.stride
     H, W = in_hw
     N = gy.shape[0]
     C = unit.fwd.cin
-    empty_class = any(cw is None for _, _, cw, _ in unit.bwd_sub)
-    gx = (torch.zeros if empty_class else torch.empty)(N, H, W, C, dtype=gy.dtype, device=gy.device)
+    native_merge = gy.is_cuda and _subpixel_ok(unit, out)
+    parts = []
     for rh, rw, cw, pd in unit.bwd_sub:
         hc, wc = len(range(rh, H, s)), len(range(rw, W, s))
         if hc == 0 or wc == 0 or cw is None:
+            parts.append(None)
             continue
-        part = conv2d(gy, cw, stride=1, pad=pd, relu=False, mask=mask, out_hw=(hc, wc), use_bias=False)
-        gx[:, rh::s, rw::s] = part[..., :C]
+        parts.append(conv2d(gy, cw, stride=1, pad=pd, relu=False, mask=mask, out_hw=(hc, wc), use_bias=False))
+    if native_merge:
+        gx = out if out is not None else torch.empty(N, H, W, C, dtype=gy.dtype, device=gy.device)
+        native.lib().subpixel_merge(parts, emask, gx, s, bool(accumulate and out is not None))
+        return gx
+    assert out is None and emask is None and not accumulate
+    empty_class = any(p is None for p in parts)
+    gx = (torch.zeros if empty_class else torch.empty)(N, H, W, C, dtype=gy.dtype, device=gy.device)
+    for (rh, rw, _, _), part in zip(unit.bwd_sub, parts):
+        if part is not None:
+            gx[:, rh::s, rw::s] = part[..., :C]
     return gx
 
 

@@ -164,3 +164,43 @@ def test_frontends_per_rank_ingest_world3():
         assert len({v[2] for v in seen.values()}) == 3 and len({v[1] for v in seen.values()}) == 3
     finally:
         _stop(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_frontends_on_gpu_match_the_engine(native_lib):
+    """Two front ends + the GPU owner (HIP engine, GPU JPEG): a response equals the engine's own mosaic
+    for the same image (up to the q95 JPEG round trip), through urlencoded and multipart bodies."""
+    import torch
+
+    from deconv_api_amd import ops
+    from deconv_api_amd.codec.image import decode_image, encode_jpeg, parse_result_data_url
+    from deconv_api_amd.engine.deconvnet import DeconvNet
+    from deconv_api_amd.models.vgg16 import VGG16
+
+    port = _free_port()
+    base = f"http://127.0.0.1:{port}"
+    p = _start([sys.executable, "-m", "deconv_api_amd.serve.launch"], port, 2,
+               extra_env={"DV_DEVICE": "cuda", "DV_HIP_GRAPHS": "1"})
+    try:
+        _wait_ready(base, p, 240)
+        rd = json.loads(_get(base, "/ready")[1])
+        assert rd["device"].startswith("cuda") and rd["native"] is True, rd
+        rng = np.random.default_rng(7)
+        img = rng.integers(0, 256, (224, 224, 3), dtype=np.uint8)
+        from deconv_api_amd.codec import make_data_url
+
+        url = make_data_url(img, "PNG")
+        outs = [_post(base, {"file": url, "layer": "block4_pool"}, multipart=mp) for mp in (False, True)]
+        assert all(st == 200 for st, _ in outs), outs[0][1] if outs[0][0] != 200 else outs[1][1]
+        assert outs[0][1] == outs[1][1]
+        got = parse_result_data_url(outs[0][1])
+    finally:
+        _stop(p)
+    eng = DeconvNet(VGG16.random(0).build("cuda", torch.bfloat16))  # the launcher's weights (seed 0)
+    x = torch.empty(1, 224, 224, 8, dtype=torch.bfloat16, device="cuda")
+    ops.resize_preprocess(torch.from_numpy(img).cuda()[None], x)
+    want = eng.run(x, "block4_pool").mosaic[0].cpu().numpy()
+    ref = decode_image(encode_jpeg(want, 95))
+    mse = float(((got.astype(np.float64) - ref.astype(np.float64)) ** 2).mean())
+    assert mse == 0 or 10 * np.log10(255.0 ** 2 / mse) >= 35.0, mse
