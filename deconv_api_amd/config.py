@@ -37,10 +37,10 @@ class Config:
     frontends: int = 4                    # serve/launch.py: HTTP front-end processes per rank (serve/ingest.py);
                                           #   0 = uvicorn inside the GPU process (multi-rank: rank 0 shards batches)
     jpeg_quality: int = 95                # OpenCV imencode default (app/main.py:73)
-    # request batcher. Sweep at 128 in-process clients (profiles/latency_r3_batch_sweep.txt):
-    # 16 / 2 ms 2858 req/s (p50 41 ms) vs 64 / 2 ms 1989 (p50 59 ms) - small batches keep more of
-    # them in flight through decode -> GPU -> encode; the engine still does ~5.7k img/s at B = 16
-    max_batch: int = 16
+    # request batcher. Through real HTTP with 8 front-end processes (profiles/http_load_r6.txt run d):
+    # 16 -> 4957, 32 -> 5566, 64 -> 5357 req/s (JPEG-only, 256 clients): at 16 the GPU was ~85 % busy
+    # with B = 16 batches. (Round 3, in-process clients and one GIL, preferred 16: latency_r3_batch_sweep.txt)
+    max_batch: int = 32
     batch_timeout_ms: float = 2.0
     max_queue: int = 4096                 # backpressure: 503 beyond this many pending requests
     request_timeout_s: float = 120.0
