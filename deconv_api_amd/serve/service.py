@@ -45,6 +45,10 @@ class ServiceOverloaded(RuntimeError):
     pass
 
 
+# batches above this size are trimmed to a full graph bucket (the rest waits for the next batch)
+TRIM_MIN = 16
+
+
 @dataclass
 class _Job:
     """One request in the batcher. ``deliver(value, exc)`` hands the result back: for an HTTP
@@ -110,6 +114,7 @@ class DeconvService:
 
         self.native_codec = bool(self.cfg.native_codec and _native() is not None)
         self.q: "queue.Queue[_Job]" = queue.Queue()
+        self._carry: List[_Job] = []
         self.done_q: "queue.Queue" = queue.Queue()
         self.batches = 0
         self.images = 0
@@ -194,11 +199,14 @@ class DeconvService:
 
     # ------------------------------------------------------------------ GPU worker
     def _collect(self, wait_s: float = 0.1) -> List[_Job]:
-        try:
-            first = self.q.get(timeout=wait_s) if wait_s > 0 else self.q.get_nowait()
-        except queue.Empty:
-            return []
-        jobs = [first]
+        if self._carry:  # the tail of the previous collection, trimmed to a graph bucket (below)
+            jobs, self._carry = self._carry, []
+        else:
+            try:
+                first = self.q.get(timeout=wait_s) if wait_s > 0 else self.q.get_nowait()
+            except queue.Empty:
+                return []
+            jobs = [first]
         # dynamic batching: wait for stragglers only while the GPU still has a batch in flight
         # (they would queue behind it anyway); an idle GPU starts the batch immediately
         busy = not self.done_q.empty() or self._batch_t0 is not None
@@ -217,6 +225,14 @@ class DeconvService:
                 jobs.append(self.q.get(timeout=rem))
             except queue.Empty:
                 break
+        if self.graphs is not None and len(jobs) > TRIM_MIN:
+            # a graph replays its whole batch bucket (engine/graphs.py BUCKETS): 46 images run the 64-image
+            # graph. Under load run the largest bucket that is full now and carry the rest to the next batch
+            from ..engine.graphs import BUCKETS
+
+            fit = max(b for b in BUCKETS if b <= len(jobs))
+            if fit < len(jobs):
+                jobs, self._carry = jobs[:fit], jobs[fit:]
         return jobs
 
     def _worker(self):
