@@ -38,6 +38,7 @@ from typing import Callable, Dict, Optional
 
 import numpy as np
 
+from ..codec.image import MAX_PIXELS
 from ..utils import metrics as M
 from ..utils.logging import get_logger
 
@@ -47,6 +48,7 @@ REQ = struct.Struct("<IBBHIIQI")
 RESP = struct.Struct("<IHQ")
 DECONV, STATUS, METRICS, LAYERS, DREAM = 1, 2, 3, 4, 5
 SOCK_BUF = 8 << 20
+MAX_DREAM_BODY = 256 << 20  # JSON header + data URL of one /deepdream request
 
 
 def socket_path(port: int, rank: int) -> str:
@@ -144,20 +146,26 @@ class IngestServer:
                 rid, kind, _, llen, h, w, nbytes, dec_us = REQ.unpack(_recv_exact(c, REQ.size))
                 layer = _recv_exact(c, llen).decode() if llen else ""
                 if kind == DECONV:
-                    if nbytes != h * w * 3:
-                        _recv_exact(c, nbytes)
-                        reply(rid, 400, b"pixel payload does not match its shape")
-                        continue
+                    if nbytes != h * w * 3 or h * w > MAX_PIXELS:
+                        # the front ends enforce the same cap before decoding; a frame that breaks it is not
+                        # worth draining (up to 2^64 bytes): answer and drop the connection
+                        reply(rid, 400, b"pixel payload does not match its shape or exceeds DV_MAX_PIXELS")
+                        return
                     img = np.empty((h, w, 3), np.uint8)
                     _recv_into(c, memoryview(img).cast("B"))
                     self.requests += 1
                     M.HOST_STAGE.observe(dec_us * 1e-6, stage="decode")
                     self._deconv(rid, layer, img, reply)
                 elif kind == DREAM:
+                    if nbytes > MAX_DREAM_BODY:
+                        reply(rid, 413, b"dream request too large")
+                        return
                     body = _recv_exact(c, nbytes)
                     self._dream(rid, body, reply)
                 else:
-                    _recv_exact(c, nbytes)
+                    if nbytes:  # info requests carry no payload
+                        reply(rid, 400, b"unexpected payload")
+                        return
                     reply(rid, *self._info(kind))
         except (ConnectionError, OSError, struct.error):
             pass
