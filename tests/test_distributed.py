@@ -1,4 +1,4 @@
-"""CPU multi-process (gloo, world_size 2/3) tests of the data-parallel path: weight broadcast
+"""CPU multi-process (gloo, world_size 2/3/4) tests of the data-parallel path: weight broadcast
 bit-equality, all-gather order, ragged shard padding, and sharded deconvnet == single process."""
 import os
 import socket
@@ -59,7 +59,7 @@ def _run(fn, world, *args):
     return sorted(out, key=lambda t: t[0])
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_broadcast_gather(world):
     res = _run(_worker_collectives, world)
     for rank, same, order, mx in res:
@@ -99,13 +99,16 @@ def _worker_sharded(rank, world, port, q):
         q.put((rank, traceback.format_exc(), None, None))
 
 
-def test_sharded_deconv_matches_single():
-    res = _run(_worker_sharded, 2)
-    r0, r1 = res
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_deconv_matches_single(world):
+    """5 ragged images over 2 or 4 ranks (shards 3/2 and 2/1/1/1), then a 1-image batch (empty shards)."""
+    res = _run(_worker_sharded, world)
+    r0 = res[0]
     assert r0[1] == (5, 64, 64, 3), r0
     assert r0[2] is True
     assert r0[3] == (1, 64, 64, 3)
-    assert r1[1] == 2, r1
+    for r in res[1:]:
+        assert r[1] == 2, r  # every follower served both batches
 
 
 def _worker_failover(rank, world, port, q, dead_rank):
