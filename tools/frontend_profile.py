@@ -15,7 +15,6 @@ import socket
 import subprocess
 import sys
 import tempfile
-import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
