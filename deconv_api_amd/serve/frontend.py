@@ -2,8 +2,9 @@
 
     python -m deconv_api_amd.serve.frontend --sock /tmp/dv-ingest-80-r0-123.sock --index 0
 
-Started by serve/launch.py before the GPU owner touches the GPU (so nothing is exec'd from a
-process with a GPU context); never touches the GPU itself. It runs the same FastAPI app as the
+Started (and restarted when it dies) by the rank's front-end supervisor (serve/supervisor.py), which
+serve/launch.py starts before the GPU owner touches the GPU (so no process with a GPU context starts
+another program); never touches the GPU itself. It runs the same FastAPI app as the
 single-process server (api/app.py, the reference's surface app/main.py:19-78) on a listening
 socket bound with SO_REUSEPORT to the serving port, next to every other front end of every rank
 on the node. A request is parsed and decoded here (native base64, PIL on the codec threads), its

@@ -6,9 +6,10 @@
 Rank 0 creates (or loads) the VGG16 weights and broadcasts them over RCCL; every rank builds the
 same engine on its GPU. Two serving layouts:
 
-  * ``DV_FRONTENDS=N`` (default 4): each rank starts N HTTP front-end processes (serve/frontend.py)
-    BEFORE touching its GPU, all bound to the port with SO_REUSEPORT, and serves what they decode
-    through an ``IngestServer`` (serve/ingest.py). Ranks are independent on the request path:
+  * ``DV_FRONTENDS=N`` (default 4): each rank starts a front-end supervisor (serve/supervisor.py)
+    BEFORE touching its GPU; it runs N HTTP front-end processes (serve/frontend.py, restarted when
+    one dies), all bound to the port with SO_REUSEPORT, and the rank serves what they decode through
+    an ``IngestServer`` (serve/ingest.py). Ranks are independent on the request path:
     every rank parses, decodes, batches and encodes only its own front ends' requests, so HTTP
     throughput scales with the ranks (no rank-0 decode / resize / scatter). ``/deepdream`` runs on
     the receiving rank's GPU (tiled on that GPU above ``dream_tile``).
@@ -45,18 +46,20 @@ def build_engine(cfg: Config, info: pdist.DistInfo) -> DeconvNet:
     return DeconvNet(model.build(info.device, cfg.torch_dtype(info.device)))
 
 
-def spawn_frontends(cfg: Config, path: str, n: int) -> list:
-    """Start ``n`` front-end processes for the ingest socket ``path``. Called before this process
-    initialises the GPU: the children are fresh interpreters that never open it."""
-    env = dict(os.environ, DV_HOST=cfg.host, DV_PORT=str(cfg.port))
-    return [subprocess.Popen([sys.executable, "-m", "deconv_api_amd.serve.frontend", "--sock", path,
-                              "--index", str(i)], env=env) for i in range(n)]
+def spawn_frontends(cfg: Config, path: str, n: int) -> subprocess.Popen:
+    """Start the rank's front-end supervisor (serve/supervisor.py), which starts the ``n`` front ends
+    for the ingest socket ``path`` and restarts one that dies. Called before this process initialises
+    the GPU: the children are fresh interpreters that never open it, and this process never starts
+    another program after that."""
+    return subprocess.Popen([sys.executable, "-m", "deconv_api_amd.serve.supervisor", "--sock", path, "--n", str(n),
+                             "--owner-pid", str(os.getpid())],
+                            env=dict(os.environ, DV_HOST=cfg.host, DV_PORT=str(cfg.port)))
 
 
-def serve_frontends(cfg: Config, info: pdist.DistInfo, eng: DeconvNet, path: str, fes: list,
+def serve_frontends(cfg: Config, info: pdist.DistInfo, eng: DeconvNet, path: str, sup: subprocess.Popen,
                     stop: threading.Event) -> None:
     """This rank's GPU owner: the batching service + /deepdream behind the ingest socket, until
-    ``stop`` is set or every front end has exited."""
+    ``stop`` is set or the front-end supervisor has exited (every front end down for good)."""
     from .dream_service import DreamService
     from .ingest import IngestServer
 
@@ -64,22 +67,20 @@ def serve_frontends(cfg: Config, info: pdist.DistInfo, eng: DeconvNet, path: str
     dream = DreamService(cfg)
     srv = IngestServer(path, svc, dream, rank=info.rank)
     log.info("serving through front ends", extra={"fields": {"rank": info.rank, "world": info.world,
-                                                             "frontends": len(fes), "port": cfg.port}})
+                                                             "frontends": cfg.frontends, "port": cfg.port}})
     try:
         while not stop.wait(0.5):
-            if fes and all(p.poll() is not None for p in fes):
-                log.error("every front end exited", extra={"fields": {"codes": [p.returncode for p in fes]}})
+            if sup.poll() is not None:
+                log.error("front-end supervisor exited", extra={"fields": {"code": sup.returncode}})
                 break
     finally:
         srv.close()
-        for p in fes:
-            if p.poll() is None:
-                p.terminate()
-        for p in fes:
-            try:
-                p.wait(timeout=10)
-            except subprocess.TimeoutExpired:
-                p.kill()
+        if sup.poll() is None:
+            sup.terminate()  # it terminates the front ends
+        try:
+            sup.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            sup.kill()
         svc.close()
         dream.close()
 
@@ -94,20 +95,20 @@ def main(argv=None):
     cfg = Config.from_env(**overrides)
     setup(cfg.log_json)
     stop = threading.Event()
-    fes, path = [], None
+    sup, path = None, None
     if cfg.frontends > 0:
         from .ingest import socket_path
 
         # before pdist.init(): nothing that touches the GPU has run in this process yet
         path = socket_path(cfg.port, int(os.environ.get("RANK", "0")))
-        fes = spawn_frontends(cfg, path, cfg.frontends)
+        sup = spawn_frontends(cfg, path, cfg.frontends)
         for sig in (signal.SIGTERM, signal.SIGINT):
             signal.signal(sig, lambda *_: stop.set())
     info = pdist.init()
     eng = build_engine(cfg, info)
     if cfg.frontends > 0:
         try:
-            serve_frontends(cfg, info, eng, path, fes, stop)
+            serve_frontends(cfg, info, eng, path, sup, stop)
         finally:
             if torch.distributed.is_initialized():  # ranks are independent here: no exit barrier
                 torch.distributed.destroy_process_group()

@@ -133,6 +133,45 @@ def test_frontends_serve_reference_surface():
     assert p.returncode is not None
 
 
+@pytest.mark.timeout(300)
+def test_frontend_restarted_after_it_dies():
+    """The rank's supervisor (serve/supervisor.py) starts a front end again when one is killed; the
+    service keeps answering through the survivor meanwhile and through both afterwards."""
+    port = _free_port()
+    base = f"http://127.0.0.1:{port}"
+    p = _start([sys.executable, "-m", "deconv_api_amd.serve.launch"], port, 2)
+    try:
+        _wait_ready(base, p)
+        url = _png_url(seed=5)
+        assert _post(base, {"file": url, "layer": "block1_conv1"})[0] == 200
+        pids = set()
+        for _ in range(200):  # fresh connections reach both front ends sooner or later
+            pids.add(json.loads(_get(base, "/ready")[1])["frontend"]["pid"])
+            if len(pids) == 2:
+                break
+        assert len(pids) == 2, pids
+        victim = sorted(pids)[0]
+        os.kill(victim, signal.SIGKILL)  # our own child process, by its exact pid
+        t0 = time.time()
+        conns, seen = 0, set()
+        while time.time() - t0 < 120:
+            try:
+                rd = json.loads(_get(base, "/ready")[1])
+            except OSError:
+                continue  # a connection the kernel had queued on the dead listener
+            conns = rd["ingest"]["connections"]
+            seen.add(rd["frontend"]["pid"])
+            if conns >= 3 and len(seen - {victim}) == 2:
+                break
+            time.sleep(0.2)
+        assert conns >= 3 and victim not in seen and len(seen) == 2, (conns, seen, victim)
+        for i in range(6):
+            st, out = _post(base, {"file": url, "layer": "block1_conv1"}, multipart=bool(i % 2))
+            assert st == 200 and out.startswith("data:image/webp;base64,")
+    finally:
+        _stop(p)
+
+
 @pytest.mark.timeout(420)
 def test_frontends_per_rank_ingest_world3():
     """torchrun world 3 (Gloo, CPU): every rank runs its own front end on the shared port
