@@ -134,6 +134,37 @@ def test_frontends_serve_reference_surface():
 
 
 @pytest.mark.timeout(300)
+def test_frontends_relay_deepdream():
+    """POST /deepdream through a front end runs on the owner's DreamService (CPU InceptionV3 here);
+    its 400 for an image too small for the octaves comes back unchanged."""
+    port = _free_port()
+    base = f"http://127.0.0.1:{port}"
+    p = _start([sys.executable, "-m", "deconv_api_amd.serve.launch"], port, 1)
+    try:
+        _wait_ready(base, p)
+
+        def dream(fields):
+            body = "&".join(f"{k}={quote_plus(v)}" for k, v in fields.items()).encode()
+            req = urllib.request.Request(base + "/deepdream", data=body,
+                                         headers={"Content-Type": "application/x-www-form-urlencoded"})
+            try:
+                with urllib.request.urlopen(req, timeout=240) as r:
+                    return r.status, json.loads(r.read())
+            except urllib.error.HTTPError as e:
+                return e.code, json.loads(e.read())
+
+        st, out = dream({"file": _png_url(80, 80, seed=9), "octaves": "1", "steps": "1"})
+        assert st == 200 and out.startswith("data:image/"), (st, out if st != 200 else "")
+        from deconv_api_amd.codec.image import parse_result_data_url
+
+        assert parse_result_data_url(out).shape == (80, 80, 3)
+        st, out = dream({"file": _png_url(40, 40, seed=9), "octaves": "4", "steps": "1"})
+        assert st == 400 and out["detail"], (st, out)
+    finally:
+        _stop(p)
+
+
+@pytest.mark.timeout(300)
 def test_frontend_restarted_after_it_dies():
     """The rank's supervisor (serve/supervisor.py) starts a front end again when one is killed; the
     service keeps answering through the survivor meanwhile and through both afterwards."""
