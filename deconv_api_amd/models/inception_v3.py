@@ -10,8 +10,7 @@ deepest requested layer (DeepDream's loss never reaches mixed6..mixed10).
 from __future__ import annotations
 
 import math
-import os
-from typing import Dict, Iterable, List, Optional
+from typing import Dict, Iterable, List
 
 import torch
 

@@ -12,7 +12,6 @@ On CPU the same units are plain torch functional ops (autograd), which doubles a
 from __future__ import annotations
 
 import contextlib
-import os
 from typing import Optional, Tuple
 
 import torch

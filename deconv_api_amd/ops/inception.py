@@ -29,7 +29,6 @@ the block masks gY itself. CPU tensors take the plain torch path (the oracle).
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Sequence
 
 import torch

@@ -15,7 +15,6 @@ issues the copy: behind the first MFMA-bound layers of the next step (bench.py:C
 """
 from __future__ import annotations
 
-import os
 import threading
 import time
 from typing import Dict, Sequence

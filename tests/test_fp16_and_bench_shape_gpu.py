@@ -9,7 +9,6 @@
 Reference: app/deepdream.py:441-476 (the deconvnet), app/main.py:45-78 (the route)."""
 import math
 
-import numpy as np
 import pytest
 import torch
 

@@ -7,7 +7,7 @@ import torch
 
 from deconv_api_amd import ops
 from deconv_api_amd.engine.deconvnet import DeconvNet, UnknownLayerError, visualize_all_layers
-from deconv_api_amd.models.vgg16 import VGG16, VGG16_LAYER_NAMES, vgg16_specs
+from deconv_api_amd.models.vgg16 import VGG16, VGG16_LAYER_NAMES
 from deconv_api_amd.oracle import deconv_ref, naive
 
 LAYERS = ["block1_conv1", "block1_conv2", "block1_pool", "block2_conv2", "block3_conv3", "block4_pool",
