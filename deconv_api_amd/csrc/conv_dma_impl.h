@@ -85,6 +85,9 @@ __device__ __forceinline__ void epilogue_res(const ConvArgs& a, const f32x4 (&ac
 template <int DT, int NT, int BM, int BN, int FM, int FN>
 __device__ __forceinline__ void epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
                                              int n0, int wm, int wn, int lane, int tid, bool writer = true);
+template <int DT, int NT, int BM, int BN, int FM, int FN>
+__device__ __forceinline__ void epilogue_pool_lds(const ConvArgs& a, const f32x4 (&acc)[FM][FN], uint8_t* smem, int m0,
+                                                  int n0, int wm, int wn, int lane, int tid);
 
 // DT: 16-bit storage/MFMA dtype of x, w and a 16-bit output (DT_BF16 / DT_F16, common.h)
 // MASK: backward through a ReLU: A elements are kept only where mask (same layout and pixel

@@ -1066,7 +1066,8 @@ static int persist_cfg(const ConvArgs& a, hipStream_t s) {
   // CU count queried once (keeps the launch path free of runtime queries during graph capture)
   static const int cus = [] {
     int dev = 0, n = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
     return n > 0 ? n : 256;
   }();
   const long long grid = std::min<long long>(ntiles, (long long)cus);
