@@ -274,3 +274,55 @@ def test_frontends_on_gpu_match_the_engine(native_lib):
     ref = decode_image(encode_jpeg(want, 95))
     mse = float(((got.astype(np.float64) - ref.astype(np.float64)) ** 2).mean())
     assert mse == 0 or 10 * np.log10(255.0 ** 2 / mse) >= 35.0, mse
+
+
+def test_supervisor_restart_budget(monkeypatch):
+    """supervise(): a dead front end is restarted at most RESTARTS_PER_MIN times a minute, never while the
+    owner's socket is absent, and the pass reports 'all down for good' only when nothing is alive."""
+    from deconv_api_amd.config import Config
+    from deconv_api_amd.serve import supervisor as S
+
+    class P:
+        def __init__(self, code=None):
+            self.returncode = code
+
+        def poll(self):
+            return self.returncode
+
+    spawned = []
+
+    def fake_spawn(cfg, path, i):
+        spawned.append(i)
+        return P(code=1)  # dies again at once
+
+    monkeypatch.setattr(S, "spawn_frontend", fake_spawn)
+    cfg = Config(log_json=False)
+    fes, hist = [P(), P(code=9)], {}
+    assert S.supervise(cfg, "/x", fes, hist, 0.0, can_restart=False) is True  # #0 alive, #1 not restarted
+    assert spawned == []
+    t = 1.0
+    for _ in range(S.RESTARTS_PER_MIN + 3):
+        assert S.supervise(cfg, "/x", fes, hist, t, can_restart=True) is True
+        t += 1.0
+    assert spawned == [1] * S.RESTARTS_PER_MIN  # budget spent within the minute
+    fes[0] = P(code=0)  # the survivor goes too
+    assert S.supervise(cfg, "/x", fes, hist, t, can_restart=True) is True  # #0 gets its own budget
+    assert spawned[-1] == 0
+    assert S.supervise(cfg, "/x", fes, hist, t + 61.0, can_restart=True) is True  # a minute later: #1 again
+    assert spawned[-1] in (0, 1)
+
+
+def test_supervisor_reports_all_down(monkeypatch):
+    from deconv_api_amd.config import Config
+    from deconv_api_amd.serve import supervisor as S
+
+    class P:
+        returncode = 1
+
+        def poll(self):
+            return 1
+
+    monkeypatch.setattr(S, "spawn_frontend", lambda cfg, path, i: P())
+    cfg, fes, hist = Config(log_json=False), [P(), P()], {}
+    results = [S.supervise(cfg, "/x", fes, hist, 10.0 + 0.1 * k, can_restart=True) for k in range(2 * S.RESTARTS_PER_MIN)]
+    assert results[:S.RESTARTS_PER_MIN] == [True] * S.RESTARTS_PER_MIN and results[-1] is False
