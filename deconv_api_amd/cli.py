@@ -45,10 +45,18 @@ def cmd_deconv(a, cfg) -> int:
     finally:
         svc.close()
     os.makedirs(a.out_dir, exist_ok=True)
-    for p, m in zip(a.images, mos):
+    from .runtime.staging import GpuScans
+
+    for b, p in enumerate(a.images):
+        if isinstance(mos, GpuScans):  # GPU service: the mosaics arrive JPEG-encoded on the device
+            from .codec.image import gpu_jpeg_bytes
+
+            jpeg = gpu_jpeg_bytes(mos.packed, mos.off, b, mos.H, mos.W, cfg.jpeg_quality)
+        else:
+            jpeg = encode_jpeg(np.ascontiguousarray(mos[b]), cfg.jpeg_quality)
         dst = os.path.join(a.out_dir, f"{_stem(p)}_{a.layer}.jpg")
         with open(dst, "wb") as f:
-            f.write(encode_jpeg(np.ascontiguousarray(m), cfg.jpeg_quality))
+            f.write(jpeg)
         print(dst)
     return 0
 
