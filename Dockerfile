@@ -1,6 +1,7 @@
 # MI355X (gfx950) image for the deconvnet service. The reference's image is python:3.7 + CPU
 # TensorFlow running `uvicorn main:app --port 80` (reference Dockerfile:1-15); this one builds the
-# HIP kernels in-tree and starts one process per visible GPU (rank 0 serves HTTP on port 80).
+# HIP kernels in-tree and starts one GPU-owner process per visible GPU; each rank runs DV_FRONTENDS HTTP
+# front ends on port 80 (SO_REUSEPORT, under a per-rank supervisor that restarts a dead one).
 # pinned base: ROCm 7.2 + PyTorch 2.10 (rocm7.0 wheel), Python 3.10 -- the stack this tree is tested on
 FROM rocm/pytorch:rocm7.2_ubuntu22.04_py3.10_pytorch_release_2.10.0
 
